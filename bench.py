@@ -1,0 +1,213 @@
+"""Benchmark of the combine reduction (BASELINE.json metric: "combine GB/s (device-resident
+BF16 top-k weighted reduce) at 1/2/4/8 MI355X").
+
+One step = one ElasticBuffer.combine over one synthetic batch already resident in HBM:
+8192 tokens/rank x hidden 7168 x top-8 over 256 experts (BASELINE configs 2 and 3),
+expanded layout, gating-weighted (apply_topk_weights=True), weights passed through.
+At N = 1 the combine is one fused HIP launch; at N > 1 it is phase A -> RCCL all-to-all
+over xGMI -> phase B.
+
+Algorithmic bytes per token: K*H*2 (rows read) + H*2 (row written)
++ K*4 (slot index) + K*4 (fp32 weight), with K = the token's valid top-k slots.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+(N > 1 is launched by torch.distributed.run, one process per GPU.)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def _init_dist(n_gpus: int):
+    if 'RANK' in os.environ and int(os.environ.get('WORLD_SIZE', '1')) > 1:
+        local_rank = int(os.environ.get('LOCAL_RANK', 0))
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
+    else:
+        torch.cuda.set_device(0)
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        os.environ.setdefault('MASTER_PORT', str(29500 + os.getpid() % 1000))
+        dist.init_process_group('gloo', rank=0, world_size=1)
+    return dist.get_rank(), dist.get_world_size()
+
+
+def _cpu_baseline(tokens: int, hidden: int, topk: int, min_seconds: float):
+    """PyTorch-CPU weighted sum (the reference's weighted semantics, refs/legacy) on a bounded
+    sample: `tokens` tokens x top-k x hidden, repeated for >= min_seconds."""
+    g = torch.Generator().manual_seed(0)
+    y = torch.randn((tokens, topk, hidden), generator=g).to(torch.bfloat16)
+    w = torch.rand((tokens, topk), generator=g)
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        acc = torch.zeros((tokens, hidden), dtype=torch.float32)
+        for k in range(topk):
+            acc.addcmul_(y[:, k].float(), w[:, k:k + 1])
+        out = acc.to(torch.bfloat16)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= min_seconds:
+            break
+    bytes_per = tokens * (topk * hidden * 2 + hidden * 2 + topk * 4 + topk * 4)
+    del out
+    return dict(value=round(bytes_per * reps / el / 1e9, 3), unit='GB/s', cores=torch.get_num_threads(),
+                kind='port',
+                sample=f'{reps} x ({tokens} tokens x top-{topk} x hidden {hidden}) bf16 weighted sum, '
+                       f'torch.addcmul_ fp32 loop on CPU, {el:.1f} s')
+
+
+def _pmc_traffic(workload: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_traffic.py), if any."""
+    path = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
+    try:
+        with open(path) as f:
+            data = json.load(f)
+        entry = data.get(workload)
+        return None if entry is None else float(entry['hbm_bytes_per_launch'])
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=50)
+    ap.add_argument('--warmup', type=int, default=10)
+    ap.add_argument('--tokens', type=int, default=8192)
+    ap.add_argument('--hidden', type=int, default=7168)
+    ap.add_argument('--topk', type=int, default=8)
+    ap.add_argument('--experts', type=int, default=256)
+    ap.add_argument('--plain', action='store_true', help='reference (unweighted) combine instead of weighted')
+    ap.add_argument('--cpu-seconds', type=float, default=10.0)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-loopback', action='store_true')
+    args = ap.parse_args()
+
+    rank, world = _init_dist(args.gpus)
+    from deepep_amd import ElasticBuffer
+    from deepep_amd.kernels import MODE_FUSED
+    T, H, K, E = args.tokens, args.hidden, args.topk, args.experts
+    weighted = not args.plain
+    dev = torch.device('cuda', torch.cuda.current_device())
+    torch.manual_seed(0 + rank)
+    scores = torch.rand((T, E), device=dev)
+    topk_w, topk_idx = torch.topk(scores, K, dim=-1, sorted=False)
+    topk_idx = topk_idx.to(torch.int64)
+    x = torch.randn((T, H), device=dev).to(torch.bfloat16)
+    buf = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=T, hidden=H, num_topk=K)
+    ex_x, _, ex_w, handle, _ = buf.dispatch(x, topk_idx=topk_idx, topk_weights=topk_w, num_experts=E, do_expand=True)
+    y = torch.randn(ex_x.shape, device=dev).to(torch.bfloat16)          # expert outputs, expanded layout
+    del ex_x, x
+    valid = int((topk_idx >= 0).sum().item())
+    bytes_rank = valid * H * 2 + T * H * 2 + valid * 4 + valid * 4
+
+    def step():
+        return buf.combine(y, handle, topk_weights=ex_w, apply_topk_weights=weighted)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(buf.comm_stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(buf.comm_stream)
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    comm_ms = ev0.elapsed_time(ev1) / args.steps
+    t = torch.tensor([elapsed], dtype=torch.float64)
+    if world > 1:
+        t = t.to(dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    total_bytes = torch.tensor([float(bytes_rank)], dtype=torch.float64, device=dev if world > 1 else 'cpu')
+    if world > 1:
+        dist.all_reduce(total_bytes)
+    total_bytes = float(total_bytes.item())
+    value = total_bytes * args.steps / elapsed / 1e9
+    ms_per_step = elapsed * 1e3 / args.steps
+
+    # Dominant kernel, timed alone on the comm stream (launches back to back, same arguments)
+    roofline = None
+    if world == 1:
+        plan = handle._combine_plans[('multi', 1)]
+        out = torch.empty((T, H), dtype=torch.bfloat16, device=dev)
+        out_w = torch.empty((T, K), dtype=torch.float32, device=dev)
+        kern = buf.kernels
+
+        def launch():
+            kern.combine_reduce(MODE_FUSED, y, out, T, table=plan.local_table, row_weights=ex_w if weighted else None,
+                                wtable=plan.local_table, wsrc=ex_w, out_weights=out_w, stream=buf.comm_stream)
+        for _ in range(5):
+            launch()
+        k0, k1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        k0.record(buf.comm_stream)
+        for _ in range(args.steps):
+            launch()
+        k1.record(buf.comm_stream)
+        torch.cuda.synchronize()
+        kern_us = k0.elapsed_time(k1) * 1e3 / args.steps
+        achieved = bytes_rank / (kern_us * 1e-6) / 1e9
+        workload = f'combine_fused_{"weighted" if weighted else "plain"}_t{T}_h{H}_k{K}'
+        roofline = dict(bound='hbm', achieved=round(achieved, 1), peak=HBM_PEAK_GBPS, unit='GB/s',
+                        frac=round(achieved / HBM_PEAK_GBPS, 4), traffic=_pmc_traffic(workload),
+                        kernel='combine_reduce_kernel<FUSED>', kernel_us=round(kern_us, 2),
+                        bytes_per_launch=bytes_rank, in_region_us_per_step=round(comm_ms * 1e3, 2))
+
+    loopback = None
+    if world == 1 and not args.no_loopback:
+        # Host-staged loopback (north_star): pinned host rows -> H2D -> combine -> D2H.
+        host_y = torch.empty(y.shape, dtype=y.dtype, pin_memory=True).copy_(y)
+        host_out = torch.empty((T, H), dtype=torch.bfloat16, pin_memory=True)
+        dev_y = torch.empty_like(y)
+        torch.cuda.synchronize()
+        n_lb = 3
+        t_lb = time.perf_counter()
+        for _ in range(n_lb):
+            dev_y.copy_(host_y, non_blocking=True)
+            o, _, _ = buf.combine(dev_y, handle, topk_weights=ex_w, apply_topk_weights=weighted)
+            host_out.copy_(o, non_blocking=True)
+        torch.cuda.synchronize()
+        el_lb = (time.perf_counter() - t_lb) / n_lb
+        loopback = dict(gbps=round(bytes_rank / el_lb / 1e9, 2), ms_per_batch=round(el_lb * 1e3, 2),
+                        note='algorithmic bytes / (H2D of the expanded rows + combine + D2H of the output)')
+        del host_y, host_out, dev_y
+
+    cpu_baseline = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu_baseline = _cpu_baseline(1024, H, K, args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            'metric': 'combine GB/s (device-resident BF16 top-k weighted reduce) at 1/2/4/8 MI355X',
+            'value': round(value, 2), 'unit': 'GB/s', 'n_gpus': world, 'steps': args.steps,
+            'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 4), 'higher_is_better': True,
+            'scaling': 'weak', 'vs_baseline': None, 'dtype': 'bf16 (fp32 accumulate)', 'data': 'synthetic',
+            'config': {'workload': f'EP={world} combine, {T} tokens/rank x hidden {H} x top-{K}, '
+                                   f'{E} experts, uniform routing, expanded layout, '
+                                   f'{"gating-weighted" if weighted else "plain (reference semantics)"}',
+                       'tokens_per_rank': T, 'hidden': H, 'topk': K, 'experts': E,
+                       'parallelism': f'ep{world}'},
+            'roofline': roofline, 'cpu_baseline': cpu_baseline, 'loopback': loopback,
+        }
+        print(json.dumps(line), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

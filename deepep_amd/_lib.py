@@ -1,0 +1,79 @@
+"""ctypes binding of libdeepep_amd.so (C-ABI in include/deepep_amd.h).
+
+The library is built in-tree by __graft_entry__.build() (hipcc --offload-arch=gfx950).
+There is no fallback: if the library is missing or a call fails, the error is raised
+(RuntimeError, as the reference's EP_HOST_ASSERT -> EPException does).
+"""
+import ctypes
+import os
+import threading
+from typing import Optional
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get('DEEPEP_AMD_LIB', os.path.join(_HERE, 'libdeepep_amd.so'))
+ABI_VERSION = 1
+
+MODE_LOCAL, MODE_EPILOGUE, MODE_FUSED = 0, 1, 2
+
+_lib = None
+_lock = threading.Lock()
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_I64 = ctypes.c_int64
+
+# Every symbol include/deepep_amd.h declares, with its ctypes signature.
+SIGNATURES = {
+    'deepep_amd_abi_version': (_I, []),
+    'deepep_amd_last_error': (ctypes.c_char_p, []),
+    'deepep_combine_reduce': (_I, [_I, _I,
+                                   _P, _I64, _I64,
+                                   _P, _I64, _I,
+                                   _P,
+                                   _P, _P,
+                                   _P, _I64,
+                                   _I, _I,
+                                   _P, _I64,
+                                   _P, _P, _I,
+                                   _I, _P,
+                                   _P]),
+    'deepep_build_local_plan': (_I, [_P, _I, _I, _I, _I, _P, _I, _I, _P, _P, _P]),
+    'deepep_combine_buffer_size': (_I64, [_I, _I, _I, _I, _I]),
+}
+
+
+class LibraryMissing(RuntimeError):
+    pass
+
+
+def load(path: Optional[str] = None):
+    """Load (once) and return the ctypes library; raise LibraryMissing if absent."""
+    global _lib
+    with _lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise LibraryMissing(f'deepep_amd: HIP library not found at {p}; run __graft_entry__.build()')
+        lib = ctypes.CDLL(p)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        version = lib.deepep_amd_abi_version()
+        if version != ABI_VERSION:
+            raise RuntimeError(f'deepep_amd: ABI version {version} != expected {ABI_VERSION}')
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().deepep_amd_last_error().decode(errors='replace')
+        raise RuntimeError(f'deepep_amd: {what} failed ({rc}): {msg}')
+
+
+def ptr(t) -> Optional[int]:
+    """Raw device address of a tensor (None for None)."""
+    return None if t is None else t.data_ptr()

@@ -1,0 +1,605 @@
+"""ElasticBuffer: the drop-in Python surface for DeepEP's combine path on MI355X.
+
+Mirrors deep_ep.ElasticBuffer (deep_ep/buffers/elastic.py:195-1107 in /root/reference):
+same constructor and method signatures, same argument meaning, same stream
+semantics (csrc/elastic/buffer.hpp:526-584) and the same error behaviour
+(RuntimeError on a violated host assertion).  What differs is underneath:
+
+* combine (the hot path) runs hand-written gfx950 kernels from libdeepep_amd.so:
+  EP = 1   one fused launch (local reduce + epilogue, no receive buffer);
+  EP > 1   phase A (local reduce per received token) -> one RCCL all_to_all_single
+           of the bf16 partials over xGMI -> phase B (epilogue reduce + bias).
+* dispatch (the handle producer, not the optimisation target of this build) is
+  written with torch ops and one RCCL all_to_all_single of packed token rows; it
+  produces the reference's handle layout (recv_src_metadata etc.) with the
+  deterministic receive order the combine plan relies on (handle.py).
+
+Single node only: num_scaleout_ranks == 1 (hybrid RDMA mode, Engram, PP and AGRS
+are out of scope for this build).
+"""
+import math
+import os
+from typing import List, Optional, Sequence, Tuple, Union
+
+import torch
+import torch.distributed as dist
+
+from .event import EventHandle, EventOverlap
+from .handle import CombinePlan, EPHandle, epilogue_tables, single_reduction_tables
+from .kernels import MODE_EPILOGUE, MODE_FUSED, MODE_LOCAL
+from .utils import align, ceil_div, value_or
+
+topk_idx_t = torch.int32 if int(os.environ.get('EP_NUM_TOPK_IDX_BITS', 64)) == 32 else torch.int64
+
+BUFFER_ALIGNMENT = 2 * 1024 * 1024          # symmetric::kNumAlignmentBytes (symmetric.hpp:16)
+_TOKEN_ALIGN = 32                           # ptx::kNumTMAAlignBytes (ptx.cuh:16)
+
+
+def _assert(cond: bool, msg: str = '') -> None:
+    """EP_HOST_ASSERT: the reference raises EPException, surfaced to Python as RuntimeError."""
+    if not cond:
+        raise RuntimeError(f'Assertion failed: {msg}')
+
+
+def _token_bytes(hidden_bytes: int, sf_bytes: int, num_topk: int, with_metadata: bool) -> int:
+    """TokenLayout::get_num_bytes<false> (layout.cuh:179-209)."""
+    meta = num_topk * 8 + ((1 + num_topk) * 4 if with_metadata else 0)
+    return (align(hidden_bytes, _TOKEN_ALIGN) + align(sf_bytes, _TOKEN_ALIGN) + align(meta, _TOKEN_ALIGN))
+
+
+def calculate_buffer_size(num_ranks: int, num_max_tokens_per_rank: int, hidden: int, num_topk: int,
+                          use_fp8_dispatch: bool, allow_multiple_reduction: bool) -> int:
+    """ElasticBuffer::calculate_buffer_size for one node (buffer.hpp:589-686)."""
+    _assert(num_max_tokens_per_rank > 0 and hidden > 0, 'num_max_tokens_per_rank > 0 and hidden > 0')
+    num_topk = 32 if num_topk == 0 else num_topk
+    elem = 1 if use_fp8_dispatch else 2
+    num_sf_packs = ceil_div(hidden, 32) if use_fp8_dispatch else 0
+    dispatch_bytes = num_ranks * num_max_tokens_per_rank * _token_bytes(hidden * elem, num_sf_packs * 4, num_topk, True)
+    slots = min(num_ranks, num_topk) if allow_multiple_reduction else num_topk
+    combine_bytes = slots * num_max_tokens_per_rank * _token_bytes(hidden * 2, 0, num_topk, False)
+    return align(max(dispatch_bytes, combine_bytes), BUFFER_ALIGNMENT)
+
+
+class ElasticBuffer:
+    """The elastic EP buffer (single node): dispatch produces an EPHandle, combine reduces."""
+
+    def __init__(self,
+                 group: dist.ProcessGroup,
+                 num_bytes: Optional[int] = None,
+                 num_cpu_bytes: int = 0,
+                 num_max_tokens_per_rank: int = 0,
+                 hidden: int = 0,
+                 num_topk: int = 0,
+                 use_fp8_dispatch: bool = False,
+                 deterministic: bool = False,
+                 allow_hybrid_mode: bool = True,
+                 allow_multiple_reduction: bool = True,
+                 prefer_overlap_with_compute: bool = True,
+                 sl_idx: int = 3,
+                 num_allocated_qps: int = 0,
+                 num_cpu_timeout_secs: int = 300, num_gpu_timeout_secs: int = 100,
+                 explicitly_destroy: bool = False):
+        self.group = group
+        self.rank_idx = group.rank()
+        self.num_ranks = group.size()
+        self.allow_hybrid_mode = allow_hybrid_mode
+        self.allow_multiple_reduction = allow_multiple_reduction
+        self.prefer_overlap_with_compute = prefer_overlap_with_compute
+        self.deterministic = deterministic
+        _assert(num_cpu_bytes == 0, 'CPU buffer segments (Engram storage) are not supported by this build')
+        if num_bytes is None:
+            num_bytes = calculate_buffer_size(self.num_ranks, num_max_tokens_per_rank, hidden, num_topk,
+                                              use_fp8_dispatch, allow_multiple_reduction)
+        _assert(num_bytes % BUFFER_ALIGNMENT == 0, 'num_bytes must be aligned to 2 MB')
+        if os.environ.get('EP_BUFFER_DEBUG', 0):
+            print(f'Initializing EP elastic buffer with {num_bytes} bytes at rank EP {self.rank_idx}/{self.num_ranks}')
+        self.num_bytes = num_bytes
+        self.num_max_tokens_per_rank = num_max_tokens_per_rank
+        if num_allocated_qps == 0:
+            num_allocated_qps = 17 if not allow_hybrid_mode else 65
+        self.num_allocated_qps = num_allocated_qps
+        self.num_cpu_timeout_secs = num_cpu_timeout_secs
+        self.num_gpu_timeout_secs = num_gpu_timeout_secs
+        self.explicitly_destroy = explicitly_destroy
+        # One node: every peer is reachable over xGMI (the NVLink domain of the reference)
+        self.num_scaleout_ranks, self.num_scaleup_ranks = 1, self.num_ranks
+        self.scaleout_rank_idx, self.scaleup_rank_idx = 0, self.rank_idx
+        self.num_rdma_ranks, self.num_nvlink_ranks = 1, self.num_ranks
+        self.use_cuda = torch.cuda.is_available()
+        self.device = torch.device('cuda', torch.cuda.current_device()) if self.use_cuda else torch.device('cpu')
+        self.comm_stream = torch.cuda.Stream(device=self.device) if self.use_cuda else None
+        self._kernels = None
+        self.runtime = self           # non-None while alive (the reference keeps its C++ runtime here)
+        if self.use_cuda:
+            torch.cuda.synchronize()
+        group.barrier()
+        if self.use_cuda:
+            torch.cuda.synchronize()
+
+    # ------------------------------------------------------------------ infrastructure
+    @property
+    def kernels(self):
+        if self._kernels is None:
+            from .kernels import HipKernels
+            self._kernels = HipKernels()
+        return self._kernels
+
+    def destroy(self) -> None:
+        assert self.explicitly_destroy
+        if self.runtime is not None:
+            if self.use_cuda:
+                torch.cuda.synchronize()
+            self.runtime = None
+
+    @staticmethod
+    def get_buffer_size_hint(group: dist.ProcessGroup, num_max_tokens_per_rank: int, hidden: int,
+                             num_topk: int = 0, use_fp8_dispatch: bool = False,
+                             allow_hybrid_mode: bool = True, allow_multiple_reduction: bool = True) -> int:
+        return calculate_buffer_size(group.size(), num_max_tokens_per_rank, hidden, num_topk,
+                                     use_fp8_dispatch, allow_multiple_reduction)
+
+    @staticmethod
+    def get_elastic_buffer_alignment() -> int:
+        return BUFFER_ALIGNMENT
+
+    def barrier(self, use_comm_stream: bool = True, with_cpu_sync: bool = False, sequential: bool = True) -> None:
+        if with_cpu_sync and self.use_cuda:
+            torch.cuda.synchronize()
+        if self.use_cuda and use_comm_stream:
+            with torch.cuda.stream(self.comm_stream):
+                dist.barrier(group=self.group)
+        else:
+            dist.barrier(group=self.group)
+        if with_cpu_sync and self.use_cuda:
+            torch.cuda.synchronize()
+
+    @staticmethod
+    def capture() -> EventHandle:
+        return EventHandle()
+
+    def get_comm_stream(self) -> torch.cuda.Stream:
+        return self.comm_stream
+
+    def get_physical_domain_size(self) -> Tuple[int, int]:
+        return self.num_rdma_ranks, self.num_nvlink_ranks
+
+    def get_logical_domain_size(self) -> Tuple[int, int]:
+        return self.num_scaleout_ranks, self.num_scaleup_ranks
+
+    def get_theoretical_num_sms(self, num_experts: int, num_topk: int, num_scaleout_topk: int = 0,
+                                rdma_gbs: float = 0, nvlink_gbs: float = 0,
+                                sm_read_gbs: float = 200, sm_write_gbs: float = 50) -> int:
+        """Bandwidth model of elastic.py:728-834 for one node, with xGMI in place of NVLink.
+
+        On MI355X the combine kernels size their own grids from the CU count and occupancy;
+        the value is kept in the handle for API compatibility (and is what `num_sms` means
+        to callers that pass it through)."""
+        assert num_scaleout_topk == 0
+        nvlink_gbs = nvlink_gbs or float(os.environ.get('EP_XGMI_GBS', 7 * 64))
+        num_device_sms = torch.cuda.get_device_properties(self.device).multi_processor_count if self.use_cuda else 256
+
+        def expected_topk(groups: int) -> float:
+            return groups * (1 - math.comb(num_experts - num_experts // groups, num_topk) / math.comb(num_experts, num_topk))
+
+        num_sms = num_device_sms
+        if self.num_ranks > 1:
+            e_topk = expected_topk(self.num_ranks)
+            sm_read = 1 / e_topk
+            sm_write = self.num_nvlink_ranks / self.num_ranks
+            traffic = self.num_nvlink_ranks / self.num_ranks * (1 - 1 / self.num_nvlink_ranks)
+            num_sms = max(nvlink_gbs / traffic * sm_read / sm_read_gbs, nvlink_gbs / traffic * sm_write / sm_write_gbs)
+        num_sms = align(max(4, math.ceil(num_sms * 1.25)), 2)
+        num_sms = num_sms if self.prefer_overlap_with_compute else max(num_sms, 64)
+        return min(num_sms, num_device_sms)
+
+    def get_theoretical_num_qps(self, num_sms: int) -> int:
+        num_qps = min(num_sms, 8 + 1)
+        if self.allow_hybrid_mode:
+            num_qps = num_sms * 16 + 1
+        return min(num_qps, self.num_allocated_qps)
+
+    # ------------------------------------------------------------------ streams (buffer.hpp:526-584)
+    def _prologue(self, previous_event: Optional[EventHandle], allocate_on_comm_stream: bool):
+        if not self.use_cuda:
+            return None
+        compute_stream = torch.cuda.current_stream()
+        if allocate_on_comm_stream:
+            torch.cuda.set_stream(self.comm_stream)
+        if previous_event is not None:
+            _assert(allocate_on_comm_stream, 'previous_event requires allocate_on_comm_stream')
+            previous_event.stream_wait(self.comm_stream)
+        else:
+            self.comm_stream.wait_stream(compute_stream)
+        return compute_stream
+
+    def _before_epilogue(self, previous_event_before_epilogue: Optional[EventHandle]) -> None:
+        if previous_event_before_epilogue is not None and self.use_cuda:
+            previous_event_before_epilogue.stream_wait(self.comm_stream)
+
+    def _epilogue(self, tensors: Sequence[Optional[torch.Tensor]], compute_stream,
+                  allocate_on_comm_stream: bool, async_with_compute_stream: bool) -> Optional[EventHandle]:
+        if not self.use_cuda:
+            return None
+        event = None
+        if async_with_compute_stream:
+            event = EventHandle(self.comm_stream)
+            if int(os.environ.get('EP_AVOID_RECORD_STREAM', 0)):
+                event.tensors_to_record = list(tensors)
+            else:
+                for t in tensors:
+                    if t is not None and t.is_cuda:
+                        t.record_stream(compute_stream)
+                        t.record_stream(self.comm_stream)
+        else:
+            compute_stream.wait_stream(self.comm_stream)
+        if allocate_on_comm_stream:
+            torch.cuda.set_stream(compute_stream)
+        return event
+
+    def _stream_ctx(self):
+        if self.use_cuda:
+            return torch.cuda.stream(self.comm_stream)
+        import contextlib
+        return contextlib.nullcontext()
+
+    def _a2a(self, out: torch.Tensor, inp: torch.Tensor, out_splits: Optional[List[int]] = None,
+             in_splits: Optional[List[int]] = None) -> None:
+        """all_to_all_single over the buffer's group (RCCL over xGMI on GPU, gloo on CPU).
+        A one-rank group is a plain copy.  Tests on a single device replace this method."""
+        if self.num_ranks == 1:
+            out.copy_(inp)
+            return
+        dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
+
+    def _all_to_all(self, out: torch.Tensor, inp: torch.Tensor, out_splits: List[int], in_splits: List[int]) -> None:
+        """Row all-to-all of byte views: one message per peer, any row dtype."""
+        o = out.view(torch.uint8).view(out.shape[0], out.shape[1] * out.element_size())
+        i = inp.view(torch.uint8).view(inp.shape[0], inp.shape[1] * inp.element_size())
+        self._a2a(o, i, out_splits, in_splits)
+
+    # ------------------------------------------------------------------ dispatch (handle producer)
+    def dispatch(self,
+                 x: Union[torch.Tensor, Tuple[torch.Tensor, torch.Tensor]],
+                 topk_idx: Optional[torch.Tensor] = None,
+                 topk_weights: Optional[torch.Tensor] = None,
+                 cumulative_local_expert_recv_stats: Optional[torch.Tensor] = None,
+                 num_experts: Optional[int] = None,
+                 num_max_tokens_per_rank: Optional[int] = None,
+                 expert_alignment: Optional[int] = None,
+                 num_sms: int = 0, num_qps: int = 0,
+                 previous_event: Optional[EventHandle] = None,
+                 previous_event_before_epilogue: Optional[EventHandle] = None,
+                 async_with_compute_stream: bool = False,
+                 allocate_on_comm_stream: bool = False,
+                 handle: Optional[EPHandle] = None,
+                 do_handle_copy: bool = True,
+                 do_cpu_sync: Optional[bool] = None,
+                 do_expand: bool = False,
+                 do_zero_padding: bool = False,
+                 use_tma_aligned_col_major_sf: bool = False):
+        """Dispatch tokens to the ranks owning their experts (elastic.py:855-1033 contract)."""
+        num_topk = (handle.topk_idx if topk_idx is None else topk_idx).shape[1]
+        num_sms = self.get_theoretical_num_sms(num_experts or handle.num_experts, num_topk) if num_sms == 0 else num_sms
+        num_qps = self.get_theoretical_num_qps(num_sms) if num_qps == 0 else num_qps
+        _assert(num_qps <= self.num_allocated_qps, 'Allocated QPs are not enough')
+        x, sf = x if isinstance(x, tuple) else (x, None)
+        if handle is not None:
+            _assert(topk_idx is None, 'topk_idx must be None with a cached handle')
+            _assert(do_cpu_sync is None or not do_cpu_sync, 'Cannot do CPU sync with cached handle')
+            topk_idx = handle.topk_idx
+            num_max_tokens_per_rank = value_or(num_max_tokens_per_rank, handle.num_max_tokens_per_rank)
+            num_experts = value_or(num_experts, handle.num_experts)
+            expert_alignment = value_or(expert_alignment, handle.expert_alignment)
+            do_cpu_sync = False
+            _assert((num_experts, expert_alignment, num_max_tokens_per_rank) ==
+                    (handle.num_experts, handle.expert_alignment, handle.num_max_tokens_per_rank),
+                    'cached handle context mismatch')
+            do_expand = handle.do_expand if do_expand is None else do_expand
+        num_max_tokens_per_rank = value_or(num_max_tokens_per_rank, self.num_max_tokens_per_rank)
+        expert_alignment = value_or(expert_alignment, 1)
+        do_cpu_sync = value_or(do_cpu_sync, True)
+
+        T, H = x.shape
+        R, r = self.num_ranks, self.rank_idx
+        _assert(num_experts is not None and num_experts % R == 0, 'num_experts must be divisible by the rank count')
+        _assert(topk_idx.dim() == 2 and topk_idx.shape[0] == T and topk_idx.dtype == topk_idx_t,
+                'topk_idx must be [num_tokens, num_topk] of deep_ep.topk_idx_t')
+        _assert(T <= num_max_tokens_per_rank, 'num_tokens exceeds num_max_tokens_per_rank')
+        _assert(not do_zero_padding or do_expand, 'do_zero_padding requires do_expand')
+        if topk_weights is not None:
+            _assert(topk_weights.shape == topk_idx.shape and topk_weights.dtype == torch.float32,
+                    'topk_weights must be float32 [num_tokens, num_topk]')
+        K = num_topk
+        epr = num_experts // R
+        compute_stream = self._prologue(previous_event, allocate_on_comm_stream)
+        with self._stream_ctx():
+            dev = x.device
+            # --- routing: destination ranks of every token, send order (rank, ascending token)
+            rank_of = torch.where(topk_idx >= 0, torch.div(topk_idx, epr, rounding_mode='floor'),
+                                  torch.full_like(topk_idx, -1))
+            is_to = (rank_of.unsqueeze(-1) == torch.arange(R, device=dev).view(1, 1, R)).any(dim=1)   # [T, R]
+            send_counts = is_to.sum(dim=0)
+            dst_slot = torch.where(is_to, torch.cumsum(is_to.to(torch.int64), 0) - 1,
+                                   torch.full(is_to.shape, -1, dtype=torch.int64, device=dev)).to(torch.int32)
+            pairs = is_to.t().nonzero()                                   # sorted by (dst rank, token)
+            send_tok = pairs[:, 1]
+            # --- counts exchange (host sync: all_to_all sizes are host values)
+            recv_counts_t = torch.empty_like(send_counts)
+            self._a2a(recv_counts_t, send_counts)
+            send_counts_l = [int(v) for v in send_counts.tolist()]
+            recv_counts_l = [int(v) for v in recv_counts_t.tolist()]
+            N = sum(recv_counts_l)
+            # --- one packed byte row per (token, destination): [x | sf | topk_idx | weights | src idx]
+            w = topk_weights if topk_weights is not None else torch.zeros(topk_idx.shape, dtype=torch.float32, device=dev)
+            src_global = (r * num_max_tokens_per_rank + torch.arange(T, device=dev)).to(torch.int32)
+            fields = [x.contiguous().view(torch.uint8).view(T, -1)]
+            if sf is not None:
+                fields.append(sf.contiguous().view(torch.uint8).view(T, -1))
+            fields += [topk_idx.contiguous().view(torch.uint8).view(T, -1),
+                       w.contiguous().view(torch.uint8).view(T, -1),
+                       src_global.view(torch.uint8).view(T, -1)]
+            widths = [f.shape[1] for f in fields]
+            row_bytes = sum(widths)
+            pad = (-row_bytes) % 16
+            if pad:
+                fields.append(torch.zeros((T, pad), dtype=torch.uint8, device=dev))
+            packed = torch.cat(fields, dim=1)[send_tok]
+            recv_packed = torch.empty((N, row_bytes + pad), dtype=torch.uint8, device=dev)
+            self._a2a(recv_packed, packed, recv_counts_l, send_counts_l)
+            off = 0
+            views = []
+            for wd in widths:
+                views.append(recv_packed[:, off:off + wd])
+                off += wd
+            it = iter(views)
+            recv_x = next(it).contiguous().view(x.dtype).view(N, H)
+            recv_sf = next(it).contiguous().view(sf.dtype).view(N, -1) if sf is not None else None
+            recv_idx_g = next(it).contiguous().view(topk_idx.dtype).view(N, K)
+            recv_w = next(it).contiguous().view(torch.float32).view(N, K)
+            recv_src = next(it).contiguous().view(torch.int32).view(N)
+            # --- local view of the received tokens
+            in_r = (recv_idx_g >= r * epr) & (recv_idx_g < (r + 1) * epr)
+            recv_topk_idx = torch.where(in_r, recv_idx_g - r * epr, torch.full_like(recv_idx_g, -1))
+            src_rank = torch.repeat_interleave(torch.arange(R, device=dev, dtype=torch.int32),
+                                               torch.tensor(recv_counts_l, device=dev, dtype=torch.int64))
+            lanes = torch.arange(K, device=dev, dtype=torch.int32).view(1, K)
+            master = torch.where(in_r, lanes, torch.full_like(lanes, -1)).amax(dim=1)
+            meta = torch.full((N, K + 2), -1, dtype=torch.int32, device=dev)
+            meta[:, 0] = recv_src
+            meta[:, 1] = src_rank * K + master
+            counts = torch.zeros(epr, dtype=torch.int64, device=dev)
+            if N:
+                counts.scatter_add_(0, recv_topk_idx[in_r], torch.ones_like(recv_topk_idx[in_r]))
+            counts_l = [int(v) for v in counts.tolist()]
+            aligned_l = [align(c, expert_alignment) for c in counts_l]
+            if cumulative_local_expert_recv_stats is not None:
+                cumulative_local_expert_recv_stats += counts.to(cumulative_local_expert_recv_stats.dtype)
+            num_unaligned = counts.to(torch.int32)
+            if not do_expand:
+                psum_expert = torch.tensor(aligned_l, dtype=torch.int64).cumsum(0).to(torch.int32).to(dev)
+                num_expanded = N
+                out_x, out_sf, out_idx, out_w = recv_x, recv_sf, recv_topk_idx, (recv_w if topk_weights is not None else None)
+            else:
+                starts = [0] * epr
+                for e in range(1, epr):
+                    starts[e] = starts[e - 1] + aligned_l[e - 1]
+                starts_t = torch.tensor(starts, dtype=torch.int64, device=dev)
+                psum_expert = (starts_t + counts).to(torch.int32)
+                num_expanded = sum(aligned_l)
+                # expanded rows grouped by expert, ascending received token inside an expert
+                ii, kk = in_r.nonzero(as_tuple=True)                     # row-major: ascending token
+                ee = recv_topk_idx[ii, kk]
+                order = torch.argsort(ee * max(N, 1) + ii, stable=True)
+                ii, kk, ee = ii[order], kk[order], ee[order]
+                first = torch.cumsum(counts, 0) - counts
+                rank_in_e = torch.arange(ii.numel(), device=dev) - first[ee]
+                rows = starts_t[ee] + rank_in_e
+                meta[ii, 2 + kk] = rows.to(torch.int32)
+                alloc = torch.zeros if do_zero_padding else torch.empty
+                out_x = alloc((num_expanded, H), dtype=x.dtype, device=dev)
+                out_x[rows] = recv_x[ii]
+                out_sf = None
+                if sf is not None:
+                    out_sf = alloc((num_expanded, recv_sf.shape[1]), dtype=sf.dtype, device=dev)
+                    out_sf[rows] = recv_sf[ii]
+                out_idx = None
+                out_w = None
+                if topk_weights is not None:
+                    out_w = torch.zeros((num_expanded,), dtype=torch.float32, device=dev)
+                    out_w[rows] = recv_w[ii, kk]
+            psum_rank = torch.tensor(recv_counts_l, dtype=torch.int64).cumsum(0).to(torch.int32).to(dev)
+            num_recv = N
+            if not do_cpu_sync and handle is None:
+                # Worst-case shapes, as the reference allocates without a CPU sync (buffer.hpp:1065-1070)
+                worst = num_max_tokens_per_rank * R
+                meta = torch.cat([meta, torch.full((worst - N, K + 2), -1, dtype=torch.int32, device=dev)])
+                if not do_expand:
+                    out_x = torch.cat([out_x, torch.zeros((worst - N, H), dtype=x.dtype, device=dev)])
+                    out_idx = torch.cat([out_idx, torch.full((worst - N, K), -1, dtype=out_idx.dtype, device=dev)])
+                    if out_w is not None:
+                        out_w = torch.cat([out_w, torch.zeros((worst - N, K), dtype=torch.float32, device=dev)])
+                    if out_sf is not None:
+                        out_sf = torch.cat([out_sf, torch.zeros((worst - N, out_sf.shape[1]), dtype=out_sf.dtype, device=dev)])
+                    num_expanded = worst
+                num_recv = worst
+            cloned_idx = topk_idx.clone() if do_handle_copy else topk_idx
+        self._before_epilogue(previous_event_before_epilogue)
+        event = self._epilogue([x, sf, topk_idx, topk_weights, out_x, out_sf, out_idx, out_w, meta],
+                               compute_stream, allocate_on_comm_stream, async_with_compute_stream)
+        is_cached = handle is not None
+        if not is_cached:
+            handle = EPHandle(do_expand, num_experts, expert_alignment, num_max_tokens_per_rank, num_sms,
+                              cloned_idx, num_recv, num_expanded, aligned_l, psum_rank, psum_expert,
+                              num_unaligned, meta, dst_slot, None, None)
+            handle._recv_counts = recv_counts_l
+        out_x = (out_x, out_sf) if out_sf is not None else out_x
+        return out_x, out_idx, out_w, handle, EventOverlap(event)
+
+    # ------------------------------------------------------------------ combine (the hot path)
+    @staticmethod
+    def _unpack_bias(bias) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor]]:
+        bias_0, bias_1 = None, None
+        if isinstance(bias, torch.Tensor):
+            bias_0 = bias
+        elif isinstance(bias, tuple):
+            assert len(bias) == 2
+            bias_0, bias_1 = bias
+        return bias_0, bias_1
+
+    def _plan(self, handle: EPHandle, single_reduction: bool) -> CombinePlan:
+        key = ('single' if single_reduction else 'multi', self.num_ranks)
+        plan = handle._combine_plans.get(key)
+        if plan is not None:
+            return plan
+        T, K = handle.topk_idx.shape
+        R = self.num_ranks
+        plan = CombinePlan(num_ranks=R, num_tokens=T, num_topk=K, expanded=handle.do_expand)
+        meta = handle.recv_src_metadata
+        recv_counts = handle._recv_counts
+        if recv_counts is None:     # handle built elsewhere: counts from the inclusive prefix sum
+            psum = [0] + [int(v) for v in handle.psum_num_recv_tokens_per_scaleup_rank.tolist()]
+            recv_counts = [psum[i + 1] - psum[i] for i in range(R)]
+        n_recv = sum(recv_counts)
+        plan.recv_counts = recv_counts
+        if R == 1:
+            width = K if handle.do_expand else 1
+            plan.local_table = torch.empty((T, width), dtype=torch.int32, device=meta.device)
+            if not handle.do_expand:
+                plan.local_wtable = torch.empty((T, K), dtype=torch.int32, device=meta.device)
+            self.kernels.build_local_plan(meta, n_recv, K, handle.num_max_tokens_per_rank, handle.do_expand,
+                                          plan.local_table, T, handle.topk_idx, plan.local_wtable,
+                                          stream=self.comm_stream)
+        elif single_reduction:
+            plan.table_b1, plan.back_counts1 = single_reduction_tables(handle.topk_idx, handle.num_experts, R)
+            slots = meta[:n_recv, 2:]
+            valid = slots >= 0
+            plan.send_slots1 = slots[valid].view(-1, 1).to(torch.int32).contiguous()
+            per_tok = valid.sum(dim=1)
+            bounds = [0]
+            for c in recv_counts:
+                bounds.append(bounds[-1] + c)
+            csum = torch.cat([per_tok.new_zeros(1), torch.cumsum(per_tok, 0)])
+            cs = csum[torch.tensor(bounds, device=csum.device)].tolist()
+            plan.send_counts1 = [int(cs[i + 1] - cs[i]) for i in range(R)]
+        else:
+            plan.table_b, plan.wtable_b, plan.back_counts = epilogue_tables(handle.topk_idx, handle.num_experts, R)
+        handle._combine_plans[key] = plan
+        return plan
+
+    def combine(self,
+                x: torch.Tensor,
+                handle: EPHandle,
+                topk_weights: Optional[torch.Tensor] = None,
+                bias: Union[torch.Tensor, Tuple[torch.Tensor, torch.Tensor]] = None,
+                num_sms: int = 0, num_qps: int = 0,
+                previous_event: Optional[EventHandle] = None,
+                previous_event_before_epilogue: Optional[EventHandle] = None,
+                async_with_compute_stream: bool = False,
+                allocate_on_comm_stream: bool = False,
+                *,
+                apply_topk_weights: bool = False) \
+            -> Tuple[torch.Tensor, Optional[torch.Tensor], EventOverlap]:
+        """Combine (reduce) tokens back to their source ranks (elastic.py:1046-1107 contract).
+
+        `apply_topk_weights` (extension, default False = reference semantics): scale every
+        expanded row by its top-k weight inside the reduction (the gating-weighted sum of the
+        legacy low_latency_combine, csrc/kernels/legacy/internode_ll.cu:1072-1135).  Requires
+        the expanded layout and `topk_weights`.  The weights are still passed through."""
+        num_sms = handle.num_sms if num_sms == 0 else num_sms
+        num_qps = self.get_theoretical_num_qps(num_sms) if num_qps == 0 else num_qps
+        _assert(num_qps <= self.num_allocated_qps, 'Allocated QPs are not enough')
+        bias_0, bias_1 = self._unpack_bias(bias)
+        return self._combine(x, topk_weights, bias_0, bias_1, handle, num_sms, previous_event,
+                             previous_event_before_epilogue, async_with_compute_stream,
+                             allocate_on_comm_stream, apply_topk_weights)
+
+    def _combine(self, x, topk_weights, bias_0, bias_1, handle, num_sms, previous_event,
+                 previous_event_before_epilogue, async_with_compute_stream, allocate_on_comm_stream,
+                 apply_topk_weights):
+        # ---- checks of ElasticBuffer::combine (buffer.hpp:1197-1247)
+        _assert(self.runtime is not None, 'buffer destroyed')
+        _assert(num_sms > 0, 'num_sms > 0')
+        _assert(x.dim() == 2 and x.is_contiguous() and x.dtype == torch.bfloat16, 'x must be contiguous bf16 [N, hidden]')
+        num_tokens, hidden = x.shape
+        _assert((hidden * x.element_size()) % 16 == 0, 'hidden * sizeof(bf16) must be a multiple of 16')
+        topk_idx = handle.topk_idx
+        _assert(topk_idx.dim() == 2 and topk_idx.is_contiguous() and topk_idx.dtype == topk_idx_t, 'topk_idx layout')
+        T, K = topk_idx.shape
+        psum = handle.psum_num_recv_tokens_per_scaleup_rank
+        _assert(psum.dim() == 1 and psum.shape[0] == self.num_scaleup_ranks and psum.dtype == torch.int32,
+                'psum_num_recv_tokens_per_scaleup_rank must be int32 [num_scaleup_ranks]')
+        _assert(T <= handle.num_max_tokens_per_rank, 'num_combined_tokens <= num_max_tokens_per_rank')
+        meta = handle.recv_src_metadata
+        _assert(meta.dim() == 2 and meta.shape[1] == K + 2 and meta.dtype == torch.int32 and meta.is_contiguous(),
+                'recv_src_metadata must be contiguous int32 [num_recv_tokens, num_topk + 2]')
+        expanded = handle.do_expand
+        if not expanded:
+            _assert(meta.shape[0] == num_tokens, 'non-expanded x must have one row per received token')
+        if topk_weights is not None:
+            if expanded:
+                _assert(topk_weights.dim() == 1 and topk_weights.shape[0] == num_tokens, 'expanded weights are [N]')
+            else:
+                _assert(topk_weights.dim() == 2 and tuple(topk_weights.shape) == (num_tokens, K), 'weights are [N, K]')
+            _assert(topk_weights.is_contiguous() and topk_weights.dtype == torch.float32, 'weights must be float32')
+        for b in (bias_0, bias_1):
+            if b is not None:
+                _assert(b.dim() == 2 and b.is_contiguous() and b.dtype == x.dtype and tuple(b.shape) == (T, hidden),
+                        'bias must be contiguous bf16 [num_combined_tokens, hidden]')
+        single_reduction = expanded and not self.allow_multiple_reduction
+        if single_reduction:
+            _assert(topk_weights is None, 'expanded combine without multiple reduction cannot carry top-k weights')
+        if apply_topk_weights:
+            _assert(expanded and topk_weights is not None and not single_reduction,
+                    'apply_topk_weights needs the expanded layout, topk_weights and multiple reduction')
+
+        compute_stream = self._prologue(previous_event, allocate_on_comm_stream)
+        kern = self.kernels
+        stream = self.comm_stream
+        R = self.num_ranks
+        with self._stream_ctx():
+            plan = self._plan(handle, single_reduction)
+            combined_x = torch.empty((T, hidden), dtype=x.dtype, device=x.device)
+            combined_w = torch.empty((T, K), dtype=torch.float32, device=x.device) if topk_weights is not None else None
+            row_w = topk_weights if apply_topk_weights else None
+            wsrc = topk_weights.view(-1) if topk_weights is not None else None
+            if R == 1:
+                self._before_epilogue(previous_event_before_epilogue)
+                if single_reduction:
+                    kern.combine_reduce(MODE_EPILOGUE, x, combined_x, T, table=plan.local_table,
+                                        bias0=bias_0, bias1=bias_1, stream=stream)
+                else:
+                    wtable = plan.local_table if expanded else plan.local_wtable
+                    kern.combine_reduce(MODE_FUSED, x, combined_x, T, table=plan.local_table, row_weights=row_w,
+                                        bias0=bias_0, bias1=bias_1, wtable=wtable, wsrc=wsrc,
+                                        out_weights=combined_w, stream=stream)
+            elif single_reduction:
+                n_send = sum(plan.send_counts1)
+                send = torch.empty((n_send, hidden), dtype=x.dtype, device=x.device)
+                kern.combine_reduce(MODE_LOCAL, x, send, n_send, table=plan.send_slots1, stream=stream)
+                recv = torch.empty((sum(plan.back_counts1), hidden), dtype=x.dtype, device=x.device)
+                self._all_to_all(recv, send, plan.back_counts1, plan.send_counts1)
+                self._before_epilogue(previous_event_before_epilogue)
+                kern.combine_reduce(MODE_EPILOGUE, recv, combined_x, T, table=plan.table_b1,
+                                    bias0=bias_0, bias1=bias_1, stream=stream)
+            else:
+                n_recv = sum(plan.recv_counts)
+                partial = torch.empty((n_recv, hidden), dtype=x.dtype, device=x.device)
+                partial_w = torch.empty((n_recv, K), dtype=torch.float32, device=x.device) if topk_weights is not None else None
+                table_a = meta[:n_recv, 2:] if expanded else None
+                kern.combine_reduce(MODE_LOCAL, x, partial, n_recv, table=table_a, row_weights=row_w,
+                                    wtable=table_a, wsrc=wsrc, out_weights=partial_w, stream=stream)
+                n_back = sum(plan.back_counts)
+                recv = torch.empty((n_back, hidden), dtype=x.dtype, device=x.device)
+                self._all_to_all(recv, partial, plan.back_counts, plan.recv_counts)
+                recv_w = None
+                if partial_w is not None:
+                    recv_w = torch.empty((n_back, K), dtype=torch.float32, device=x.device)
+                    self._all_to_all(recv_w, partial_w, plan.back_counts, plan.recv_counts)
+                self._before_epilogue(previous_event_before_epilogue)
+                kern.combine_reduce(MODE_EPILOGUE, recv, combined_x, T, table=plan.table_b,
+                                    bias0=bias_0, bias1=bias_1, wtable=plan.wtable_b,
+                                    wsrc=recv_w.view(-1) if recv_w is not None else None,
+                                    out_weights=combined_w, stream=stream)
+        event = self._epilogue([x, topk_weights, bias_0, bias_1, meta, topk_idx, combined_x, combined_w, psum],
+                               compute_stream, allocate_on_comm_stream, async_with_compute_stream)
+        return combined_x, combined_w, EventOverlap(event)

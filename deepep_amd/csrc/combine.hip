@@ -1,0 +1,467 @@
+// combine.hip -- the combine reduction for MI355X (gfx950, CDNA4), exported through
+// the C-ABI declared in include/deepep_amd.h.
+//
+// What is computed (semantics of the reference, /root/reference paths):
+//   DEEPEP_MODE_LOCAL    combine_impl's local reduce       deep_ep/include/deep_ep/impls/combine.cuh:114-213
+//   DEEPEP_MODE_EPILOGUE combine_reduce_epilogue_impl      deep_ep/include/deep_ep/impls/combine_reduce_epilogue.cuh:62-125
+//   arithmetic core      combine_reduce                    deep_ep/include/deep_ep/impls/combine_utils.cuh:55-170
+//   weighted variant     legacy low-latency combine        csrc/kernels/legacy/internode_ll.cu:1072-1135
+//
+// How (MI355X-first, not a translation of the TMA/warp design):
+//   * one 256-thread workgroup (4 wave64) owns a tile of `units_per_block` output rows;
+//   * the tile's slot table (and, weighted, the gating weights) is staged into LDS with one
+//     coalesced pass, compacted to the ascending list of valid slots per row, and the top-k
+//     weight pass-through is written in the same pass;
+//   * each wave then streams (row, 1-KiB-column-chunk) items: for a chunk every lane holds
+//     VPT x 16 B of each of up to 8 source rows in flight (global_load_dwordx4, non-temporal:
+//     every expanded row is read exactly once), accumulates bf16 -> fp32 in registers in the
+//     reference's order, rounds once with v_cvt_pk_bf16_f32 (RNE) and stores 16 B per lane.
+//   No MFMA: this is an HBM-bound gather + elementwise add (roofline in DESIGN.md).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdarg.h>
+
+#include <algorithm>
+
+#include "../../include/deepep_amd.h"
+
+namespace {
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kThreads = 256;
+constexpr int kWaves = kThreads / 64;
+constexpr int kMaxWidth = 32;          // top-k <= 32, as the reference (combine_reduce_epilogue.cuh:64)
+constexpr int kMaxUnitsPerBlock = 16;
+constexpr int kGroup = 8;              // source rows in flight per lane per group
+
+thread_local char g_last_error[512] = "";
+
+int set_error(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_last_error, sizeof(g_last_error), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+__device__ __forceinline__ float bf16_lo(uint32_t u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float bf16_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
+
+// Round-to-nearest-even pack of two floats (v_cvt_pk_bf16_f32), = __float22bfloat162_rn.
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+    const bf16x2 r = __builtin_convertvector((f32x2){a, b}, bf16x2);
+    return __builtin_bit_cast(uint32_t, r);
+}
+
+template <bool kNT>
+__device__ __forceinline__ u32x4 load16(const u32x4* p) {
+    if constexpr (kNT)
+        return __builtin_nontemporal_load(p);
+    else
+        return *p;
+}
+
+template <bool kNT>
+__device__ __forceinline__ void store16(u32x4* p, const u32x4& v) {
+    if constexpr (kNT)
+        __builtin_nontemporal_store(v, p);
+    else
+        *p = v;
+}
+
+struct Params {
+    const uint16_t* src;
+    int64_t num_src_rows;
+    int64_t src_stride;          // elements
+    const int32_t* table;
+    int64_t table_stride;
+    int table_width;
+    const float* row_weights;
+    const uint16_t* bias0;
+    const uint16_t* bias1;
+    uint16_t* out;
+    int64_t out_stride;          // elements
+    int num_units;
+    int hidden;
+    const int32_t* wtable;
+    int64_t wtable_stride;
+    const float* wsrc;
+    float* out_weights;
+    int num_weights;
+    int units_per_block;
+    int32_t* error_flag;
+};
+
+// acc[8*v + e] += element e of the 16-byte vector (8 bf16)
+__device__ __forceinline__ void acc_add(float* acc, const u32x4& v) {
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        acc[2 * d] += bf16_lo(v[d]);
+        acc[2 * d + 1] += bf16_hi(v[d]);
+    }
+}
+
+__device__ __forceinline__ void acc_fma(float* acc, const u32x4& v, float w) {
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        acc[2 * d] = __builtin_fmaf(bf16_lo(v[d]), w, acc[2 * d]);
+        acc[2 * d + 1] = __builtin_fmaf(bf16_hi(v[d]), w, acc[2 * d + 1]);
+    }
+}
+
+__device__ __forceinline__ u32x4 acc_pack(const float* acc) {
+    u32x4 r;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+        r[d] = pack_bf16x2(acc[2 * d], acc[2 * d + 1]);
+    return r;
+}
+
+template <int kMode, bool kWeighted, int kVPT, bool kNT>
+__global__ void __launch_bounds__(kThreads)
+combine_reduce_kernel(const Params p) {
+    __shared__ int32_t s_slot[kMaxUnitsPerBlock][kMaxWidth];
+    __shared__ float s_w[kMaxUnitsPerBlock][kMaxWidth];
+    __shared__ int32_t s_cnt[kMaxUnitsPerBlock];
+
+    const int tid = static_cast<int>(threadIdx.x);
+    const int upb = p.units_per_block;
+    const int u0 = static_cast<int>(blockIdx.x) * upb;
+    const int nu = min(upb, p.num_units - u0);
+    const int width = p.table == nullptr ? 1 : p.table_width;
+
+    // ---- stage the tile's slot table (+ gating weights) into LDS, coalesced
+    for (int e = tid; e < nu * width; e += kThreads) {
+        const int u = e / width, j = e - u * width;
+        int32_t s = p.table == nullptr ? (u0 + u)
+                                       : p.table[static_cast<int64_t>(u0 + u) * p.table_stride + j];
+        if (s >= p.num_src_rows) {                      // never dereference a bad slot
+            if (p.error_flag != nullptr) atomicOr(p.error_flag, 1);
+            s = -1;
+        }
+        s_slot[u][j] = s;
+        if constexpr (kWeighted)
+            s_w[u][j] = s >= 0 ? p.row_weights[s] : 0.0f;
+    }
+    // ---- top-k weight pass-through (combine.cuh:215-226, combine_reduce_epilogue.cuh:127-141)
+    if (p.out_weights != nullptr) {
+        for (int e = tid; e < nu * p.num_weights; e += kThreads) {
+            const int u = e / p.num_weights, k = e - u * p.num_weights;
+            const int64_t gu = u0 + u;
+            const int64_t i = p.wtable == nullptr ? gu * p.num_weights + k
+                                                  : static_cast<int64_t>(p.wtable[gu * p.wtable_stride + k]);
+            p.out_weights[gu * p.num_weights + k] = i >= 0 ? p.wsrc[i] : 0.0f;
+        }
+    }
+    __syncthreads();
+    // ---- compact to the ascending list of valid slots (compute_topk_slots, combine_utils.cuh:41-53)
+    if (tid < nu) {
+        int n = 0;
+        for (int j = 0; j < width; ++j) {
+            const int32_t s = s_slot[tid][j];
+            if (s >= 0) {
+                s_slot[tid][n] = s;                    // n <= j: in-place compaction is safe
+                if constexpr (kWeighted) s_w[tid][n] = s_w[tid][j];
+                ++n;
+            }
+        }
+        s_cnt[tid] = n;
+    }
+    __syncthreads();
+
+    // ---- stream the rows: items = (unit, column chunk of 64 lanes x kVPT x 16 B)
+    const int wave = tid >> 6, lane = tid & 63;
+    const int nvec = p.hidden >> 3;                     // 16-byte vectors per row
+    constexpr int kChunkVecs = 64 * kVPT;
+    const int nchunks = (nvec + kChunkVecs - 1) / kChunkVecs;
+    const bool has_bias0 = p.bias0 != nullptr, has_bias1 = p.bias1 != nullptr;
+    const bool has_bias = has_bias0 || has_bias1;
+
+    for (int it = wave; it < nu * nchunks; it += kWaves) {
+        const int u = it / nchunks;
+        const int c = it - u * nchunks;
+        const int n = __builtin_amdgcn_readfirstlane(s_cnt[u]);
+        const int64_t gu = u0 + u;
+        int vidx[kVPT];
+        bool vok[kVPT];
+#pragma unroll
+        for (int v = 0; v < kVPT; ++v) {
+            vidx[v] = c * kChunkVecs + v * 64 + lane;
+            vok[v] = vidx[v] < nvec;
+        }
+
+        float acc[kVPT][8];
+        u32x4 result[kVPT];
+
+        // Phase-A (or weighted) reduction over the compacted slots, ascending.
+        // Initial value: -0.0f when the reference adds the two sources in bf16 without an fp32
+        // zero in front (the hadd bypass, combine_utils.cuh:79-110: -0 + a == a exactly),
+        // +0.0f where it starts from `float2 reduced = {}` (combine_utils.cuh:114).
+        bool copy_row = false;
+        if constexpr (kMode == DEEPEP_MODE_LOCAL || kMode == DEEPEP_MODE_FUSED) {
+            copy_row = !kWeighted && n == 1;            // no_local_reduce (combine.cuh:134-156)
+            const float init = (!kWeighted && n == 2) ? -0.0f : 0.0f;
+#pragma unroll
+            for (int v = 0; v < kVPT; ++v)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) acc[v][e] = init;
+        } else {
+            // Epilogue: bias first (bias0 then bias1), then the partials; bypass without bias.
+            const float init = (!has_bias && n == 2) ? -0.0f : 0.0f;
+#pragma unroll
+            for (int v = 0; v < kVPT; ++v)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) acc[v][e] = init;
+            if (has_bias0) {
+#pragma unroll
+                for (int v = 0; v < kVPT; ++v)
+                    if (vok[v]) acc_add(acc[v], load16<kNT>(reinterpret_cast<const u32x4*>(p.bias0 + gu * p.hidden) + vidx[v]));
+            }
+            if (has_bias1) {
+#pragma unroll
+                for (int v = 0; v < kVPT; ++v)
+                    if (vok[v]) acc_add(acc[v], load16<kNT>(reinterpret_cast<const u32x4*>(p.bias1 + gu * p.hidden) + vidx[v]));
+            }
+        }
+
+        for (int g = 0; g < n; g += kGroup) {
+            u32x4 vals[kGroup][kVPT];
+#pragma unroll
+            for (int j = 0; j < kGroup; ++j) {
+                if (g + j < n) {
+                    const int32_t s = __builtin_amdgcn_readfirstlane(s_slot[u][g + j]);
+                    const u32x4* row = reinterpret_cast<const u32x4*>(p.src + static_cast<int64_t>(s) * p.src_stride);
+#pragma unroll
+                    for (int v = 0; v < kVPT; ++v)
+                        vals[j][v] = vok[v] ? load16<kNT>(row + vidx[v]) : (u32x4){0u, 0u, 0u, 0u};
+                }
+            }
+            if (copy_row) {
+#pragma unroll
+                for (int v = 0; v < kVPT; ++v) result[v] = vals[0][v];
+            } else {
+#pragma unroll
+                for (int j = 0; j < kGroup; ++j) {
+                    if (g + j < n) {
+                        if constexpr (kWeighted) {
+                            const float w = s_w[u][g + j];
+#pragma unroll
+                            for (int v = 0; v < kVPT; ++v) acc_fma(acc[v], vals[j][v], w);
+                        } else {
+#pragma unroll
+                            for (int v = 0; v < kVPT; ++v) acc_add(acc[v], vals[j][v]);
+                        }
+                    }
+                }
+            }
+        }
+        if (!copy_row) {
+#pragma unroll
+            for (int v = 0; v < kVPT; ++v) result[v] = acc_pack(acc[v]);
+        }
+
+        if constexpr (kMode == DEEPEP_MODE_FUSED) {
+            // Phase B over the single per-rank partial (EP = 1): epilogue with one slot.
+            // No bias: hadd bypass with a zero second operand -> +0 + partial.
+            // Bias: fp32 +0 + bias0 + bias1 + partial, one rounding (combine_utils.cuh:111-165).
+            const bool present = n > 0;
+#pragma unroll
+            for (int v = 0; v < kVPT; ++v) {
+                float a[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) a[e] = 0.0f;
+                if (has_bias0 && vok[v]) acc_add(a, load16<kNT>(reinterpret_cast<const u32x4*>(p.bias0 + gu * p.hidden) + vidx[v]));
+                if (has_bias1 && vok[v]) acc_add(a, load16<kNT>(reinterpret_cast<const u32x4*>(p.bias1 + gu * p.hidden) + vidx[v]));
+                if (present) acc_add(a, result[v]);
+                result[v] = acc_pack(a);
+            }
+        }
+
+        uint16_t* orow = p.out + gu * p.out_stride;
+#pragma unroll
+        for (int v = 0; v < kVPT; ++v)
+            if (vok[v]) store16<kNT>(reinterpret_cast<u32x4*>(orow) + vidx[v], result[v]);
+    }
+}
+
+template <int kMode, bool kWeighted, int kVPT>
+void launch(const Params& p, bool nt, hipStream_t stream) {
+    const dim3 grid((p.num_units + p.units_per_block - 1) / p.units_per_block);
+    if (nt)
+        hipLaunchKernelGGL((combine_reduce_kernel<kMode, kWeighted, kVPT, true>), grid, dim3(kThreads), 0, stream, p);
+    else
+        hipLaunchKernelGGL((combine_reduce_kernel<kMode, kWeighted, kVPT, false>), grid, dim3(kThreads), 0, stream, p);
+}
+
+template <int kMode, bool kWeighted>
+void launch_vpt(const Params& p, int vpt, bool nt, hipStream_t stream) {
+    if (vpt == 1) launch<kMode, kWeighted, 1>(p, nt, stream);
+    else if (vpt == 2) launch<kMode, kWeighted, 2>(p, nt, stream);
+    else launch<kMode, kWeighted, 4>(p, nt, stream);
+}
+
+bool aligned16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15u) == 0; }
+
+// ---------------------------------------------------------------- plan builder
+__global__ void fill_kernel(int32_t* dst, int64_t n, int32_t value) {
+    for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
+         i += static_cast<int64_t>(gridDim.x) * blockDim.x)
+        dst[i] = value;
+}
+
+__global__ void local_plan_kernel(const int32_t* meta, int num_recv, int num_topk, int t_max, int expanded,
+                                  int32_t* plan, int plan_width, int num_tokens,
+                                  const int64_t* topk_idx, int32_t* wtable) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= num_recv) return;
+    const int stride = num_topk + 2;
+    const int t = meta[static_cast<int64_t>(i) * stride] % t_max;
+    if (t < 0 || t >= num_tokens) return;
+    if (expanded) {
+        for (int k = 0; k < plan_width; ++k)
+            plan[static_cast<int64_t>(t) * plan_width + k] = meta[static_cast<int64_t>(i) * stride + 2 + k];
+    } else {
+        plan[static_cast<int64_t>(t) * plan_width] = i;
+    }
+    if (wtable != nullptr)
+        for (int k = 0; k < num_topk; ++k)
+            wtable[static_cast<int64_t>(t) * num_topk + k] =
+                topk_idx[static_cast<int64_t>(t) * num_topk + k] >= 0 ? i * num_topk + k : -1;
+}
+
+}  // namespace
+
+extern "C" {
+
+int deepep_amd_abi_version(void) { return DEEPEP_AMD_ABI_VERSION; }
+
+const char* deepep_amd_last_error(void) { return g_last_error; }
+
+int deepep_combine_reduce(int mode, int weighted,
+                          const void* src, int64_t num_src_rows, int64_t src_row_stride,
+                          const int32_t* table, int64_t table_stride, int table_width,
+                          const float* row_weights,
+                          const void* bias0, const void* bias1,
+                          void* out, int64_t out_row_stride,
+                          int num_units, int hidden,
+                          const int32_t* wtable, int64_t wtable_stride,
+                          const float* wsrc, float* out_weights, int num_weights,
+                          int units_per_block, int32_t* error_flag,
+                          deepep_stream_t stream) {
+    if (mode < DEEPEP_MODE_LOCAL || mode > DEEPEP_MODE_FUSED)
+        return set_error(DEEPEP_ERR_INVALID_ARG, "invalid mode %d", mode);
+    if (num_units < 0 || hidden < 0)
+        return set_error(DEEPEP_ERR_INVALID_ARG, "negative size (num_units=%d, hidden=%d)", num_units, hidden);
+    if (num_units == 0) return DEEPEP_OK;
+    if (hidden % 8 != 0)
+        return set_error(DEEPEP_ERR_INVALID_ARG, "hidden (%d) * sizeof(bf16) must be a multiple of 16 bytes", hidden);
+    if (out == nullptr || (hidden > 0 && src == nullptr && num_src_rows > 0))
+        return set_error(DEEPEP_ERR_INVALID_ARG, "null src/out");
+    if (!aligned16(src) || !aligned16(out) || !aligned16(bias0) || !aligned16(bias1))
+        return set_error(DEEPEP_ERR_INVALID_ARG, "src/out/bias must be 16-byte aligned");
+    if (src_row_stride % 8 != 0 || out_row_stride % 8 != 0 || src_row_stride < hidden || out_row_stride < hidden)
+        return set_error(DEEPEP_ERR_INVALID_ARG, "row strides must be >= hidden and multiples of 8 elements");
+    if (table != nullptr && (table_width < 1 || table_width > kMaxWidth || table_stride < table_width))
+        return set_error(DEEPEP_ERR_INVALID_ARG, "table width %d outside [1, %d] or stride too small", table_width, kMaxWidth);
+    if (weighted && (mode == DEEPEP_MODE_EPILOGUE || row_weights == nullptr))
+        return set_error(DEEPEP_ERR_INVALID_ARG, "weighted reduction needs row weights and mode LOCAL or FUSED");
+    if (mode == DEEPEP_MODE_LOCAL && (bias0 != nullptr || bias1 != nullptr))
+        return set_error(DEEPEP_ERR_INVALID_ARG, "bias is applied by the epilogue, not the local reduce");
+    if (out_weights != nullptr && (wsrc == nullptr || num_weights < 1 || num_weights > kMaxWidth))
+        return set_error(DEEPEP_ERR_INVALID_ARG, "weight pass-through needs wsrc and 1 <= num_weights <= %d", kMaxWidth);
+    if (units_per_block <= 0) units_per_block = 4;
+    if (units_per_block > kMaxUnitsPerBlock) units_per_block = kMaxUnitsPerBlock;
+
+    Params p;
+    p.src = static_cast<const uint16_t*>(src);
+    p.num_src_rows = num_src_rows;
+    p.src_stride = src_row_stride;
+    p.table = table;
+    p.table_stride = table_stride;
+    p.table_width = table_width;
+    p.row_weights = row_weights;
+    p.bias0 = static_cast<const uint16_t*>(bias0);
+    p.bias1 = static_cast<const uint16_t*>(bias1);
+    p.out = static_cast<uint16_t*>(out);
+    p.out_stride = out_row_stride;
+    p.num_units = num_units;
+    p.hidden = hidden;
+    p.wtable = wtable;
+    p.wtable_stride = wtable_stride;
+    p.wsrc = wsrc;
+    p.out_weights = out_weights;
+    p.num_weights = num_weights;
+    p.units_per_block = units_per_block;
+    p.error_flag = error_flag;
+
+    const int nvec = hidden / 8;
+    const int vpt = nvec >= 128 ? 2 : 1;
+    const bool nt = true;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (mode == DEEPEP_MODE_LOCAL) {
+        if (weighted) launch_vpt<DEEPEP_MODE_LOCAL, true>(p, vpt, nt, s);
+        else launch_vpt<DEEPEP_MODE_LOCAL, false>(p, vpt, nt, s);
+    } else if (mode == DEEPEP_MODE_EPILOGUE) {
+        launch_vpt<DEEPEP_MODE_EPILOGUE, false>(p, vpt, nt, s);
+    } else {
+        if (weighted) launch_vpt<DEEPEP_MODE_FUSED, true>(p, vpt, nt, s);
+        else launch_vpt<DEEPEP_MODE_FUSED, false>(p, vpt, nt, s);
+    }
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess)
+        return set_error(DEEPEP_ERR_HIP, "combine launch failed: %s", hipGetErrorString(err));
+    return DEEPEP_OK;
+}
+
+int deepep_build_local_plan(const int32_t* src_metadata, int num_recv_tokens, int num_topk,
+                            int num_max_tokens_per_rank, int expanded,
+                            int32_t* plan, int plan_width, int num_tokens,
+                            const int64_t* topk_idx, int32_t* wtable,
+                            deepep_stream_t stream) {
+    if (num_recv_tokens < 0 || num_tokens < 0 || num_topk < 1 || num_topk > kMaxWidth || num_max_tokens_per_rank < 1)
+        return set_error(DEEPEP_ERR_INVALID_ARG, "invalid plan sizes");
+    if (plan == nullptr || (num_recv_tokens > 0 && src_metadata == nullptr))
+        return set_error(DEEPEP_ERR_INVALID_ARG, "null plan/metadata");
+    if (plan_width != (expanded ? num_topk : 1))
+        return set_error(DEEPEP_ERR_INVALID_ARG, "plan width must be num_topk (expanded) or 1");
+    if (wtable != nullptr && topk_idx == nullptr)
+        return set_error(DEEPEP_ERR_INVALID_ARG, "wtable needs topk_idx");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const int64_t n_plan = static_cast<int64_t>(num_tokens) * plan_width;
+    if (n_plan > 0)
+        hipLaunchKernelGGL(fill_kernel, dim3(static_cast<unsigned>(std::min<int64_t>((n_plan + 255) / 256, 1024))), dim3(256), 0, s,
+                           plan, n_plan, -1);
+    if (wtable != nullptr && num_tokens > 0) {
+        const int64_t n_w = static_cast<int64_t>(num_tokens) * num_topk;
+        hipLaunchKernelGGL(fill_kernel, dim3(static_cast<unsigned>(std::min<int64_t>((n_w + 255) / 256, 1024))), dim3(256), 0, s,
+                           wtable, n_w, -1);
+    }
+    if (num_recv_tokens > 0)
+        hipLaunchKernelGGL(local_plan_kernel, dim3((num_recv_tokens + 255) / 256), dim3(256), 0, s,
+                           src_metadata, num_recv_tokens, num_topk, num_max_tokens_per_rank, expanded,
+                           plan, plan_width, num_tokens, topk_idx, wtable);
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess)
+        return set_error(DEEPEP_ERR_HIP, "plan launch failed: %s", hipGetErrorString(err));
+    return DEEPEP_OK;
+}
+
+int64_t deepep_combine_buffer_size(int num_max_tokens_per_rank, int hidden, int num_topk,
+                                   int num_ranks, int allow_multiple_reduction) {
+    // TokenLayout(hidden * 2, 0, num_topk, false) with 32-byte alignment (layout.cuh:179-209),
+    // receive slots = min(R, K) with multiple reduction else K (buffer.hpp:616-633); the
+    // xGMI fabric is load/store reachable, so no separate send buffer (is_scaleup_nvlink).
+    if (num_max_tokens_per_rank <= 0 || hidden <= 0 || num_ranks <= 0)
+        return set_error(DEEPEP_ERR_INVALID_ARG, "invalid buffer size arguments");
+    if (num_topk == 0) num_topk = 32;
+    auto align = [](int64_t x, int64_t a) { return (x + a - 1) / a * a; };
+    const int64_t token_bytes = align(int64_t(hidden) * 2, 32) + align(int64_t(num_topk) * 8, 32);
+    const int64_t slots = allow_multiple_reduction ? std::min(num_ranks, num_topk) : num_topk;
+    return slots * num_max_tokens_per_rank * token_bytes;
+}
+
+}  // extern "C"

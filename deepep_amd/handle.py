@@ -1,0 +1,145 @@
+"""EPHandle and the per-handle combine plan.
+
+EPHandle keeps the attributes of the reference's handle
+(deep_ep/buffers/elastic.py:25-98 in /root/reference) so user code that reads them
+keeps working.  What is new is `CombinePlan`: the token -> source-row tables the
+combine kernels read, derived once from the handle's routing and cached on it
+(the reference re-derives them inside every combine_reduce_epilogue_impl launch,
+combine_reduce_epilogue.cuh:62-95, by walking topk_idx and the symmetric receive
+buffer; here they are small int32 tables, 4*K bytes per token).
+
+Invariant the plan relies on for EP > 1 (guaranteed by ElasticBuffer.dispatch):
+on every expert rank the received tokens are grouped by source rank and ascending
+source token inside a rank -- the order of refs.dispatch (deep_ep/utils/refs.py:10-123)
+and of the reference's deterministic mode (elastic.py:117-131).  The source rank can
+then compute where each of its tokens' partials lands after the exchange without
+any extra communication.
+"""
+from dataclasses import dataclass
+from typing import List, Optional
+
+import torch
+
+
+@dataclass
+class CombinePlan:
+    num_ranks: int
+    num_tokens: int
+    num_topk: int
+    expanded: bool
+    # EP == 1: token-major source-row table for the fused kernel
+    local_table: Optional[torch.Tensor] = None        # [T, K] (expanded) or [T, 1] int32
+    local_wtable: Optional[torch.Tensor] = None       # [T, K] int32, non-expanded weight pass-through
+    # EP > 1, multiple reduction
+    recv_counts: Optional[List[int]] = None           # rows this rank holds per source rank (phase A output)
+    back_counts: Optional[List[int]] = None           # partial rows this rank receives per expert rank
+    table_b: Optional[torch.Tensor] = None            # [T, min(R, K)] rows of the receive buffer, master order
+    wtable_b: Optional[torch.Tensor] = None           # [T, K] row * K + k, or -1
+    # EP > 1, single reduction (allow_multiple_reduction=False, expanded): rows sent unreduced
+    send_slots1: Optional[torch.Tensor] = None        # [N_send, 1] expanded rows in send order
+    send_counts1: Optional[List[int]] = None
+    back_counts1: Optional[List[int]] = None
+    table_b1: Optional[torch.Tensor] = None           # [T, K] rows of the receive buffer per (t, k)
+
+
+def epilogue_tables(topk_idx: torch.Tensor, num_experts: int, num_ranks: int):
+    """Source-side tables for EP > 1 (multiple reduction).
+
+    For token t and expert rank r (r owns an expert of t), the partial of t computed
+    on r arrives at row offset[r] + pos_r(t) of the exchange receive buffer, where
+    pos_r(t) counts the earlier tokens routed to r.  Rows are listed in ascending
+    order of the highest top-k lane that maps to r (the dedup master lane,
+    deep_ep/include/deep_ep/common/ptx.cuh:412-421, combine_reduce_epilogue.cuh:74-95).
+    """
+    T, K = topk_idx.shape
+    R = num_ranks
+    dev = topk_idx.device
+    epr = num_experts // R
+    rank_of = torch.where(topk_idx >= 0, torch.div(topk_idx, epr, rounding_mode='floor'),
+                          torch.full_like(topk_idx, -1))
+    ranks = torch.arange(R, device=dev)
+    hit = rank_of.unsqueeze(-1) == ranks.view(1, 1, R)                 # [T, K, R]
+    is_to = hit.any(dim=1)                                              # [T, R]
+    back_counts = is_to.sum(dim=0)                                      # [R]
+    pos = torch.cumsum(is_to.to(torch.int64), dim=0) - 1
+    offsets = torch.cumsum(back_counts, dim=0) - back_counts
+    row = torch.where(is_to, offsets.view(1, R) + pos, torch.full_like(pos, -1))
+    lanes = torch.arange(K, device=dev).view(1, K, 1)
+    master = torch.where(hit, lanes, torch.full_like(lanes, -1)).amax(dim=1)      # [T, R]
+    key = torch.where(is_to, master, K + ranks.view(1, R))
+    order = torch.argsort(key, dim=1, stable=True)[:, :min(R, K)]
+    table_b = row.gather(1, order).to(torch.int32).contiguous()
+    k_idx = torch.arange(K, device=dev).view(1, K)
+    row_of_lane = row.gather(1, rank_of.clamp(min=0))
+    wtable_b = torch.where(rank_of >= 0, row_of_lane * K + k_idx, torch.full_like(row_of_lane, -1))
+    return table_b, wtable_b.to(torch.int32).contiguous(), [int(v) for v in back_counts.tolist()]
+
+
+def single_reduction_tables(topk_idx: torch.Tensor, num_experts: int, num_ranks: int):
+    """Source-side table for unreduced sends: row of (t, k) in the receive buffer.
+
+    Expert ranks send every valid (token, lane) row in (ascending token, ascending
+    lane) order per source rank, so row(t, k) = offset[r] + #{(t', k') < (t, k) on r}.
+    """
+    T, K = topk_idx.shape
+    R = num_ranks
+    dev = topk_idx.device
+    epr = num_experts // R
+    rank_of = torch.where(topk_idx >= 0, torch.div(topk_idx, epr, rounding_mode='floor'),
+                          torch.full_like(topk_idx, -1)).reshape(-1)
+    onehot = rank_of.unsqueeze(-1) == torch.arange(R, device=dev).view(1, R)    # [T*K, R]
+    counts = onehot.sum(dim=0)
+    pos = torch.cumsum(onehot.to(torch.int64), dim=0) - 1
+    offsets = torch.cumsum(counts, dim=0) - counts
+    row_all = offsets.view(1, R) + pos
+    row = torch.where(rank_of >= 0, row_all.gather(1, rank_of.clamp(min=0).view(-1, 1)).view(-1),
+                      torch.full_like(rank_of, -1))
+    return row.view(T, K).to(torch.int32).contiguous(), [int(v) for v in counts.tolist()]
+
+
+class EPHandle:
+    """Communication handle returned by `ElasticBuffer.dispatch` (same attributes as the reference)."""
+
+    def __init__(self,
+                 do_expand: bool,
+                 num_experts: int, expert_alignment: int,
+                 num_max_tokens_per_rank: int,
+                 num_sms: int,
+                 topk_idx: torch.Tensor,
+                 num_recv_tokens: int,
+                 num_expanded_tokens: int,
+                 num_recv_tokens_per_expert_list: list,
+                 psum_num_recv_tokens_per_scaleup_rank: torch.Tensor,
+                 psum_num_recv_tokens_per_expert: torch.Tensor,
+                 num_unaligned_recv_tokens_per_expert: torch.Tensor,
+                 recv_src_metadata: torch.Tensor,
+                 dst_buffer_slot_idx: torch.Tensor,
+                 token_metadata_at_forward: Optional[torch.Tensor],
+                 channel_linked_list: Optional[torch.Tensor]):
+        assert topk_idx is not None
+        self.do_expand = do_expand
+        self.num_experts = num_experts
+        self.expert_alignment = expert_alignment
+        self.num_max_tokens_per_rank = num_max_tokens_per_rank
+        self.num_sms = num_sms
+        self.topk_idx = topk_idx
+        self.psum_num_recv_tokens_per_scaleup_rank = psum_num_recv_tokens_per_scaleup_rank
+        self.psum_num_recv_tokens_per_expert = psum_num_recv_tokens_per_expert
+        self.num_unaligned_recv_tokens_per_expert = num_unaligned_recv_tokens_per_expert
+        self.num_recv_tokens_per_expert_list = num_recv_tokens_per_expert_list
+        self.recv_src_metadata = recv_src_metadata
+        self.dst_buffer_slot_idx = dst_buffer_slot_idx
+        self.token_metadata_at_forward = token_metadata_at_forward
+        self.channel_linked_list = channel_linked_list
+        self.num_recv_tokens = num_recv_tokens
+        self.num_expanded_tokens = num_expanded_tokens
+        self.cached_recv_src_metadata_before_sort = None
+        # Host-side copies captured at dispatch (counts per source rank), and the combine plan cache
+        self._recv_counts: Optional[List[int]] = None
+        self._combine_plans = {}
+
+    def deterministic_sort(self, *args, **kwargs) -> None:
+        """The dispatch of this build is deterministic by construction (received tokens sorted by
+        source global index, expanded rows by (expert, source index)), which is the order the
+        reference's deterministic_sort produces (elastic.py:100-192); nothing to do."""
+        return None

@@ -1,0 +1,109 @@
+"""Tensor-level wrappers over the C-ABI (deepep_amd/_lib.py).
+
+`HipKernels` is the only kernel provider the product uses.  It accepts torch
+tensors, checks dtypes/shapes/devices on the host (the checks of
+csrc/elastic/buffer.hpp:1200-1247 in the reference that concern the kernels), and
+passes raw device pointers plus the stream handle to libdeepep_amd.so.
+"""
+from typing import Optional
+
+import torch
+
+from . import _lib
+from ._lib import MODE_EPILOGUE, MODE_FUSED, MODE_LOCAL, ptr
+
+__all__ = ['HipKernels', 'MODE_LOCAL', 'MODE_EPILOGUE', 'MODE_FUSED']
+
+
+def _require(cond: bool, msg: str) -> None:
+    if not cond:
+        raise RuntimeError(f'deepep_amd: {msg}')
+
+
+def _stream_handle(stream) -> int:
+    return stream.cuda_stream if stream is not None else torch.cuda.current_stream().cuda_stream
+
+
+def _table_view(table: Optional[torch.Tensor]):
+    """(tensor, row stride in elements, width) of a 2-D int32 table view (rows may be strided)."""
+    if table is None:
+        return None, 0, 1
+    _require(table.dim() == 2 and table.dtype == torch.int32 and table.stride(1) == 1,
+             'slot tables must be 2-D int32 with unit column stride')
+    return table, table.stride(0), table.shape[1]
+
+
+class HipKernels:
+    """The HIP implementation of the combine primitives (gfx950)."""
+
+    name = 'hip'
+
+    def __init__(self):
+        self.lib = _lib.load()
+
+    def combine_reduce(self, mode: int, src: torch.Tensor, out: torch.Tensor, num_units: int,
+                       table: Optional[torch.Tensor] = None,
+                       row_weights: Optional[torch.Tensor] = None,
+                       bias0: Optional[torch.Tensor] = None, bias1: Optional[torch.Tensor] = None,
+                       wtable: Optional[torch.Tensor] = None, wsrc: Optional[torch.Tensor] = None,
+                       out_weights: Optional[torch.Tensor] = None,
+                       units_per_block: int = 0, error_flag: Optional[torch.Tensor] = None,
+                       stream=None) -> None:
+        _require(src.is_cuda and out.is_cuda, 'combine tensors must be on the GPU')
+        _require(src.dtype == torch.bfloat16 and out.dtype == torch.bfloat16, 'combine rows must be bfloat16')
+        _require(src.dim() == 2 and out.dim() == 2 and src.stride(1) == 1 and out.stride(1) == 1,
+                 'combine rows must be 2-D with unit column stride')
+        hidden = out.shape[1]
+        _require(src.shape[1] == hidden or src.shape[0] == 0, 'source and output hidden sizes differ')
+        _require(out.shape[0] >= num_units, 'output has fewer rows than units')
+        for b in (bias0, bias1):
+            if b is not None:
+                _require(b.is_cuda and b.dtype == torch.bfloat16 and b.is_contiguous() and
+                         tuple(b.shape) == (num_units, hidden), 'bias must be contiguous bf16 [num_tokens, hidden]')
+        t, t_stride, t_width = _table_view(table)
+        if t is not None:
+            _require(t.shape[0] >= num_units, 'slot table has fewer rows than units')
+        w, w_stride, _ = _table_view(wtable)
+        num_weights = 0
+        if out_weights is not None:
+            _require(out_weights.dtype == torch.float32 and out_weights.is_contiguous() and out_weights.dim() == 2,
+                     'weights must be contiguous float32 [units, k]')
+            num_weights = out_weights.shape[1]
+            _require(wsrc is not None and wsrc.dtype == torch.float32 and wsrc.is_contiguous(),
+                     'weight source must be contiguous float32')
+        weighted = row_weights is not None
+        if weighted:
+            _require(row_weights.dtype == torch.float32 and row_weights.is_contiguous(),
+                     'row weights must be contiguous float32')
+        rc = self.lib.deepep_combine_reduce(
+            mode, int(weighted),
+            ptr(src), src.shape[0], src.stride(0) if src.shape[0] > 0 else hidden,
+            ptr(t), t_stride, t_width,
+            ptr(row_weights),
+            ptr(bias0), ptr(bias1),
+            ptr(out), out.stride(0) if out.shape[0] > 0 else hidden,
+            num_units, hidden,
+            ptr(w), w_stride,
+            ptr(wsrc), ptr(out_weights), num_weights,
+            units_per_block, ptr(error_flag),
+            _stream_handle(stream))
+        _lib.check(rc, 'combine_reduce')
+
+    def build_local_plan(self, src_metadata: torch.Tensor, num_recv_tokens: int, num_topk: int,
+                         num_max_tokens_per_rank: int, expanded: bool, plan: torch.Tensor,
+                         num_tokens: int, topk_idx: Optional[torch.Tensor] = None,
+                         wtable: Optional[torch.Tensor] = None, stream=None) -> None:
+        _require(src_metadata.is_cuda and src_metadata.dtype == torch.int32 and src_metadata.is_contiguous(),
+                 'recv_src_metadata must be contiguous int32 on the GPU')
+        _require(plan.is_contiguous() and plan.dtype == torch.int32, 'plan must be contiguous int32')
+        rc = self.lib.deepep_build_local_plan(
+            ptr(src_metadata), num_recv_tokens, num_topk, num_max_tokens_per_rank, int(expanded),
+            ptr(plan), plan.shape[1], num_tokens, ptr(topk_idx), ptr(wtable), _stream_handle(stream))
+        _lib.check(rc, 'build_local_plan')
+
+    def combine_buffer_size(self, num_max_tokens_per_rank: int, hidden: int, num_topk: int,
+                            num_ranks: int, allow_multiple_reduction: bool) -> int:
+        v = self.lib.deepep_combine_buffer_size(num_max_tokens_per_rank, hidden, num_topk, num_ranks,
+                                                int(allow_multiple_reduction))
+        _lib.check(0 if v >= 0 else int(v), 'combine_buffer_size')
+        return int(v)

@@ -49,7 +49,9 @@ def _get_lib():
         lib.oracle_combine_phase_a.argtypes = [P, I64, I, P, I, I, I, P, I, P, P]
         lib.oracle_combine_phase_b.argtypes = [P, P, I, I, P, I, I, I, I, I, I, P, P, I, P, P]
         lib.oracle_combine_weighted_ll.argtypes = [P, P, P, I, I, I, P]
-        for f in (lib.oracle_combine_phase_a, lib.oracle_combine_phase_b, lib.oracle_combine_weighted_ll):
+        lib.oracle_combine_rows.argtypes = [I, I, P, I64, I64, P, I64, I, P, P, P, P, I64, I, I, P, I64, P, P, I]
+        for f in (lib.oracle_combine_phase_a, lib.oracle_combine_phase_b, lib.oracle_combine_weighted_ll,
+                  lib.oracle_combine_rows):
             f.restype = ctypes.c_int
         _lib = lib
     return _lib
@@ -136,6 +138,11 @@ def weighted_ll(y: np.ndarray, topk_idx: np.ndarray, w: np.ndarray) -> np.ndarra
     if rc != 0:
         raise ValueError('oracle weighted: invalid arguments')
     return out
+
+
+def rows_lib():
+    """The C library, for callers that drive oracle_combine_rows with raw host pointers."""
+    return _get_lib()
 
 
 def use_rank_layout(allow_multiple_reduction: bool, num_ranks: int, num_topk: int) -> bool:

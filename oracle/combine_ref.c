@@ -247,3 +247,58 @@ int oracle_combine_weighted_ll(const uint16_t* y, const int64_t* topk_idx, const
     }
     return 0;
 }
+
+/* --------------------------------------------------- table-driven rows
+ * The same per-row arithmetic, driven by the slot tables the product's C-ABI
+ * takes (include/deepep_amd.h, deepep_combine_reduce) instead of the
+ * reference's receive buffer.  Used by the CPU orchestration tests as a
+ * stand-in kernel provider; its semantics are the phase-A/phase-B rules above
+ * (mode 0 = phase A, 1 = phase B with width = table width, 2 = phase A then
+ * phase B over one slot).  Pointers are host pointers. */
+int oracle_combine_rows(int mode, int weighted,
+                        const uint16_t* src, int64_t num_src_rows, int64_t src_stride,
+                        const int32_t* table, int64_t table_stride, int table_width,
+                        const float* row_weights,
+                        const uint16_t* bias0, const uint16_t* bias1,
+                        uint16_t* out, int64_t out_stride, int num_units, int hidden,
+                        const int32_t* wtable, int64_t wtable_stride,
+                        const float* wsrc, float* out_weights, int num_weights) {
+    const uint16_t* rows[64];
+    float w[64];
+    uint16_t partial[65536];
+    if (table_width > 64 || hidden > 65536) return -1;
+    const int width = table ? table_width : 1;
+    for (int u = 0; u < num_units; ++u) {
+        int n = 0;
+        for (int j = 0; j < width; ++j) {
+            const int64_t s = table ? table[(int64_t)u * table_stride + j] : u;
+            if (s < 0) continue;
+            if (s >= num_src_rows) return -1;
+            rows[n] = src + s * src_stride;
+            w[n] = weighted ? row_weights[s] : 0.0f;
+            ++n;
+        }
+        uint16_t* dst = out + (int64_t)u * out_stride;
+        const uint16_t* b0 = bias0 ? bias0 + (int64_t)u * hidden : NULL;
+        const uint16_t* b1 = bias1 ? bias1 + (int64_t)u * hidden : NULL;
+        if (mode == 1) {
+            combine_reduce_row(rows, n, width, b0, b1, hidden, dst);
+        } else {
+            uint16_t* a = mode == 2 ? partial : dst;
+            if (weighted) weighted_reduce_row(rows, w, n, hidden, a);
+            else if (n == 1) memcpy(a, rows[0], (size_t)hidden * 2);
+            else combine_reduce_row(rows, n, width, NULL, NULL, hidden, a);
+            if (mode == 2) {
+                const uint16_t* one[1] = {partial};
+                combine_reduce_row(one, n > 0 ? 1 : 0, 1, b0, b1, hidden, dst);
+            }
+        }
+        if (out_weights) {
+            for (int k = 0; k < num_weights; ++k) {
+                const int64_t i = wtable ? wtable[(int64_t)u * wtable_stride + k] : (int64_t)u * num_weights + k;
+                out_weights[(int64_t)u * num_weights + k] = i >= 0 ? wsrc[i] : 0.0f;
+            }
+        }
+    }
+    return 0;
+}

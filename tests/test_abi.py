@@ -1,0 +1,79 @@
+"""CPU checks of the C-ABI boundary: the in-tree library loads, exports every function
+include/deepep_amd.h declares with the ABI version the host layer expects, and rejects
+invalid arguments with an error code and message before touching the GPU."""
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_functions():
+    text = open(os.path.join(ROOT, 'include', 'deepep_amd.h')).read()
+    text = re.sub(r'/\*.*?\*/', '', text, flags=re.S)
+    return sorted(set(re.findall(r'\b(deepep_\w+)\s*\(', text)))
+
+
+@pytest.fixture(scope='module')
+def lib():
+    import __graft_entry__
+    __graft_entry__.build()
+    from deepep_amd import _lib
+    return _lib.load()
+
+
+def test_exports_every_declared_symbol(lib):
+    from deepep_amd import _lib
+    declared = _declared_functions()
+    assert declared, 'no declarations parsed'
+    for name in declared:
+        assert hasattr(lib, name), f'{name} not exported'
+    assert sorted(_lib.SIGNATURES) == declared
+
+
+def test_abi_version(lib):
+    assert lib.deepep_amd_abi_version() == 1
+
+
+def test_invalid_arguments_are_rejected_without_a_gpu(lib):
+    # mode out of range
+    rc = lib.deepep_combine_reduce(7, 0, None, 0, 8, None, 0, 1, None, None, None, 16, 8, 1, 8,
+                                   None, 0, None, None, 0, 0, None, None)
+    assert rc == -1 and b'mode' in lib.deepep_amd_last_error()
+    # hidden not a multiple of 8 elements
+    rc = lib.deepep_combine_reduce(1, 0, 16, 1, 8, None, 0, 1, None, None, None, 16, 8, 1, 6,
+                                   None, 0, None, None, 0, 0, None, None)
+    assert rc == -1 and b'hidden' in lib.deepep_amd_last_error()
+    # misaligned pointers
+    rc = lib.deepep_combine_reduce(1, 0, 18, 1, 8, None, 0, 1, None, None, None, 32, 8, 1, 8,
+                                   None, 0, None, None, 0, 0, None, None)
+    assert rc == -1 and b'aligned' in lib.deepep_amd_last_error()
+    # bias in the local phase
+    rc = lib.deepep_combine_reduce(0, 0, 16, 1, 8, None, 0, 1, None, 32, None, 48, 8, 1, 8,
+                                   None, 0, None, None, 0, 0, None, None)
+    assert rc == -1 and b'bias' in lib.deepep_amd_last_error()
+    # table width beyond top-32
+    rc = lib.deepep_combine_reduce(1, 0, 16, 1, 8, 64, 40, 33, None, None, None, 48, 8, 1, 8,
+                                   None, 0, None, None, 0, 0, None, None)
+    assert rc == -1
+    # zero units: nothing to do, success without a launch
+    assert lib.deepep_combine_reduce(1, 0, 16, 1, 8, None, 0, 1, None, None, None, 48, 8, 0, 8,
+                                     None, 0, None, None, 0, 0, None, None) == 0
+
+
+def test_buffer_size_matches_reference_formula(lib):
+    from deepep_amd.buffer import calculate_buffer_size
+    # ElasticBuffer::get_combine_buffer_size, one node: min(R, K) slots x T x (align(2H, 32) + align(8K, 32))
+    assert lib.deepep_combine_buffer_size(4096, 7168, 8, 8, 1) == 8 * 4096 * (14336 + 64)
+    assert lib.deepep_combine_buffer_size(128, 1024, 2, 8, 1) == 2 * 128 * (2048 + 32)
+    assert lib.deepep_combine_buffer_size(128, 1024, 2, 1, 0) == 2 * 128 * (2048 + 32)
+    assert lib.deepep_combine_buffer_size(0, 7168, 8, 8, 1) < 0
+    size = calculate_buffer_size(8, 4096, 7168, 8, False, True)
+    assert size % (2 << 20) == 0 and size >= lib.deepep_combine_buffer_size(4096, 7168, 8, 8, 1)
+
+
+def test_product_fails_loudly_without_library(tmp_path, monkeypatch):
+    from deepep_amd import _lib
+    with pytest.raises(_lib.LibraryMissing):
+        _lib.load(str(tmp_path / 'missing.so'))

@@ -1,0 +1,156 @@
+"""The ElasticBuffer host orchestration on CPU, across 1, 2, 4 and 8 gloo ranks.
+
+Dispatch (handle producer), combine planning, the all-to-all exchange and the
+stream-free bookkeeping run exactly as on the GPU; the row kernels are the
+oracle's (tests/oracle_kernels.py, injected).  Expected outputs are the reference
+oracle's golden fixtures (bitwise), mirroring tests/elastic/test_ep.py:185-231 and
+:502-511 in the reference: combine of the caller-pre-reduced non-expanded input,
+"reduced" (expanded) combine, bias 0/1/2, weight pass-through, and the
+allow_multiple_reduction=False variant.
+"""
+import os
+import socket
+import traceback
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from tests.helpers import load, ordered_accumulate, ranks_of
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def _u16_to_bf16(a: np.ndarray) -> torch.Tensor:
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.int16)).view(torch.bfloat16)
+
+
+def _bf16_to_u16(t: torch.Tensor) -> np.ndarray:
+    return t.contiguous().view(torch.int16).numpy().view(np.uint16)
+
+
+def _worker(rank, world, port, fixture, queue):
+    import sys
+    sys.path.insert(0, ROOT)
+    try:
+        os.environ['MASTER_ADDR'] = '127.0.0.1'
+        os.environ['MASTER_PORT'] = str(port)
+        dist.init_process_group('gloo', rank=rank, world_size=world)
+        from deepep_amd import ElasticBuffer
+        from tests.oracle_kernels import OracleKernels
+        fx = load(fixture)
+        T, H, K, E, R = (int(v) for v in fx['meta'])
+        assert R == world
+        ranks = ranks_of(fx)
+        me = ranks[rank]
+        topk_idx = torch.from_numpy(me['topk_idx'].copy())
+        topk_w = torch.from_numpy(me['topk_weights'].copy())
+        x = (_u16_to_bf16(me['x']) if 'x' in me else
+             torch.randn((T, H), generator=torch.Generator().manual_seed(rank)).to(torch.bfloat16))
+        biases = [_u16_to_bf16(me['bias0']), _u16_to_bf16(me['bias1'])]
+        failures = []
+
+        def y_of(g: int) -> np.ndarray:
+            s, t = divmod(int(g), T)
+            return ranks[s]['y'][t]
+
+        for amr in (True, False):
+            buf = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=T, hidden=H, num_topk=K,
+                                allow_multiple_reduction=amr, explicitly_destroy=True)
+            buf._kernels = OracleKernels()
+            # ---- non-expanded dispatch + combine (test_ep.py:143-149, 185-217)
+            recv_x, recv_idx, recv_w, handle, _ = buf.dispatch(x, topk_idx=topk_idx, topk_weights=topk_w,
+                                                               num_experts=E, num_max_tokens_per_rank=T)
+            n = handle.num_recv_tokens
+            src = handle.recv_src_metadata[:n, 0].numpy()
+            if 'dispatch_recv_src_token_idx' in me:
+                if not np.array_equal(src, me['dispatch_recv_src_token_idx']):
+                    failures.append('dispatch order != refs.dispatch')
+                if not np.array_equal(recv_idx.numpy(), me['dispatch_recv_topk_idx']):
+                    failures.append('recv_topk_idx != refs.dispatch')
+                if not np.array_equal(_bf16_to_u16(recv_x), me['dispatch_recv_x']):
+                    failures.append('recv_x != refs.dispatch')
+            local = np.stack([y_of(g) for g in src]) if n else np.zeros((0, K, H), np.uint16)
+            local = np.where((recv_idx.numpy() == -1)[..., None], np.uint16(0), local)
+            x_red = _u16_to_bf16(ordered_accumulate(local)) if n else torch.empty((0, H), dtype=torch.bfloat16)
+            # ---- expanded dispatch + "reduced" combine input (test_ep.py:151-206)
+            ex_x, ex_idx, ex_w, ex_handle, _ = buf.dispatch(x, topk_idx=topk_idx, topk_weights=topk_w,
+                                                            num_experts=E, num_max_tokens_per_rank=T,
+                                                            do_expand=True)
+            assert ex_idx is None
+            meta = ex_handle.recv_src_metadata.numpy()
+            x_exp = np.full((ex_x.shape[0], H), 0x7fc1, dtype=np.uint16)
+            for i in range(meta.shape[0]):
+                y = y_of(meta[i, 0])
+                for k in range(K):
+                    if meta[i, 2 + k] >= 0:
+                        x_exp[meta[i, 2 + k]] = y[k]
+            x_exp = _u16_to_bf16(x_exp)
+            for nb in (0, 1, 2):
+                bias = None if nb == 0 else (biases[0] if nb == 1 else (biases[0], biases[1]))
+                if amr:
+                    out, out_w, _ = buf.combine(x_red, handle, topk_weights=recv_w, bias=bias)
+                    if not np.array_equal(_bf16_to_u16(out), me[f'combined_multi_b{nb}']):
+                        failures.append(f'non-expanded combine b{nb}')
+                    if not torch.equal(out_w, topk_w):
+                        failures.append(f'non-expanded weights b{nb}')
+                    out, out_w, _ = buf.combine(x_exp, ex_handle, topk_weights=ex_w, bias=bias)
+                    if not np.array_equal(_bf16_to_u16(out), me[f'combined_multi_b{nb}']):
+                        failures.append(f'expanded combine b{nb}')
+                    if not torch.equal(out_w, topk_w):
+                        failures.append(f'expanded weights b{nb}')
+                else:
+                    out, out_w, _ = buf.combine(x_exp, ex_handle, bias=bias)
+                    if not np.array_equal(_bf16_to_u16(out), me[f'combined_single_b{nb}']):
+                        failures.append(f'single-reduction expanded combine b{nb}')
+                    assert out_w is None
+                    out, _, _ = buf.combine(x_red, handle, topk_weights=recv_w, bias=bias)
+                    if not np.array_equal(_bf16_to_u16(out), me[f'combined_multi_b{nb}']):
+                        failures.append(f'single-reduction non-expanded combine b{nb}')
+            buf.destroy()
+        queue.put((rank, failures))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:
+        queue.put((rank, [traceback.format_exc()]))
+
+
+def _spawn(fixture, world):
+    ctx = mp.get_context('spawn')
+    queue = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, fixture, queue)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = {}
+    try:
+        for _ in range(world):
+            rank, failures = queue.get(timeout=240)
+            results[rank] = failures
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    return results
+
+
+@pytest.mark.parametrize('fixture,world', [
+    ('f1_ep1_t128_h1024_k2.npz', 1),
+    ('f4_ep4_t96_h256_k2.npz', 4),
+    ('f2_ep8_t64_h256_k8.npz', 8),
+    ('f3_ep8_skew_t128_h64_k8.npz', 8),
+])
+def test_elastic_buffer_matches_golden(fixture, world):
+    results = _spawn(fixture, world)
+    assert len(results) == world
+    bad = {r: f for r, f in results.items() if f}
+    assert not bad, bad

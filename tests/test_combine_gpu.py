@@ -1,0 +1,295 @@
+"""GPU parity tests: the HIP kernels (through the C-ABI) against the oracle, bitwise.
+
+* kernel level: every reduction mode, weighted/unweighted, bias 0/1/2, slot-table widths
+  1..32, ragged hidden sizes (tail lanes), empty tables, -0/inf edge values;
+* ElasticBuffer level on one GPU: the golden fixtures of the reference oracle at EP = 1
+  (BASELINE config 1) and, with 4 or 8 ranks simulated by threads on the one device
+  (the all-to-all replaced by device copies), at EP = 4 and EP = 8 (incl. skewed routing);
+* BASELINE config 2 at full size (8192 tokens x 7168 x top-8): full output bitwise vs the
+  oracle, plain and gating-weighted.
+Tolerance: bitwise for everything (bf16 outputs and the fp32 weight pass-through).
+"""
+import os
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from tests.helpers import load, ordered_accumulate, ranks_of
+from tests.oracle_kernels import OracleKernels
+
+pytestmark = pytest.mark.gpu
+
+MODE_LOCAL, MODE_EPILOGUE, MODE_FUSED = 0, 1, 2
+
+
+def _u16(t: torch.Tensor) -> np.ndarray:
+    return t.detach().cpu().contiguous().view(torch.int16).numpy().view(np.uint16)
+
+
+def _bf16(a: np.ndarray, device='cuda') -> torch.Tensor:
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.int16)).view(torch.bfloat16).to(device)
+
+
+@pytest.fixture(scope='module')
+def kern():
+    from deepep_amd.kernels import HipKernels
+    assert torch.cuda.is_available()
+    return HipKernels()
+
+
+def _random_rows(rng, n, h, special=False):
+    a = rng.standard_normal((n, h)).astype(np.float32) * rng.choice([1e-3, 1.0, 300.0], size=(n, 1)).astype(np.float32)
+    u = oracle.f32_to_bf16(a)
+    if special:
+        m = rng.random((n, h))
+        u[m < 0.05] = 0x8000        # -0
+        u[(m >= 0.05) & (m < 0.10)] = 0x0000
+        u[(m >= 0.10) & (m < 0.11)] = 0x7f80   # +inf
+        u[(m >= 0.11) & (m < 0.12)] = 0x0001   # denormal
+    return u
+
+
+def _run(kern, mode, weighted, units, width, hidden, nb, seed, identity=False, special=False, upb=0, wt=True):
+    rng = np.random.default_rng(seed)
+    nsrc = units * max(width, 1) + 3
+    src = _random_rows(rng, nsrc, hidden, special)
+    if identity:
+        table = None
+    else:
+        table = rng.integers(0, nsrc, size=(units, width)).astype(np.int32)
+        table[rng.random((units, width)) < 0.3] = -1
+        if units > 2:
+            table[0] = -1                         # a row with no valid source
+            table[1, 1:] = -1                     # exactly one
+    row_w = rng.random(nsrc).astype(np.float32) if weighted else None
+    b = [_random_rows(rng, units, hidden, special) for _ in range(2)]
+    bias0 = b[0] if nb >= 1 else None
+    bias1 = b[1] if nb >= 2 else None
+    K = 4
+    wtable = rng.integers(-1, units * K, size=(units, K)).astype(np.int32) if wt else None
+    wsrc = rng.random(units * K).astype(np.float32)
+    # GPU through the C-ABI
+    g = dict(src=_bf16(src), out=torch.empty((units, hidden), dtype=torch.bfloat16, device='cuda'),
+             table=None if table is None else torch.from_numpy(table).cuda(),
+             row_weights=None if row_w is None else torch.from_numpy(row_w).cuda(),
+             bias0=None if bias0 is None else _bf16(bias0), bias1=None if bias1 is None else _bf16(bias1),
+             wtable=None if wtable is None else torch.from_numpy(wtable).cuda(),
+             wsrc=torch.from_numpy(wsrc).cuda(), out_weights=torch.empty((units, K), device='cuda'))
+    err = torch.zeros(1, dtype=torch.int32, device='cuda')
+    kern.combine_reduce(mode, g['src'], g['out'], units, table=g['table'], row_weights=g['row_weights'],
+                        bias0=g['bias0'], bias1=g['bias1'], wtable=g['wtable'], wsrc=g['wsrc'],
+                        out_weights=g['out_weights'], units_per_block=upb, error_flag=err)
+    torch.cuda.synchronize()
+    # oracle on the host
+    c = {k: (v.cpu() if isinstance(v, torch.Tensor) else v) for k, v in g.items()}
+    c['out'] = torch.empty((units, hidden), dtype=torch.bfloat16)
+    c['out_weights'] = torch.empty((units, K))
+    OracleKernels().combine_reduce(mode, c['src'], c['out'], units, table=c['table'], row_weights=c['row_weights'],
+                                   bias0=c['bias0'], bias1=c['bias1'], wtable=c['wtable'], wsrc=c['wsrc'],
+                                   out_weights=c['out_weights'])
+    assert int(err.item()) == 0
+    got, exp = _u16(g['out']), _u16(c['out'])
+    if not np.array_equal(got, exp):
+        bad = np.argwhere(got != exp)[:5]
+        raise AssertionError(f'mismatch at {bad.tolist()}: got {[hex(got[tuple(i)]) for i in bad]} '
+                             f'expected {[hex(exp[tuple(i)]) for i in bad]}')
+    assert torch.equal(g['out_weights'].cpu(), c['out_weights'])
+
+
+@pytest.mark.parametrize('mode', [MODE_LOCAL, MODE_EPILOGUE, MODE_FUSED])
+@pytest.mark.parametrize('width', [1, 2, 3, 8, 17, 32])
+@pytest.mark.parametrize('hidden', [64, 520, 7168])
+def test_kernel_modes_widths(kern, mode, width, hidden):
+    nbs = [0] if mode == MODE_LOCAL else [0, 1, 2]
+    for nb in nbs:
+        _run(kern, mode, False, 37, width, hidden, nb, seed=width * 100 + nb)
+        if mode != MODE_EPILOGUE:
+            _run(kern, mode, True, 37, width, hidden, nb, seed=width * 100 + nb + 7)
+
+
+@pytest.mark.parametrize('mode', [MODE_LOCAL, MODE_EPILOGUE, MODE_FUSED])
+def test_kernel_identity_table_and_special_values(kern, mode):
+    for nb in ([0] if mode == MODE_LOCAL else [0, 1, 2]):
+        _run(kern, mode, False, 19, 1, 1024, nb, seed=5 + nb, identity=True, special=True)
+        _run(kern, mode, False, 19, 8, 1024, nb, seed=9 + nb, special=True)
+
+
+@pytest.mark.parametrize('upb', [1, 3, 4, 16])
+def test_kernel_units_per_block(kern, upb):
+    _run(kern, MODE_FUSED, False, 53, 8, 7168, 1, seed=upb, upb=upb)
+    _run(kern, MODE_LOCAL, True, 53, 8, 7168, 0, seed=upb + 1, upb=upb, wt=False)
+
+
+def test_kernel_empty_and_errors(kern):
+    src = torch.zeros((4, 64), dtype=torch.bfloat16, device='cuda')
+    out = torch.empty((0, 64), dtype=torch.bfloat16, device='cuda')
+    kern.combine_reduce(MODE_FUSED, src, out, 0)                    # no units: no launch, no error
+    err = torch.zeros(1, dtype=torch.int32, device='cuda')
+    out = torch.empty((1, 64), dtype=torch.bfloat16, device='cuda')
+    table = torch.tensor([[0, 99]], dtype=torch.int32, device='cuda')   # 99 >= num_src_rows
+    kern.combine_reduce(MODE_EPILOGUE, src, out, 1, table=table, error_flag=err)
+    torch.cuda.synchronize()
+    assert err.item() == 1
+    with pytest.raises(RuntimeError):
+        kern.combine_reduce(MODE_LOCAL, src, out, 1, table=table, bias0=out)    # bias in phase A
+    with pytest.raises(RuntimeError):
+        kern.combine_reduce(MODE_EPILOGUE, src[:, :60], out[:, :60], 1)          # hidden % 8 != 0
+
+
+# ----------------------------------------------------------------------------- ElasticBuffer level
+
+class _ThreadComm:
+    """all_to_all_single among threads that each drive one simulated rank on the same GPU."""
+
+    def __init__(self, n):
+        self.n = n
+        self.bar = threading.Barrier(n)
+        self.slots = [None] * n
+
+    def a2a(self, rank, out, inp, out_splits=None, in_splits=None):
+        torch.cuda.synchronize()
+        self.slots[rank] = (inp, in_splits if in_splits is not None else [inp.shape[0] // self.n] * self.n)
+        self.bar.wait()
+        pos = 0
+        for s in range(self.n):
+            sinp, splits = self.slots[s]
+            start = sum(splits[:rank])
+            cnt = splits[rank]
+            out[pos:pos + cnt].copy_(sinp[start:start + cnt])
+            pos += cnt
+        torch.cuda.synchronize()
+        self.bar.wait()
+
+
+class _FakeGroup:
+    def __init__(self, rank, n, comm):
+        self._rank, self._n, self.comm = rank, n, comm
+
+    def rank(self):
+        return self._rank
+
+    def size(self):
+        return self._n
+
+    def barrier(self):
+        self.comm.bar.wait()
+
+
+def _buffer_case(rank, world, fixture, comm, results):
+    try:
+        torch.cuda.set_device(0)
+        from deepep_amd import ElasticBuffer
+        fx = load(fixture)
+        T, H, K, E, R = (int(v) for v in fx['meta'])
+        ranks = ranks_of(fx)
+        me = ranks[rank]
+        grp = _FakeGroup(rank, world, comm) if world > 1 else None
+        if grp is None:
+            import torch.distributed as dist
+            if not dist.is_initialized():
+                os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+                os.environ.setdefault('MASTER_PORT', '29541')
+                dist.init_process_group('gloo', rank=0, world_size=1)
+            grp = dist.group.WORLD
+        buf = ElasticBuffer(grp, num_max_tokens_per_rank=T, hidden=H, num_topk=K)
+        if world > 1:
+            buf._a2a = lambda out, inp, os_=None, is_=None: comm.a2a(rank, out, inp, os_, is_)
+        idx = torch.from_numpy(me['topk_idx'].copy()).cuda()
+        w = torch.from_numpy(me['topk_weights'].copy()).cuda()
+        x = _bf16(me['x']) if 'x' in me else torch.randn((T, H), device='cuda').to(torch.bfloat16)
+        failures = []
+
+        def y_of(g):
+            s, t = divmod(int(g), T)
+            return ranks[s]['y'][t]
+
+        recv_x, recv_idx, recv_w, handle, _ = buf.dispatch(x, topk_idx=idx, topk_weights=w, num_experts=E)
+        n = handle.num_recv_tokens
+        src = handle.recv_src_metadata[:n, 0].cpu().numpy()
+        local = np.stack([y_of(g) for g in src]) if n else np.zeros((0, K, H), np.uint16)
+        local = np.where((recv_idx.cpu().numpy() == -1)[..., None], np.uint16(0), local)
+        x_red = _bf16(ordered_accumulate(local)) if n else torch.empty((0, H), dtype=torch.bfloat16, device='cuda')
+        ex_x, _, ex_w, ex_handle, _ = buf.dispatch(x, topk_idx=idx, topk_weights=w, num_experts=E, do_expand=True)
+        meta = ex_handle.recv_src_metadata.cpu().numpy()
+        x_exp = np.full((ex_x.shape[0], H), 0x7fc1, dtype=np.uint16)
+        for i in range(meta.shape[0]):
+            y = y_of(meta[i, 0])
+            for k in range(K):
+                if meta[i, 2 + k] >= 0:
+                    x_exp[meta[i, 2 + k]] = y[k]
+        x_exp = _bf16(x_exp)
+        biases = [_bf16(me['bias0']), _bf16(me['bias1'])]
+        for nb in (0, 1, 2):
+            bias = None if nb == 0 else (biases[0] if nb == 1 else tuple(biases))
+            for xin, h, ww, tag in ((x_red, handle, recv_w, 'non-expanded'), (x_exp, ex_handle, ex_w, 'expanded')):
+                out, out_w, _ = buf.combine(xin, h, topk_weights=ww, bias=bias)
+                torch.cuda.synchronize()
+                if not np.array_equal(_u16(out), me[f'combined_multi_b{nb}']):
+                    failures.append(f'{tag} b{nb}')
+                if not torch.equal(out_w.cpu(), torch.from_numpy(me['topk_weights'])):
+                    failures.append(f'{tag} weights b{nb}')
+        results[rank] = failures
+    except Exception:
+        import traceback
+        results[rank] = [traceback.format_exc()]
+        comm.bar.abort() if comm is not None else None
+
+
+@pytest.mark.parametrize('fixture,world', [
+    ('f1_ep1_t128_h1024_k2.npz', 1),
+    ('f4_ep4_t96_h256_k2.npz', 4),
+    ('f2_ep8_t64_h256_k8.npz', 8),
+    ('f3_ep8_skew_t128_h64_k8.npz', 8),
+])
+def test_elastic_buffer_golden_on_gpu(fixture, world):
+    comm = _ThreadComm(world) if world > 1 else None
+    results = {}
+    threads = [threading.Thread(target=_buffer_case, args=(r, world, fixture, comm, results)) for r in range(world)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=300)
+    assert len(results) == world, results
+    bad = {r: f for r, f in results.items() if f}
+    assert not bad, bad
+
+
+@pytest.mark.parametrize('weighted', [False, True])
+def test_config2_full_size_bitwise(weighted):
+    """BASELINE config 2: EP=1, 8192 tokens, hidden 7168, top-8, E=256; full output vs the oracle."""
+    import torch.distributed as dist
+    from deepep_amd import ElasticBuffer
+    if not dist.is_initialized():
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        os.environ.setdefault('MASTER_PORT', '29542')
+        dist.init_process_group('gloo', rank=0, world_size=1)
+    T, H, K, E = 8192, 7168, 8, 256
+    g = torch.Generator(device='cuda').manual_seed(11)
+    scores = torch.rand((T, E), device='cuda', generator=g)
+    w, idx = torch.topk(scores, K, dim=-1, sorted=False)
+    idx = idx.to(torch.int64)
+    buf = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=T, hidden=H, num_topk=K)
+    x = torch.zeros((T, H), dtype=torch.bfloat16, device='cuda')
+    _, _, ex_w, handle, _ = buf.dispatch(x, topk_idx=idx, topk_weights=w, num_experts=E, do_expand=True)
+    y = torch.randn((handle.num_expanded_tokens, H), device='cuda', generator=g).to(torch.bfloat16)
+    out, out_w, _ = buf.combine(y, handle, topk_weights=ex_w, apply_topk_weights=weighted)
+    torch.cuda.synchronize()
+    meta = handle.recv_src_metadata.cpu().numpy()
+    part, _ = oracle.phase_a(_u16(y), meta, K, True, ex_w.cpu().numpy(), weighted=weighted)
+    recv = np.zeros((1, T, H), np.uint16)
+    recv[0, meta[:, 0] % T] = part
+    ref, _ = oracle.phase_b(recv, None, idx.cpu().numpy(), E, 1, True, True)
+    assert np.array_equal(_u16(out), ref)
+    assert torch.equal(out_w, w)
+    if weighted:
+        # and within the reference's weighted tolerance of the exact sum (test_low_latency.py:178-181)
+        yd = y.double()
+        exact = torch.zeros((T, H), dtype=torch.float64, device='cuda')
+        slots = handle.recv_src_metadata[:, 2:].long()
+        tok = (handle.recv_src_metadata[:, 0] % T).long()
+        for k in range(K):
+            exact[tok] += yd[slots[:, k]] * ex_w.double()[slots[:, k]].unsqueeze(1)
+        assert oracle.calc_diff(oracle.bf16_to_f32(_u16(out)), exact.cpu().numpy()) < 1e-5

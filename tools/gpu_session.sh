@@ -1,0 +1,29 @@
+#!/bin/bash
+# One GPU session on the gpurun box: tests, smoke, bench, rocprof kernel trace.
+# Each GPU step has its own time limit; a fault/abort/timeout (anything but exit 0/1) ends the session.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out
+mkdir -p $OUT
+run() {   # run <name> <timeout> <cmd...>
+    local name=$1 tmo=$2; shift 2
+    echo "=== $name: $*" | tee -a $OUT/session.log
+    timeout -k 10 "$tmo" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    echo "=== $name rc=$rc" | tee -a $OUT/session.log
+    tail -5 "$OUT/$name.log"
+    if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after rc=$rc"; exit $rc; fi
+    return 0
+}
+for step in "$@"; do
+    case $step in
+        tests)  run pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
+        smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+        bench)  run bench 600 python bench.py ;;
+        benchplain) run bench_plain 600 python bench.py --plain --no-cpu-baseline --no-loopback ;;
+        prof)   run rocprof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o prof --output-format csv -- python3 bench.py --no-cpu-baseline --no-loopback --steps 20 --warmup 5 ;;
+        kbench) run kbench 600 python tools/kbench.py ;;
+        *) echo "unknown step $step" ;;
+    esac
+done

@@ -120,10 +120,11 @@ def main():
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    ev0.record(buf.comm_stream)
+    stream = torch.cuda.current_stream()        # sync-mode combine runs on the caller's stream
+    ev0.record(stream)
     for _ in range(args.steps):
         step()
-    ev1.record(buf.comm_stream)
+    ev1.record(stream)
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
@@ -151,21 +152,21 @@ def main():
 
         def launch():
             kern.combine_reduce(MODE_FUSED, y, out, T, table=plan.local_table, row_weights=ex_w if weighted else None,
-                                wtable=plan.local_table, wsrc=ex_w, out_weights=out_w, stream=buf.comm_stream)
+                                wtable=plan.local_table, wsrc=ex_w, out_weights=out_w, stream=stream)
         for _ in range(5):
             launch()
         k0, k1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        k0.record(buf.comm_stream)
+        k0.record(stream)
         for _ in range(args.steps):
             launch()
-        k1.record(buf.comm_stream)
+        k1.record(stream)
         torch.cuda.synchronize()
         kern_us = k0.elapsed_time(k1) * 1e3 / args.steps
         achieved = bytes_rank / (kern_us * 1e-6) / 1e9
         workload = f'combine_fused_{"weighted" if weighted else "plain"}_t{T}_h{H}_k{K}'
         roofline = dict(bound='hbm', achieved=round(achieved, 1), peak=HBM_PEAK_GBPS, unit='GB/s',
                         frac=round(achieved / HBM_PEAK_GBPS, 4), traffic=_pmc_traffic(workload),
-                        kernel='combine_reduce_kernel<FUSED>', kernel_us=round(kern_us, 2),
+                        kernel='combine_rows_kernel<FUSED>', kernel_us=round(kern_us, 2),
                         bytes_per_launch=bytes_rank, in_region_us_per_step=round(comm_ms * 1e3, 2))
 
     loopback = None

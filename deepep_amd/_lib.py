@@ -38,6 +38,7 @@ SIGNATURES = {
                                    _I, _P,
                                    _P]),
     'deepep_build_local_plan': (_I, [_P, _I, _I, _I, _I, _P, _I, _I, _P, _P, _P]),
+    'deepep_set_launch_config': (_I, [_I, _I, _I]),
     'deepep_combine_buffer_size': (_I64, [_I, _I, _I, _I, _I]),
 }
 

@@ -8,15 +8,17 @@
 //   weighted variant     legacy low-latency combine        csrc/kernels/legacy/internode_ll.cu:1072-1135
 //
 // How (MI355X-first, not a translation of the TMA/warp design):
-//   * one 256-thread workgroup (4 wave64) owns a tile of `units_per_block` output rows;
-//   * the tile's slot table (and, weighted, the gating weights) is staged into LDS with one
-//     coalesced pass, compacted to the ascending list of valid slots per row, and the top-k
-//     weight pass-through is written in the same pass;
-//   * each wave then streams (row, 1-KiB-column-chunk) items: for a chunk every lane holds
-//     VPT x 16 B of each of up to 8 source rows in flight (global_load_dwordx4, non-temporal:
-//     every expanded row is read exactly once), accumulates bf16 -> fp32 in registers in the
-//     reference's order, rounds once with v_cvt_pk_bf16_f32 (RNE) and stores 16 B per lane.
-//   No MFMA: this is an HBM-bound gather + elementwise add (roofline in DESIGN.md).
+//   * the work is split into items = (output row, column chunk of 64 lanes x 2 x 16 B); one wave64
+//     owns one item and a 256-thread workgroup owns 4 consecutive items (7 items per token at
+//     hidden 7168), so the grid is ~14K workgroups with no tail imbalance;
+//   * the item's row of the slot table (and, weighted, the gating weights) is staged once per
+//     workgroup in LDS, one entry per lane; the valid slots are visited in ascending order through
+//     the wave's ballot mask (= the reference's compacted slot order);
+//   * each lane keeps 8 rows x 2 x 16 B of non-temporal global_load_dwordx4 in flight (every
+//     expanded row is read exactly once), accumulates bf16 -> fp32 in registers in the reference's
+//     order, rounds once with v_cvt_pk_bf16_f32 (RNE) and writes 2 x 16 B with a write-through
+//     (sc1) buffer store.
+//   No MFMA: this is an HBM-bound gather + elementwise add (roofline and measurements in DESIGN.md).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -32,10 +34,7 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kThreads = 256;
-constexpr int kWaves = kThreads / 64;
 constexpr int kMaxWidth = 32;          // top-k <= 32, as the reference (combine_reduce_epilogue.cuh:64)
-constexpr int kMaxUnitsPerBlock = 16;
 constexpr int kGroup = 8;              // source rows in flight per lane per group
 
 thread_local char g_last_error[512] = "";
@@ -121,187 +120,216 @@ __device__ __forceinline__ u32x4 acc_pack(const float* acc) {
     return r;
 }
 
-template <int kMode, bool kWeighted, int kVPT, bool kNT>
-__global__ void __launch_bounds__(kThreads)
-combine_reduce_kernel(const Params p) {
-    __shared__ int32_t s_slot[kMaxUnitsPerBlock][kMaxWidth];
-    __shared__ float s_w[kMaxUnitsPerBlock][kMaxWidth];
-    __shared__ int32_t s_cnt[kMaxUnitsPerBlock];
+// Output stores: buffer_store_dwordx4 with a per-row descriptor (the hardware range check
+// drops the lanes past the row end).  The cache policy is a template parameter; measured on
+// MI355X (tools/probe.hip, 8192 x 7168 x top-8): sc1 (write-through, line dropped from L2)
+// 164.6 us, plain 166.2 us, nt 171.8 us for the gather + store pattern; write-only 8.0 / 7.4 /
+// 5.9 TB/s.  sc1 is the default.
+constexpr int kAuxNT = 2, kAuxSC1 = 16;      // (sc0 = 1)
 
-    const int tid = static_cast<int>(threadIdx.x);
-    const int upb = p.units_per_block;
-    const int u0 = static_cast<int>(blockIdx.x) * upb;
-    const int nu = min(upb, p.num_units - u0);
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void* row, int bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(row), 0, bytes, 0x00020000);
+}
+
+// One wave per item = (unit u, column chunk c): the chunk is 64 lanes x kVPT x 16 B of every
+// source row of u.  A 256-thread workgroup takes 4 consecutive items.  The unit's slot table row
+// (and its gating weights) is staged once per workgroup in LDS (kLDS) or per wave in registers,
+// one entry per lane; the valid slots are then visited in ascending order through the ballot mask,
+// which is exactly the compacted order of compute_topk_slots (combine_utils.cuh:41-53).
+template <int kMode, bool kWeighted, int kVPT, bool kFull, int kStoreAux, bool kLDS>
+__global__ void __launch_bounds__(256)
+combine_rows_kernel(const Params p) {
+    constexpr int kChunkVecs = 64 * kVPT;
+    const int tid = static_cast<int>(threadIdx.x), lane = tid & 63, wave = tid >> 6;
+    const int nvec = p.hidden >> 3;                          // 16-byte vectors per row
+    const int nchunks = (nvec + kChunkVecs - 1) / kChunkVecs;
+    const int64_t items = static_cast<int64_t>(p.num_units) * nchunks;
+    const int64_t it0 = static_cast<int64_t>(blockIdx.x) * 4;
+    const int64_t it = it0 + wave;
     const int width = p.table == nullptr ? 1 : p.table_width;
 
-    // ---- stage the tile's slot table (+ gating weights) into LDS, coalesced
-    for (int e = tid; e < nu * width; e += kThreads) {
-        const int u = e / width, j = e - u * width;
-        int32_t s = p.table == nullptr ? (u0 + u)
-                                       : p.table[static_cast<int64_t>(u0 + u) * p.table_stride + j];
-        if (s >= p.num_src_rows) {                      // never dereference a bad slot
+    auto load_slot = [&](int64_t u, int j) -> int32_t {
+        int32_t s = p.table == nullptr ? static_cast<int32_t>(u) : p.table[u * p.table_stride + j];
+        if (s >= p.num_src_rows) {                           // never dereference a bad slot
             if (p.error_flag != nullptr) atomicOr(p.error_flag, 1);
             s = -1;
         }
-        s_slot[u][j] = s;
-        if constexpr (kWeighted)
-            s_w[u][j] = s >= 0 ? p.row_weights[s] : 0.0f;
-    }
-    // ---- top-k weight pass-through (combine.cuh:215-226, combine_reduce_epilogue.cuh:127-141)
-    if (p.out_weights != nullptr) {
-        for (int e = tid; e < nu * p.num_weights; e += kThreads) {
-            const int u = e / p.num_weights, k = e - u * p.num_weights;
-            const int64_t gu = u0 + u;
-            const int64_t i = p.wtable == nullptr ? gu * p.num_weights + k
-                                                  : static_cast<int64_t>(p.wtable[gu * p.wtable_stride + k]);
-            p.out_weights[gu * p.num_weights + k] = i >= 0 ? p.wsrc[i] : 0.0f;
-        }
-    }
-    __syncthreads();
-    // ---- compact to the ascending list of valid slots (compute_topk_slots, combine_utils.cuh:41-53)
-    if (tid < nu) {
-        int n = 0;
-        for (int j = 0; j < width; ++j) {
-            const int32_t s = s_slot[tid][j];
-            if (s >= 0) {
-                s_slot[tid][n] = s;                    // n <= j: in-place compaction is safe
-                if constexpr (kWeighted) s_w[tid][n] = s_w[tid][j];
-                ++n;
-            }
-        }
-        s_cnt[tid] = n;
-    }
-    __syncthreads();
+        return s;
+    };
 
-    // ---- stream the rows: items = (unit, column chunk of 64 lanes x kVPT x 16 B)
-    const int wave = tid >> 6, lane = tid & 63;
-    const int nvec = p.hidden >> 3;                     // 16-byte vectors per row
-    constexpr int kChunkVecs = 64 * kVPT;
-    const int nchunks = (nvec + kChunkVecs - 1) / kChunkVecs;
+    int32_t my_slot = -1;
+    float my_w = 0.0f;
+    if constexpr (kLDS) {
+        __shared__ int32_t s_slot[4][kMaxWidth];
+        __shared__ float s_w[4][kMaxWidth];
+        const int64_t u_first = it0 / nchunks;
+        const int nu = static_cast<int>(min(it0 + 3, items - 1) / nchunks - u_first) + 1;
+        if (tid < nu * width) {                             // nu * width <= 4 * 32 = 128 threads
+            const int ul = tid / width, j = tid - ul * width;
+            const int32_t s = load_slot(u_first + ul, j);
+            s_slot[ul][j] = s;
+            if constexpr (kWeighted) s_w[ul][j] = s >= 0 ? p.row_weights[s] : 0.0f;
+        }
+        __syncthreads();
+        if (it >= items) return;
+        const int ul = static_cast<int>(it / nchunks - u_first);
+        if (lane < width) {
+            my_slot = s_slot[ul][lane];
+            if constexpr (kWeighted) my_w = s_w[ul][lane];
+        }
+    } else {
+        if (it >= items) return;
+        if (lane < width) {
+            my_slot = load_slot(it / nchunks, lane);
+            if constexpr (kWeighted) my_w = my_slot >= 0 ? p.row_weights[my_slot] : 0.0f;
+        }
+    }
+    const int64_t u = it / nchunks;
+    const int c = static_cast<int>(it - u * nchunks);
+    const uint64_t valid = __ballot(my_slot >= 0);
+    const int n = __popcll(valid);
+
+    // ---- top-k weight pass-through (combine.cuh:215-226, combine_reduce_epilogue.cuh:127-141),
+    //      written once per unit by the wave owning chunk 0
+    if (c == 0 && p.out_weights != nullptr && lane < p.num_weights) {
+        const int64_t i = p.wtable == nullptr ? u * p.num_weights + lane
+                                              : static_cast<int64_t>(p.wtable[u * p.wtable_stride + lane]);
+        p.out_weights[u * p.num_weights + lane] = i >= 0 ? p.wsrc[i] : 0.0f;
+    }
+
+    int vidx[kVPT];
+    bool vok[kVPT];
+#pragma unroll
+    for (int v = 0; v < kVPT; ++v) {
+        vidx[v] = c * kChunkVecs + v * 64 + lane;
+        vok[v] = kFull || vidx[v] < nvec;
+    }
     const bool has_bias0 = p.bias0 != nullptr, has_bias1 = p.bias1 != nullptr;
     const bool has_bias = has_bias0 || has_bias1;
 
-    for (int it = wave; it < nu * nchunks; it += kWaves) {
-        const int u = it / nchunks;
-        const int c = it - u * nchunks;
-        const int n = __builtin_amdgcn_readfirstlane(s_cnt[u]);
-        const int64_t gu = u0 + u;
-        int vidx[kVPT];
-        bool vok[kVPT];
+    // Initial value: -0.0f where the reference adds two sources in bf16 without an fp32 zero in
+    // front (the hadd bypass, combine_utils.cuh:79-110: -0 + a == a exactly), +0.0f where it
+    // starts from `float2 reduced = {}` (combine_utils.cuh:114).
+    bool copy_row = false;
+    float init;
+    if constexpr (kMode == DEEPEP_MODE_LOCAL || kMode == DEEPEP_MODE_FUSED) {
+        copy_row = !kWeighted && n == 1;                      // no_local_reduce (combine.cuh:134-156)
+        init = (!kWeighted && n == 2) ? -0.0f : 0.0f;
+    } else {
+        init = (!has_bias && n == 2) ? -0.0f : 0.0f;          // epilogue: bypass only without bias
+    }
+    float acc[kVPT][8];
+#pragma unroll
+    for (int v = 0; v < kVPT; ++v)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[v][e] = init;
+    if constexpr (kMode == DEEPEP_MODE_EPILOGUE) {
+        // bias0 then bias1 before the partials (combine_utils.cuh:113-127)
 #pragma unroll
         for (int v = 0; v < kVPT; ++v) {
-            vidx[v] = c * kChunkVecs + v * 64 + lane;
-            vok[v] = vidx[v] < nvec;
+            if (has_bias0 && vok[v]) acc_add(acc[v], *(reinterpret_cast<const u32x4*>(p.bias0 + u * p.hidden) + vidx[v]));
+            if (has_bias1 && vok[v]) acc_add(acc[v], *(reinterpret_cast<const u32x4*>(p.bias1 + u * p.hidden) + vidx[v]));
         }
+    }
 
-        float acc[kVPT][8];
-        u32x4 result[kVPT];
-
-        // Phase-A (or weighted) reduction over the compacted slots, ascending.
-        // Initial value: -0.0f when the reference adds the two sources in bf16 without an fp32
-        // zero in front (the hadd bypass, combine_utils.cuh:79-110: -0 + a == a exactly),
-        // +0.0f where it starts from `float2 reduced = {}` (combine_utils.cuh:114).
-        bool copy_row = false;
-        if constexpr (kMode == DEEPEP_MODE_LOCAL || kMode == DEEPEP_MODE_FUSED) {
-            copy_row = !kWeighted && n == 1;            // no_local_reduce (combine.cuh:134-156)
-            const float init = (!kWeighted && n == 2) ? -0.0f : 0.0f;
+    u32x4 result[kVPT];
+    for (int g = 0; g < width; g += kGroup) {
+        const uint32_t gmask = static_cast<uint32_t>(valid >> g) & 0xffu;
+        if (gmask == 0u) continue;
+        u32x4 vals[kGroup][kVPT];
 #pragma unroll
-            for (int v = 0; v < kVPT; ++v)
+        for (int j = 0; j < kGroup; ++j) {
+            if (gmask & (1u << j)) {
+                const int32_t sj = __builtin_amdgcn_readlane(my_slot, g + j);
+                const u32x4* row = reinterpret_cast<const u32x4*>(p.src + static_cast<int64_t>(sj) * p.src_stride);
 #pragma unroll
-                for (int e = 0; e < 8; ++e) acc[v][e] = init;
+                for (int v = 0; v < kVPT; ++v)
+                    vals[j][v] = vok[v] ? load16<true>(row + vidx[v]) : (u32x4){0u, 0u, 0u, 0u};
+            }
+        }
+        if (copy_row) {
+#pragma unroll
+            for (int j = 0; j < kGroup; ++j)
+                if (gmask & (1u << j))
+#pragma unroll
+                    for (int v = 0; v < kVPT; ++v) result[v] = vals[j][v];
         } else {
-            // Epilogue: bias first (bias0 then bias1), then the partials; bypass without bias.
-            const float init = (!has_bias && n == 2) ? -0.0f : 0.0f;
-#pragma unroll
-            for (int v = 0; v < kVPT; ++v)
-#pragma unroll
-                for (int e = 0; e < 8; ++e) acc[v][e] = init;
-            if (has_bias0) {
-#pragma unroll
-                for (int v = 0; v < kVPT; ++v)
-                    if (vok[v]) acc_add(acc[v], load16<kNT>(reinterpret_cast<const u32x4*>(p.bias0 + gu * p.hidden) + vidx[v]));
-            }
-            if (has_bias1) {
-#pragma unroll
-                for (int v = 0; v < kVPT; ++v)
-                    if (vok[v]) acc_add(acc[v], load16<kNT>(reinterpret_cast<const u32x4*>(p.bias1 + gu * p.hidden) + vidx[v]));
-            }
-        }
-
-        for (int g = 0; g < n; g += kGroup) {
-            u32x4 vals[kGroup][kVPT];
 #pragma unroll
             for (int j = 0; j < kGroup; ++j) {
-                if (g + j < n) {
-                    const int32_t s = __builtin_amdgcn_readfirstlane(s_slot[u][g + j]);
-                    const u32x4* row = reinterpret_cast<const u32x4*>(p.src + static_cast<int64_t>(s) * p.src_stride);
+                if (gmask & (1u << j)) {
+                    if constexpr (kWeighted) {
+                        const float w = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_w), g + j));
 #pragma unroll
-                    for (int v = 0; v < kVPT; ++v)
-                        vals[j][v] = vok[v] ? load16<kNT>(row + vidx[v]) : (u32x4){0u, 0u, 0u, 0u};
-                }
-            }
-            if (copy_row) {
+                        for (int v = 0; v < kVPT; ++v) acc_fma(acc[v], vals[j][v], w);
+                    } else {
 #pragma unroll
-                for (int v = 0; v < kVPT; ++v) result[v] = vals[0][v];
-            } else {
-#pragma unroll
-                for (int j = 0; j < kGroup; ++j) {
-                    if (g + j < n) {
-                        if constexpr (kWeighted) {
-                            const float w = s_w[u][g + j];
-#pragma unroll
-                            for (int v = 0; v < kVPT; ++v) acc_fma(acc[v], vals[j][v], w);
-                        } else {
-#pragma unroll
-                            for (int v = 0; v < kVPT; ++v) acc_add(acc[v], vals[j][v]);
-                        }
+                        for (int v = 0; v < kVPT; ++v) acc_add(acc[v], vals[j][v]);
                     }
                 }
             }
         }
-        if (!copy_row) {
-#pragma unroll
-            for (int v = 0; v < kVPT; ++v) result[v] = acc_pack(acc[v]);
-        }
-
-        if constexpr (kMode == DEEPEP_MODE_FUSED) {
-            // Phase B over the single per-rank partial (EP = 1): epilogue with one slot.
-            // No bias: hadd bypass with a zero second operand -> +0 + partial.
-            // Bias: fp32 +0 + bias0 + bias1 + partial, one rounding (combine_utils.cuh:111-165).
-            const bool present = n > 0;
-#pragma unroll
-            for (int v = 0; v < kVPT; ++v) {
-                float a[8];
-#pragma unroll
-                for (int e = 0; e < 8; ++e) a[e] = 0.0f;
-                if (has_bias0 && vok[v]) acc_add(a, load16<kNT>(reinterpret_cast<const u32x4*>(p.bias0 + gu * p.hidden) + vidx[v]));
-                if (has_bias1 && vok[v]) acc_add(a, load16<kNT>(reinterpret_cast<const u32x4*>(p.bias1 + gu * p.hidden) + vidx[v]));
-                if (present) acc_add(a, result[v]);
-                result[v] = acc_pack(a);
-            }
-        }
-
-        uint16_t* orow = p.out + gu * p.out_stride;
-#pragma unroll
-        for (int v = 0; v < kVPT; ++v)
-            if (vok[v]) store16<kNT>(reinterpret_cast<u32x4*>(orow) + vidx[v], result[v]);
     }
+    if (!copy_row) {
+#pragma unroll
+        for (int v = 0; v < kVPT; ++v) result[v] = acc_pack(acc[v]);
+    }
+
+    if constexpr (kMode == DEEPEP_MODE_FUSED) {
+        // Phase B over the single per-rank partial (EP = 1): epilogue with one slot.
+        // No bias: hadd bypass with a zero second operand -> +0 + partial.
+        // Bias: fp32 +0 + bias0 + bias1 + partial, one rounding (combine_utils.cuh:111-165).
+        const bool present = n > 0;
+#pragma unroll
+        for (int v = 0; v < kVPT; ++v) {
+            float a[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) a[e] = 0.0f;
+            if (has_bias0 && vok[v]) acc_add(a, *(reinterpret_cast<const u32x4*>(p.bias0 + u * p.hidden) + vidx[v]));
+            if (has_bias1 && vok[v]) acc_add(a, *(reinterpret_cast<const u32x4*>(p.bias1 + u * p.hidden) + vidx[v]));
+            if (present) acc_add(a, result[v]);
+            result[v] = acc_pack(a);
+        }
+    }
+
+    const __amdgpu_buffer_rsrc_t orow = row_rsrc(p.out + u * p.out_stride, p.hidden * 2);
+#pragma unroll
+    for (int v = 0; v < kVPT; ++v)
+        __builtin_amdgcn_raw_buffer_store_b128(result[v], orow, vidx[v] * 16, 0, kStoreAux);
 }
 
-template <int kMode, bool kWeighted, int kVPT>
-void launch(const Params& p, bool nt, hipStream_t stream) {
-    const dim3 grid((p.num_units + p.units_per_block - 1) / p.units_per_block);
-    if (nt)
-        hipLaunchKernelGGL((combine_reduce_kernel<kMode, kWeighted, kVPT, true>), grid, dim3(kThreads), 0, stream, p);
-    else
-        hipLaunchKernelGGL((combine_reduce_kernel<kMode, kWeighted, kVPT, false>), grid, dim3(kThreads), 0, stream, p);
+struct LaunchConfig {
+    int vec_per_lane = 0;        // 0: auto (16-byte vectors per lane per source row and item)
+    int stage_lds = -1;          // -1: auto (1 = LDS staging per workgroup, 0 = per-wave registers)
+    int store_policy = -1;       // -1: auto (0 plain, 1 nt, 2 sc1)
+};
+LaunchConfig g_config;
+
+template <int kMode, bool kWeighted, int kVPT, bool kFull, int kAux>
+void launch_lds(const Params& p, bool lds, hipStream_t stream) {
+    const int nvec = p.hidden / 8;
+    const int64_t items = static_cast<int64_t>(p.num_units) * ((nvec + 64 * kVPT - 1) / (64 * kVPT));
+    const dim3 grid(static_cast<unsigned>((items + 3) / 4)), block(256);
+    if (lds) hipLaunchKernelGGL((combine_rows_kernel<kMode, kWeighted, kVPT, kFull, kAux, true>), grid, block, 0, stream, p);
+    else hipLaunchKernelGGL((combine_rows_kernel<kMode, kWeighted, kVPT, kFull, kAux, false>), grid, block, 0, stream, p);
+}
+
+template <int kMode, bool kWeighted, int kVPT, bool kFull>
+void launch_aux(const Params& p, bool lds, int policy, hipStream_t stream) {
+    if (policy == 0) launch_lds<kMode, kWeighted, kVPT, kFull, 0>(p, lds, stream);
+    else if (policy == 1) launch_lds<kMode, kWeighted, kVPT, kFull, kAuxNT>(p, lds, stream);
+    else launch_lds<kMode, kWeighted, kVPT, kFull, kAuxSC1>(p, lds, stream);
 }
 
 template <int kMode, bool kWeighted>
-void launch_vpt(const Params& p, int vpt, bool nt, hipStream_t stream) {
-    if (vpt == 1) launch<kMode, kWeighted, 1>(p, nt, stream);
-    else if (vpt == 2) launch<kMode, kWeighted, 2>(p, nt, stream);
-    else launch<kMode, kWeighted, 4>(p, nt, stream);
+void launch_vpt(const Params& p, int vpt, bool lds, int policy, hipStream_t stream) {
+    const int nvec = p.hidden / 8;
+    if (vpt == 1) {
+        if (nvec % 64 == 0) launch_aux<kMode, kWeighted, 1, true>(p, lds, policy, stream);
+        else launch_aux<kMode, kWeighted, 1, false>(p, lds, policy, stream);
+    } else {
+        if (nvec % 128 == 0) launch_aux<kMode, kWeighted, 2, true>(p, lds, policy, stream);
+        else launch_aux<kMode, kWeighted, 2, false>(p, lds, policy, stream);
+    }
 }
 
 bool aligned16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15u) == 0; }
@@ -373,9 +401,6 @@ int deepep_combine_reduce(int mode, int weighted,
         return set_error(DEEPEP_ERR_INVALID_ARG, "bias is applied by the epilogue, not the local reduce");
     if (out_weights != nullptr && (wsrc == nullptr || num_weights < 1 || num_weights > kMaxWidth))
         return set_error(DEEPEP_ERR_INVALID_ARG, "weight pass-through needs wsrc and 1 <= num_weights <= %d", kMaxWidth);
-    if (units_per_block <= 0) units_per_block = 4;
-    if (units_per_block > kMaxUnitsPerBlock) units_per_block = kMaxUnitsPerBlock;
-
     Params p;
     p.src = static_cast<const uint16_t*>(src);
     p.num_src_rows = num_src_rows;
@@ -398,18 +423,23 @@ int deepep_combine_reduce(int mode, int weighted,
     p.units_per_block = units_per_block;
     p.error_flag = error_flag;
 
+    // Launch shape: one wave per (unit, 64 x vpt x 16-byte column chunk) item, 4 items per
+    // workgroup; at hidden 7168 a token is 7 items of 2 KiB per source row.
+    (void)units_per_block;                                  // kept in the ABI; items, not units, are tiled
     const int nvec = hidden / 8;
-    const int vpt = nvec >= 128 ? 2 : 1;
-    const bool nt = true;
+    int vpt = g_config.vec_per_lane > 0 ? g_config.vec_per_lane : (nvec >= 128 ? 2 : 1);
+    if (vpt != 1 && vpt != 2) vpt = 2;
+    const bool lds = g_config.stage_lds >= 0 ? g_config.stage_lds != 0 : true;
+    const int policy = g_config.store_policy >= 0 ? g_config.store_policy : 2;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (mode == DEEPEP_MODE_LOCAL) {
-        if (weighted) launch_vpt<DEEPEP_MODE_LOCAL, true>(p, vpt, nt, s);
-        else launch_vpt<DEEPEP_MODE_LOCAL, false>(p, vpt, nt, s);
+        if (weighted) launch_vpt<DEEPEP_MODE_LOCAL, true>(p, vpt, lds, policy, s);
+        else launch_vpt<DEEPEP_MODE_LOCAL, false>(p, vpt, lds, policy, s);
     } else if (mode == DEEPEP_MODE_EPILOGUE) {
-        launch_vpt<DEEPEP_MODE_EPILOGUE, false>(p, vpt, nt, s);
+        launch_vpt<DEEPEP_MODE_EPILOGUE, false>(p, vpt, lds, policy, s);
     } else {
-        if (weighted) launch_vpt<DEEPEP_MODE_FUSED, true>(p, vpt, nt, s);
-        else launch_vpt<DEEPEP_MODE_FUSED, false>(p, vpt, nt, s);
+        if (weighted) launch_vpt<DEEPEP_MODE_FUSED, true>(p, vpt, lds, policy, s);
+        else launch_vpt<DEEPEP_MODE_FUSED, false>(p, vpt, lds, policy, s);
     }
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess)
@@ -447,6 +477,15 @@ int deepep_build_local_plan(const int32_t* src_metadata, int num_recv_tokens, in
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess)
         return set_error(DEEPEP_ERR_HIP, "plan launch failed: %s", hipGetErrorString(err));
+    return DEEPEP_OK;
+}
+
+int deepep_set_launch_config(int vec_per_lane, int stage_lds, int store_policy) {
+    if (vec_per_lane < 0 || vec_per_lane > 2 || stage_lds < -1 || stage_lds > 1 || store_policy < -1 || store_policy > 2)
+        return set_error(DEEPEP_ERR_INVALID_ARG, "invalid launch configuration");
+    g_config.vec_per_lane = vec_per_lane;
+    g_config.stage_lds = stage_lds;
+    g_config.store_policy = store_policy;
     return DEEPEP_OK;
 }
 

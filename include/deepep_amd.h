@@ -72,7 +72,7 @@ const char* deepep_amd_last_error(void);
  *   out_weights    fp32 [num_units][num_weights] or NULL: top-k weight pass-through,
  *                  out_weights[u][k] = (i = wtable ? wtable[u*wtable_stride + k]
  *                                            : u*num_weights + k) >= 0 ? wsrc[i] : 0
- *   units_per_block  LDS tile height (0 = default)
+ *   units_per_block  reserved (0); the launch tiles (row, column-chunk) items, 4 per workgroup
  *   error_flag     device int or NULL; set to 1 when a slot is >= num_src_rows
  *                  (such slots are skipped, never dereferenced)
  */
@@ -104,6 +104,15 @@ int deepep_build_local_plan(const int32_t* src_metadata, int num_recv_tokens, in
                             int32_t* plan, int plan_width, int num_tokens,
                             const int64_t* topk_idx, int32_t* wtable,
                             deepep_stream_t stream);
+
+/*
+ * Tuning / diagnostics (process-global; 0 or -1 = automatic, the default):
+ *   vec_per_lane   16-byte vectors each lane loads per source row and item (1 or 2)
+ *   stage_lds      1: stage the slot table / weights per workgroup in LDS; 0: per wave in registers
+ *   store_policy   output store cache policy: 0 plain, 1 nt, 2 sc1 (write-through)
+ * The results are identical for every configuration; only the speed changes.
+ */
+int deepep_set_launch_config(int vec_per_lane, int stage_lds, int store_policy);
 
 /* ElasticBuffer::get_combine_buffer_size for one node (num_scaleout_ranks == 1). */
 int64_t deepep_combine_buffer_size(int num_max_tokens_per_rank, int hidden, int num_topk,

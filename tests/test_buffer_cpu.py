@@ -154,3 +154,81 @@ def test_elastic_buffer_matches_golden(fixture, world):
     assert len(results) == world
     bad = {r: f for r, f in results.items() if f}
     assert not bad, bad
+
+
+def _random_worker(rank, world, port, seed, queue):
+    import sys
+    sys.path.insert(0, ROOT)
+    try:
+        os.environ['MASTER_ADDR'] = '127.0.0.1'
+        os.environ['MASTER_PORT'] = str(port)
+        dist.init_process_group('gloo', rank=rank, world_size=world)
+        import oracle
+        from deepep_amd import ElasticBuffer
+        from tests.oracle_kernels import OracleKernels
+        T, H, K, E = 48, 136, 8, 8 * world           # hidden 136: a ragged number of 16-byte vectors
+        rng = np.random.default_rng(seed)
+        idx_all, w_all, y_all, b_all = [], [], [], []
+        for r in range(world):
+            idx = np.stack([rng.permutation(E)[:K] for _ in range(T)]).astype(np.int64)
+            idx[rng.random((T, K)) < 0.2] = -1
+            idx[0] = -1                              # a token routed nowhere
+            w = rng.random((T, K)).astype(np.float32) * (idx >= 0)
+            y = oracle.f32_to_bf16(rng.standard_normal((T, K, H)).astype(np.float32))
+            y[idx < 0] = 0
+            idx_all.append(idx), w_all.append(w), y_all.append(y)
+            b_all.append(oracle.f32_to_bf16(rng.standard_normal((T, H)).astype(np.float32)))
+        disp = oracle.simulate_dispatch(idx_all, E, T)
+        x_exp_all, w_exp_all = [], []
+        for r, d in enumerate(disp):
+            xe = np.zeros((d['num_expanded'], H), np.uint16)
+            we = np.zeros((d['num_expanded'],), np.float32)
+            for row, (g, k) in enumerate(d['expanded_src']):
+                s, t = divmod(int(g), T)
+                xe[row], we[row] = y_all[s][t, k], w_all[s][t, k]
+            x_exp_all.append(xe), w_exp_all.append(we)
+        expect = oracle.combine_ep(x_exp_all, [d['src_metadata'] for d in disp], idx_all, E, T, expanded=True,
+                                   topk_weights_per_rank=w_exp_all,
+                                   bias_per_rank=[(b, None) for b in b_all])
+        buf = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=T, hidden=H, num_topk=K)
+        buf._kernels = OracleKernels()
+        x = torch.zeros((T, H), dtype=torch.bfloat16)
+        _, _, ex_w, handle, _ = buf.dispatch(x, topk_idx=torch.from_numpy(idx_all[rank]),
+                                             topk_weights=torch.from_numpy(w_all[rank]),
+                                             num_experts=E, do_expand=True)
+        failures = []
+        if not np.array_equal(handle.recv_src_metadata.numpy(), disp[rank]['src_metadata']):
+            failures.append('recv_src_metadata differs from the oracle dispatch')
+        out, out_w, _ = buf.combine(_u16_to_bf16(x_exp_all[rank]), handle, topk_weights=ex_w,
+                                    bias=_u16_to_bf16(b_all[rank]))
+        if not np.array_equal(_bf16_to_u16(out), expect[rank][0]):
+            failures.append('combined_x')
+        if not np.array_equal(out_w.numpy(), expect[rank][1]):
+            failures.append('combined_topk_weights')
+        queue.put((rank, failures))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:
+        queue.put((rank, [traceback.format_exc()]))
+
+
+@pytest.mark.parametrize('world', [2, 3])
+def test_random_routing_world(world):
+    """world_size 2 (and 3: a rank count that does not divide top-k) against oracle.combine_ep."""
+    ctx = mp.get_context('spawn')
+    queue = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_random_worker, args=(r, world, port, 7 + world, queue)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = {}
+    try:
+        for _ in range(world):
+            rank, failures = queue.get(timeout=240)
+            results[rank] = failures
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    assert len(results) == world and not any(results.values()), results

@@ -24,6 +24,7 @@ for step in "$@"; do
         benchplain) run bench_plain 600 python bench.py --plain --no-cpu-baseline --no-loopback ;;
         prof)   run rocprof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o prof --output-format csv -- python3 bench.py --no-cpu-baseline --no-loopback --steps 20 --warmup 5 ;;
         kbench) run kbench 600 python tools/kbench.py ;;
+        probe)  run probe 600 python tools/probe.py ;;
         *) echo "unknown step $step" ;;
     esac
 done

@@ -31,8 +31,14 @@ HBM_PEAK_GBPS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-l
 def _init_dist(n_gpus: int):
     if 'RANK' in os.environ and int(os.environ.get('WORLD_SIZE', '1')) > 1:
         local_rank = int(os.environ.get('LOCAL_RANK', 0))
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
+        # DEEPEP_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share devices)
+        backend = os.environ.get('DEEPEP_BENCH_BACKEND', 'nccl')
+        dev = local_rank % torch.cuda.device_count()
+        torch.cuda.set_device(dev)
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', dev))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
@@ -169,6 +175,33 @@ def main():
                         kernel='combine_rows_kernel<FUSED>', kernel_us=round(kern_us, 2),
                         bytes_per_launch=bytes_rank, in_region_us_per_step=round(comm_ms * 1e3, 2))
 
+    phases = None
+    if world > 1:
+        # Per-phase device time of the EP > 1 combine (phase A | exchange | phase B), same step
+        buf._phase_events = []
+        n_ph = max(5, args.steps // 2)
+        for _ in range(n_ph):
+            step()
+        torch.cuda.synchronize()
+        ev = buf._phase_events
+        buf._phase_events = None
+        t_a = sum(ev[4 * i].elapsed_time(ev[4 * i + 1]) for i in range(n_ph)) / n_ph
+        t_x = sum(ev[4 * i + 1].elapsed_time(ev[4 * i + 2]) for i in range(n_ph)) / n_ph
+        t_b = sum(ev[4 * i + 2].elapsed_time(ev[4 * i + 3]) for i in range(n_ph)) / n_ph
+        plan = handle._combine_plans[('multi', world)]
+        sent_rows = sum(c for r_, c in enumerate(plan.recv_counts) if r_ != rank)
+        x_bytes = sent_rows * (H * 2 + K * 4)
+        vals = torch.tensor([t_a + t_b, t_x, t_a, t_b], dtype=torch.float64, device=dev)
+        dist.all_reduce(vals, op=dist.ReduceOp.MAX)
+        xb = torch.tensor([float(x_bytes)], dtype=torch.float64, device=dev)
+        dist.all_reduce(xb)
+        phases = dict(phase_a_ms=round(float(vals[2]), 4), exchange_ms=round(float(vals[1]), 4),
+                      phase_b_ms=round(float(vals[3]), 4),
+                      reduce_only_gbps=round(total_bytes / (float(vals[0]) * 1e-3) / 1e9, 1),
+                      exchange_gbps_per_rank=round(float(xb.item()) / world / (float(vals[1]) * 1e-3) / 1e9, 1),
+                      note='max over ranks; reduce_only = algorithmic bytes of all ranks / (phase A + phase B); '
+                           'exchange = off-rank partial rows + weights / exchange time, per rank')
+
     loopback = None
     if world == 1 and not args.no_loopback:
         # Host-staged loopback (north_star): pinned host rows -> H2D -> combine -> D2H.
@@ -203,7 +236,7 @@ def main():
                                    f'{"gating-weighted" if weighted else "plain (reference semantics)"}',
                        'tokens_per_rank': T, 'hidden': H, 'topk': K, 'experts': E,
                        'parallelism': f'ep{world}'},
-            'roofline': roofline, 'cpu_baseline': cpu_baseline, 'loopback': loopback,
+            'roofline': roofline, 'cpu_baseline': cpu_baseline, 'loopback': loopback, 'phases': phases,
         }
         print(json.dumps(line), flush=True)
     dist.barrier()

@@ -110,9 +110,17 @@ class ElasticBuffer:
         self.comm_stream = torch.cuda.Stream(device=self.device) if self.use_cuda else None
         self._kernels = None
         self.runtime = self           # non-None while alive (the reference keeps its C++ runtime here)
+        self._phase_events = None     # optional list: bench instrumentation of the EP > 1 phases
+        self._group_barrier()
+
+    def _group_barrier(self) -> None:
+        """torch.cuda.synchronize(); group barrier; synchronize (elastic.py:365-367)."""
         if self.use_cuda:
             torch.cuda.synchronize()
-        group.barrier()
+        if isinstance(self.group, dist.ProcessGroup):
+            dist.barrier(group=self.group)
+        else:
+            self.group.barrier()
         if self.use_cuda:
             torch.cuda.synchronize()
 
@@ -244,6 +252,13 @@ class ElasticBuffer:
         if allocate_on_comm_stream:
             torch.cuda.set_stream(compute_stream)
         return event
+
+    def _mark(self, stream) -> None:
+        """Record a timing event on the kernel stream when phase instrumentation is on."""
+        if self._phase_events is not None and self.use_cuda:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record(stream)
+            self._phase_events.append(ev)
 
     @staticmethod
     def _null_ctx():
@@ -606,8 +621,10 @@ class ElasticBuffer:
                 partial = torch.empty((n_recv, hidden), dtype=x.dtype, device=x.device)
                 partial_w = torch.empty((n_recv, K), dtype=torch.float32, device=x.device) if topk_weights is not None else None
                 table_a = meta[:n_recv, 2:] if expanded else None
+                self._mark(stream)
                 kern.combine_reduce(MODE_LOCAL, x, partial, n_recv, table=table_a, row_weights=row_w,
                                     wtable=table_a, wsrc=wsrc, out_weights=partial_w, stream=stream)
+                self._mark(stream)
                 n_back = sum(plan.back_counts)
                 recv = torch.empty((n_back, hidden), dtype=x.dtype, device=x.device)
                 self._all_to_all(recv, partial, plan.back_counts, plan.recv_counts)
@@ -616,10 +633,12 @@ class ElasticBuffer:
                     recv_w = torch.empty((n_back, K), dtype=torch.float32, device=x.device)
                     self._all_to_all(recv_w, partial_w, plan.back_counts, plan.recv_counts)
                 self._before_epilogue(previous_event_before_epilogue)
+                self._mark(stream)
                 kern.combine_reduce(MODE_EPILOGUE, recv, combined_x, T, table=plan.table_b,
                                     bias0=bias_0, bias1=bias_1, wtable=plan.wtable_b,
                                     wsrc=recv_w.view(-1) if recv_w is not None else None,
                                     out_weights=combined_w, stream=stream)
+                self._mark(stream)
         event = None
         if not sync_mode:
             event = self._epilogue([x, topk_weights, bias_0, bias_1, meta, topk_idx, combined_x, combined_w, psum],

@@ -1,0 +1,56 @@
+"""Summaries of rocprofv3 output for profiles/ (kernel stats and PMC traffic).
+
+  python tools/summarize_prof.py stats  <kernel_stats.csv> <out.md>
+  python tools/summarize_prof.py pmc    <out.json> <workload> <bytes_per_launch> <counter_csv>...
+The PMC summary applies the gfx950 corrections of MI355X_MICROARCH.md (HBM section):
+FETCH_SIZE (KiB) counts half the bytes of a wide coalesced read stream -> x2; WRITE_SIZE (KiB)
+is exact for 16-B-per-lane stores.  TCC_EA0_RDREQ/WRREQ x 64 B are recorded alongside.
+"""
+import csv
+import json
+import sys
+from collections import defaultdict
+
+
+def stats(path, out):
+    rows = list(csv.DictReader(open(path)))
+    lines = ['| kernel | calls | avg us | min us | max us | share % |', '|---|---|---|---|---|---|']
+    for r in rows[:12]:
+        name = r['Name']
+        short = name.split('(')[0][:90] if 'combine_rows_kernel' not in name else name.split('((anonymous')[0]
+        lines.append(f"| `{short}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.2f} | {float(r['MinNs']) / 1e3:.2f} | "
+                     f"{float(r['MaxNs']) / 1e3:.2f} | {float(r['Percentage']):.1f} |")
+    open(out, 'w').write('\n'.join(lines) + '\n')
+    print('\n'.join(lines))
+
+
+def pmc(out, workload, algo_bytes, *paths):
+    per = defaultdict(list)
+    for p in paths:
+        for r in csv.DictReader(open(p)):
+            if 'combine_rows_kernel' not in r.get('Kernel_Name', ''):
+                continue
+            per[r['Counter_Name']].append(float(r['Counter_Value']))
+    avg = {k: sum(v) / len(v) for k, v in per.items()}
+    entry = {'counters_avg_per_launch': avg, 'algorithmic_bytes_per_launch': int(algo_bytes)}
+    read = 2 * avg['FETCH_SIZE'] * 1024 if 'FETCH_SIZE' in avg else None
+    write = avg['WRITE_SIZE'] * 1024 if 'WRITE_SIZE' in avg else None
+    if read is not None and write is not None:
+        entry['hbm_read_bytes_per_launch'] = read
+        entry['hbm_write_bytes_per_launch'] = write
+        entry['hbm_bytes_per_launch'] = read + write
+        entry['traffic_over_algorithmic'] = (read + write) / int(algo_bytes)
+    try:
+        data = json.load(open(out))
+    except (OSError, ValueError):
+        data = {}
+    data[workload] = entry
+    json.dump(data, open(out, 'w'), indent=1, sort_keys=True)
+    print(json.dumps({workload: entry}, indent=1))
+
+
+if __name__ == '__main__':
+    if sys.argv[1] == 'stats':
+        stats(sys.argv[2], sys.argv[3])
+    else:
+        pmc(sys.argv[2], sys.argv[3], sys.argv[4], *sys.argv[5:])

@@ -86,13 +86,15 @@ def _pmc_traffic(workload: str):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=50)
-    ap.add_argument('--warmup', type=int, default=10)
+    ap.add_argument('--steps', type=int, default=200)
+    ap.add_argument('--warmup', type=int, default=20)
     ap.add_argument('--tokens', type=int, default=8192)
     ap.add_argument('--hidden', type=int, default=7168)
     ap.add_argument('--topk', type=int, default=8)
     ap.add_argument('--experts', type=int, default=256)
     ap.add_argument('--plain', action='store_true', help='reference (unweighted) combine instead of weighted')
+    ap.add_argument('--fp8-dispatch', action='store_true', help='BASELINE config 4: FP8 e4m3 dispatch, BF16 combine')
+    ap.add_argument('--skew', type=float, default=1.0, help='BASELINE config 5: rank-0 overload ratio (e.g. 4)')
     ap.add_argument('--cpu-seconds', type=float, default=10.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-loopback', action='store_true')
@@ -105,13 +107,21 @@ def main():
     weighted = not args.plain
     dev = torch.device('cuda', torch.cuda.current_device())
     torch.manual_seed(0 + rank)
-    scores = torch.rand((T, E), device=dev)
+    if args.skew != 1.0:
+        from deepep_amd.utils import get_unbalanced_scores
+        scores = get_unbalanced_scores(T, E, world, K, args.skew, device=dev)
+    else:
+        scores = torch.rand((T, E), device=dev)
     topk_w, topk_idx = torch.topk(scores, K, dim=-1, sorted=False)
     topk_idx = topk_idx.to(torch.int64)
     x = torch.randn((T, H), device=dev).to(torch.bfloat16)
     buf = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=T, hidden=H, num_topk=K)
+    if args.fp8_dispatch:
+        from deepep_amd.utils import per_token_cast_to_fp8
+        x = per_token_cast_to_fp8(x)
     ex_x, _, ex_w, handle, _ = buf.dispatch(x, topk_idx=topk_idx, topk_weights=topk_w, num_experts=E, do_expand=True)
-    y = torch.randn(ex_x.shape, device=dev).to(torch.bfloat16)          # expert outputs, expanded layout
+    ex_shape = (ex_x[0] if isinstance(ex_x, tuple) else ex_x).shape
+    y = torch.randn(ex_shape, device=dev).to(torch.bfloat16)            # expert outputs, expanded layout
     del ex_x, x
     valid = int((topk_idx >= 0).sum().item())
     bytes_rank = valid * H * 2 + T * H * 2 + valid * 4 + valid * 4
@@ -232,7 +242,8 @@ def main():
             'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 4), 'higher_is_better': True,
             'scaling': 'weak', 'vs_baseline': None, 'dtype': 'bf16 (fp32 accumulate)', 'data': 'synthetic',
             'config': {'workload': f'EP={world} combine, {T} tokens/rank x hidden {H} x top-{K}, '
-                                   f'{E} experts, uniform routing, expanded layout, '
+                                   f'{E} experts, {"skewed x%g" % args.skew if args.skew != 1.0 else "uniform"} routing, '
+                                   f'{"FP8 dispatch, " if args.fp8_dispatch else ""}expanded layout, '
                                    f'{"gating-weighted" if weighted else "plain (reference semantics)"}',
                        'tokens_per_rank': T, 'hidden': H, 'topk': K, 'experts': E,
                        'parallelism': f'ep{world}'},

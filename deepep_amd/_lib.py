@@ -11,7 +11,7 @@ from typing import Optional
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('DEEPEP_AMD_LIB', os.path.join(_HERE, 'libdeepep_amd.so'))
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 MODE_LOCAL, MODE_EPILOGUE, MODE_FUSED = 0, 1, 2
 
@@ -35,6 +35,7 @@ SIGNATURES = {
                                    _I, _I,
                                    _P, _I64,
                                    _P, _P, _I,
+                                   _I64,
                                    _I, _P,
                                    _P]),
     'deepep_build_local_plan': (_I, [_P, _I, _I, _I, _I, _P, _I, _I, _P, _P, _P]),

@@ -25,7 +25,7 @@ import torch
 import torch.distributed as dist
 
 from .event import EventHandle, EventOverlap
-from .handle import CombinePlan, EPHandle, epilogue_tables, single_reduction_tables
+from .handle import CombinePlan, EPHandle, epilogue_tables, single_reduction_tables, weight_table
 from .kernels import MODE_EPILOGUE, MODE_FUSED, MODE_LOCAL
 from .utils import align, ceil_div, value_or
 
@@ -511,7 +511,8 @@ class ElasticBuffer:
             cs = csum[torch.tensor(bounds, device=csum.device)].tolist()
             plan.send_counts1 = [int(cs[i + 1] - cs[i]) for i in range(R)]
         else:
-            plan.table_b, plan.wtable_b, plan.back_counts = epilogue_tables(handle.topk_idx, handle.num_experts, R)
+            plan.table_b, plan.row_of_lane, plan.back_counts = epilogue_tables(handle.topk_idx, handle.num_experts, R)
+            plan.wtables = {}
         handle._combine_plans[key] = plan
         return plan
 
@@ -617,26 +618,33 @@ class ElasticBuffer:
                 kern.combine_reduce(MODE_EPILOGUE, recv, combined_x, T, table=plan.table_b1,
                                     bias0=bias_0, bias1=bias_1, stream=stream)
             else:
+                # One packed row per (token, expert rank): [bf16 partial | fp32 top-k weights], 16-byte
+                # aligned, so the partials and the weight pass-through move in ONE all-to-all.
                 n_recv = sum(plan.recv_counts)
-                partial = torch.empty((n_recv, hidden), dtype=x.dtype, device=x.device)
-                partial_w = torch.empty((n_recv, K), dtype=torch.float32, device=x.device) if topk_weights is not None else None
+                w_elems = 0 if topk_weights is None else align(K * 4, 16) // 2
+                row_elems = hidden + w_elems
+                packed = torch.empty((n_recv, row_elems), dtype=x.dtype, device=x.device)
+                partial = packed[:, :hidden]
+                partial_w = packed[:, hidden:].view(torch.float32)[:, :K] if w_elems else None
                 table_a = meta[:n_recv, 2:] if expanded else None
                 self._mark(stream)
                 kern.combine_reduce(MODE_LOCAL, x, partial, n_recv, table=table_a, row_weights=row_w,
                                     wtable=table_a, wsrc=wsrc, out_weights=partial_w, stream=stream)
                 self._mark(stream)
                 n_back = sum(plan.back_counts)
-                recv = torch.empty((n_back, hidden), dtype=x.dtype, device=x.device)
-                self._all_to_all(recv, partial, plan.back_counts, plan.recv_counts)
-                recv_w = None
-                if partial_w is not None:
-                    recv_w = torch.empty((n_back, K), dtype=torch.float32, device=x.device)
-                    self._all_to_all(recv_w, partial_w, plan.back_counts, plan.recv_counts)
+                recv = torch.empty((n_back, row_elems), dtype=x.dtype, device=x.device)
+                self._all_to_all(recv, packed, plan.back_counts, plan.recv_counts)
+                wtable_b, recv_wsrc = None, None
+                if w_elems:
+                    key = (row_elems // 2, hidden // 2)
+                    if key not in plan.wtables:
+                        plan.wtables[key] = weight_table(plan.row_of_lane, *key)
+                    wtable_b = plan.wtables[key]
+                    recv_wsrc = recv.view(torch.float32).view(-1)
                 self._before_epilogue(previous_event_before_epilogue)
                 self._mark(stream)
-                kern.combine_reduce(MODE_EPILOGUE, recv, combined_x, T, table=plan.table_b,
-                                    bias0=bias_0, bias1=bias_1, wtable=plan.wtable_b,
-                                    wsrc=recv_w.view(-1) if recv_w is not None else None,
+                kern.combine_reduce(MODE_EPILOGUE, recv[:, :hidden], combined_x, T, table=plan.table_b,
+                                    bias0=bias_0, bias1=bias_1, wtable=wtable_b, wsrc=recv_wsrc,
                                     out_weights=combined_w, stream=stream)
                 self._mark(stream)
         event = None

@@ -91,6 +91,7 @@ struct Params {
     const float* wsrc;
     float* out_weights;
     int num_weights;
+    int64_t out_weights_stride;  // floats between consecutive units' weight rows
     int units_per_block;
     int32_t* error_flag;
 };
@@ -194,7 +195,7 @@ combine_rows_kernel(const Params p) {
     if (c == 0 && p.out_weights != nullptr && lane < p.num_weights) {
         const int64_t i = p.wtable == nullptr ? u * p.num_weights + lane
                                               : static_cast<int64_t>(p.wtable[u * p.wtable_stride + lane]);
-        p.out_weights[u * p.num_weights + lane] = i >= 0 ? p.wsrc[i] : 0.0f;
+        p.out_weights[u * p.out_weights_stride + lane] = i >= 0 ? p.wsrc[i] : 0.0f;
     }
 
     int vidx[kVPT];
@@ -378,6 +379,7 @@ int deepep_combine_reduce(int mode, int weighted,
                           int num_units, int hidden,
                           const int32_t* wtable, int64_t wtable_stride,
                           const float* wsrc, float* out_weights, int num_weights,
+                          int64_t out_weights_stride,
                           int units_per_block, int32_t* error_flag,
                           deepep_stream_t stream) {
     if (mode < DEEPEP_MODE_LOCAL || mode > DEEPEP_MODE_FUSED)
@@ -401,6 +403,10 @@ int deepep_combine_reduce(int mode, int weighted,
         return set_error(DEEPEP_ERR_INVALID_ARG, "bias is applied by the epilogue, not the local reduce");
     if (out_weights != nullptr && (wsrc == nullptr || num_weights < 1 || num_weights > kMaxWidth))
         return set_error(DEEPEP_ERR_INVALID_ARG, "weight pass-through needs wsrc and 1 <= num_weights <= %d", kMaxWidth);
+    if (out_weights_stride == 0) out_weights_stride = num_weights;
+    if (out_weights != nullptr && out_weights_stride < num_weights)
+        return set_error(DEEPEP_ERR_INVALID_ARG, "out_weights_stride (%lld) < num_weights (%d)",
+                         static_cast<long long>(out_weights_stride), num_weights);
     Params p;
     p.src = static_cast<const uint16_t*>(src);
     p.num_src_rows = num_src_rows;
@@ -420,6 +426,7 @@ int deepep_combine_reduce(int mode, int weighted,
     p.wsrc = wsrc;
     p.out_weights = out_weights;
     p.num_weights = num_weights;
+    p.out_weights_stride = out_weights_stride;
     p.units_per_block = units_per_block;
     p.error_flag = error_flag;
 

@@ -34,7 +34,8 @@ class CombinePlan:
     recv_counts: Optional[List[int]] = None           # rows this rank holds per source rank (phase A output)
     back_counts: Optional[List[int]] = None           # partial rows this rank receives per expert rank
     table_b: Optional[torch.Tensor] = None            # [T, min(R, K)] rows of the receive buffer, master order
-    wtable_b: Optional[torch.Tensor] = None           # [T, K] row * K + k, or -1
+    row_of_lane: Optional[torch.Tensor] = None        # [T, K] receive row holding lane k's weight, or -1
+    wtables: Optional[dict] = None                    # packed-row weight tables, keyed by (row floats, offset)
     # EP > 1, single reduction (allow_multiple_reduction=False, expanded): rows sent unreduced
     send_slots1: Optional[torch.Tensor] = None        # [N_send, 1] expanded rows in send order
     send_counts1: Optional[List[int]] = None
@@ -69,10 +70,18 @@ def epilogue_tables(topk_idx: torch.Tensor, num_experts: int, num_ranks: int):
     key = torch.where(is_to, master, K + ranks.view(1, R))
     order = torch.argsort(key, dim=1, stable=True)[:, :min(R, K)]
     table_b = row.gather(1, order).to(torch.int32).contiguous()
-    k_idx = torch.arange(K, device=dev).view(1, K)
-    row_of_lane = row.gather(1, rank_of.clamp(min=0))
-    wtable_b = torch.where(rank_of >= 0, row_of_lane * K + k_idx, torch.full_like(row_of_lane, -1))
-    return table_b, wtable_b.to(torch.int32).contiguous(), [int(v) for v in back_counts.tolist()]
+    row_of_lane = torch.where(rank_of >= 0, row.gather(1, rank_of.clamp(min=0)), torch.full_like(rank_of, -1))
+    return table_b, row_of_lane.contiguous(), [int(v) for v in back_counts.tolist()]
+
+
+def weight_table(row_of_lane: torch.Tensor, row_floats: int, offset: int) -> torch.Tensor:
+    """[T, K] int32 index of lane k's weight in a float view of packed receive rows
+    (row r's weights start at r * row_floats + offset), or -1."""
+    K = row_of_lane.shape[1]
+    k_idx = torch.arange(K, device=row_of_lane.device).view(1, K)
+    idx = torch.where(row_of_lane >= 0, row_of_lane * row_floats + offset + k_idx, torch.full_like(row_of_lane, -1))
+    assert int(idx.max().item()) < 2 ** 31 if idx.numel() else True
+    return idx.to(torch.int32).contiguous()
 
 
 def single_reduction_tables(topk_idx: torch.Tensor, num_experts: int, num_ranks: int):

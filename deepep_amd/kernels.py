@@ -65,12 +65,15 @@ class HipKernels:
             _require(t.shape[0] >= num_units, 'slot table has fewer rows than units')
         w, w_stride, _ = _table_view(wtable)
         num_weights = 0
+        ow_stride = 0
         if out_weights is not None:
-            _require(out_weights.dtype == torch.float32 and out_weights.is_contiguous() and out_weights.dim() == 2,
-                     'weights must be contiguous float32 [units, k]')
+            _require(out_weights.dtype == torch.float32 and out_weights.dim() == 2 and out_weights.stride(1) == 1,
+                     'weights must be float32 [units, k] with unit column stride')
+            _require(out_weights.shape[0] >= num_units, 'weight output has fewer rows than units')
             num_weights = out_weights.shape[1]
-            _require(wsrc is not None and wsrc.dtype == torch.float32 and wsrc.is_contiguous(),
-                     'weight source must be contiguous float32')
+            ow_stride = out_weights.stride(0)
+            _require(wsrc is not None and wsrc.dtype == torch.float32 and wsrc.dim() == 1 and wsrc.stride(0) == 1,
+                     'weight source must be a 1-D float32 view')
         weighted = row_weights is not None
         if weighted:
             _require(row_weights.dtype == torch.float32 and row_weights.is_contiguous(),
@@ -84,7 +87,7 @@ class HipKernels:
             ptr(out), out.stride(0) if out.shape[0] > 0 else hidden,
             num_units, hidden,
             ptr(w), w_stride,
-            ptr(wsrc), ptr(out_weights), num_weights,
+            ptr(wsrc), ptr(out_weights), num_weights, ow_stride,
             units_per_block, ptr(error_flag),
             _stream_handle(stream))
         _lib.check(rc, 'combine_reduce')

@@ -40,7 +40,7 @@ extern "C" {
 
 typedef struct ihipStream_t* deepep_stream_t;   /* == hipStream_t */
 
-#define DEEPEP_AMD_ABI_VERSION 1
+#define DEEPEP_AMD_ABI_VERSION 2
 
 #define DEEPEP_OK               0
 #define DEEPEP_ERR_INVALID_ARG  (-1)
@@ -69,9 +69,11 @@ const char* deepep_amd_last_error(void);
  *                     (legacy low_latency_combine semantics, csrc/kernels/legacy/
  *                     internode_ll.cu:1072-1135); modes LOCAL and FUSED only
  *   bias0, bias1   bf16 [num_units][hidden] or NULL (modes EPILOGUE and FUSED)
- *   out_weights    fp32 [num_units][num_weights] or NULL: top-k weight pass-through,
- *                  out_weights[u][k] = (i = wtable ? wtable[u*wtable_stride + k]
- *                                            : u*num_weights + k) >= 0 ? wsrc[i] : 0
+ *   out_weights    fp32 rows of out_weights_stride floats (0 = num_weights) or NULL: top-k
+ *                  weight pass-through, written once per unit:
+ *                  out_weights[u*out_weights_stride + k] = (i = wtable ? wtable[u*wtable_stride + k]
+ *                                                             : u*num_weights + k) >= 0 ? wsrc[i] : 0
+ *                  (a stride lets the weights ride in the tail of packed exchange rows)
  *   units_per_block  reserved (0); the launch tiles (row, column-chunk) items, 4 per workgroup
  *   error_flag     device int or NULL; set to 1 when a slot is >= num_src_rows
  *                  (such slots are skipped, never dereferenced)
@@ -85,6 +87,7 @@ int deepep_combine_reduce(int mode, int weighted,
                           int num_units, int hidden,
                           const int32_t* wtable, int64_t wtable_stride,
                           const float* wsrc, float* out_weights, int num_weights,
+                          int64_t out_weights_stride,
                           int units_per_block, int32_t* error_flag,
                           deepep_stream_t stream);
 

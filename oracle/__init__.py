@@ -49,7 +49,7 @@ def _get_lib():
         lib.oracle_combine_phase_a.argtypes = [P, I64, I, P, I, I, I, P, I, P, P]
         lib.oracle_combine_phase_b.argtypes = [P, P, I, I, P, I, I, I, I, I, I, P, P, I, P, P]
         lib.oracle_combine_weighted_ll.argtypes = [P, P, P, I, I, I, P]
-        lib.oracle_combine_rows.argtypes = [I, I, P, I64, I64, P, I64, I, P, P, P, P, I64, I, I, P, I64, P, P, I]
+        lib.oracle_combine_rows.argtypes = [I, I, P, I64, I64, P, I64, I, P, P, P, P, I64, I, I, P, I64, P, P, I, I64]
         for f in (lib.oracle_combine_phase_a, lib.oracle_combine_phase_b, lib.oracle_combine_weighted_ll,
                   lib.oracle_combine_rows):
             f.restype = ctypes.c_int

@@ -262,7 +262,8 @@ int oracle_combine_rows(int mode, int weighted,
                         const uint16_t* bias0, const uint16_t* bias1,
                         uint16_t* out, int64_t out_stride, int num_units, int hidden,
                         const int32_t* wtable, int64_t wtable_stride,
-                        const float* wsrc, float* out_weights, int num_weights) {
+                        const float* wsrc, float* out_weights, int num_weights,
+                        int64_t out_weights_stride) {
     const uint16_t* rows[64];
     float w[64];
     uint16_t partial[65536];
@@ -296,7 +297,8 @@ int oracle_combine_rows(int mode, int weighted,
         if (out_weights) {
             for (int k = 0; k < num_weights; ++k) {
                 const int64_t i = wtable ? wtable[(int64_t)u * wtable_stride + k] : (int64_t)u * num_weights + k;
-                out_weights[(int64_t)u * num_weights + k] = i >= 0 ? wsrc[i] : 0.0f;
+                out_weights[(int64_t)u * (out_weights_stride ? out_weights_stride : num_weights) + k] =
+                    i >= 0 ? wsrc[i] : 0.0f;
             }
         }
     }

@@ -32,7 +32,8 @@ class OracleKernels:
             _p(row_weights), _p(bias0), _p(bias1),
             _p(out), out.stride(0) if out.shape[0] else hidden, num_units, hidden,
             _p(wtable), wtable.stride(0) if wtable is not None else 0,
-            _p(wsrc), _p(out_weights), out_weights.shape[1] if out_weights is not None else 0)
+            _p(wsrc), _p(out_weights), out_weights.shape[1] if out_weights is not None else 0,
+            out_weights.stride(0) if out_weights is not None else 0)
         assert rc == 0, 'oracle_combine_rows failed'
 
     def build_local_plan(self, src_metadata, num_recv_tokens, num_topk, num_max_tokens_per_rank, expanded,

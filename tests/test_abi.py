@@ -33,33 +33,33 @@ def test_exports_every_declared_symbol(lib):
 
 
 def test_abi_version(lib):
-    assert lib.deepep_amd_abi_version() == 1
+    assert lib.deepep_amd_abi_version() == 2
 
 
 def test_invalid_arguments_are_rejected_without_a_gpu(lib):
     # mode out of range
     rc = lib.deepep_combine_reduce(7, 0, None, 0, 8, None, 0, 1, None, None, None, 16, 8, 1, 8,
-                                   None, 0, None, None, 0, 0, None, None)
+                                   None, 0, None, None, 0, 0, 0, None, None)
     assert rc == -1 and b'mode' in lib.deepep_amd_last_error()
     # hidden not a multiple of 8 elements
     rc = lib.deepep_combine_reduce(1, 0, 16, 1, 8, None, 0, 1, None, None, None, 16, 8, 1, 6,
-                                   None, 0, None, None, 0, 0, None, None)
+                                   None, 0, None, None, 0, 0, 0, None, None)
     assert rc == -1 and b'hidden' in lib.deepep_amd_last_error()
     # misaligned pointers
     rc = lib.deepep_combine_reduce(1, 0, 18, 1, 8, None, 0, 1, None, None, None, 32, 8, 1, 8,
-                                   None, 0, None, None, 0, 0, None, None)
+                                   None, 0, None, None, 0, 0, 0, None, None)
     assert rc == -1 and b'aligned' in lib.deepep_amd_last_error()
     # bias in the local phase
     rc = lib.deepep_combine_reduce(0, 0, 16, 1, 8, None, 0, 1, None, 32, None, 48, 8, 1, 8,
-                                   None, 0, None, None, 0, 0, None, None)
+                                   None, 0, None, None, 0, 0, 0, None, None)
     assert rc == -1 and b'bias' in lib.deepep_amd_last_error()
     # table width beyond top-32
     rc = lib.deepep_combine_reduce(1, 0, 16, 1, 8, 64, 40, 33, None, None, None, 48, 8, 1, 8,
-                                   None, 0, None, None, 0, 0, None, None)
+                                   None, 0, None, None, 0, 0, 0, None, None)
     assert rc == -1
     # zero units: nothing to do, success without a launch
     assert lib.deepep_combine_reduce(1, 0, 16, 1, 8, None, 0, 1, None, None, None, 48, 8, 0, 8,
-                                     None, 0, None, None, 0, 0, None, None) == 0
+                                     None, 0, None, None, 0, 0, 0, None, None) == 0
 
 
 def test_buffer_size_matches_reference_formula(lib):

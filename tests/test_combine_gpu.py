@@ -293,3 +293,71 @@ def test_config2_full_size_bitwise(weighted):
         for k in range(K):
             exact[tok] += yd[slots[:, k]] * ex_w.double()[slots[:, k]].unsqueeze(1)
         assert oracle.calc_diff(oracle.bf16_to_f32(_u16(out)), exact.cpu().numpy()) < 1e-5
+
+
+def _ep1_setup(T, H, K, E, seed=3):
+    import torch.distributed as dist
+    from deepep_amd import ElasticBuffer
+    if not dist.is_initialized():
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        os.environ.setdefault('MASTER_PORT', '29543')
+        dist.init_process_group('gloo', rank=0, world_size=1)
+    g = torch.Generator(device='cuda').manual_seed(seed)
+    scores = torch.rand((T, E), device='cuda', generator=g)
+    w, idx = torch.topk(scores, K, dim=-1, sorted=False)
+    idx = idx.to(torch.int64)
+    idx[torch.rand(idx.shape, device='cuda', generator=g) < 0.1] = -1
+    w = w.masked_fill(idx < 0, 0)
+    buf = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=T, hidden=H, num_topk=K)
+    return buf, idx, w, g
+
+
+def test_hip_graph_capture_replays_combine():
+    """The sync-mode combine is capturable into a HIP graph (torch.cuda.graph) and replays bitwise."""
+    T, H, K, E = 512, 7168, 8, 64
+    buf, idx, w, g = _ep1_setup(T, H, K, E)
+    x = torch.randn((T, H), device='cuda', generator=g).to(torch.bfloat16)
+    ex_x, _, ex_w, handle, _ = buf.dispatch(x, topk_idx=idx, topk_weights=w, num_experts=E, do_expand=True)
+    y = torch.randn(ex_x.shape, device='cuda', generator=g).to(torch.bfloat16)
+    bias = torch.randn((T, H), device='cuda', generator=g).to(torch.bfloat16)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(3):
+            buf.combine(y, handle, topk_weights=ex_w, bias=bias, apply_topk_weights=True)
+    torch.cuda.current_stream().wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        out, out_w, _ = buf.combine(y, handle, topk_weights=ex_w, bias=bias, apply_topk_weights=True)
+    y.copy_(torch.randn(y.shape, device='cuda', generator=g).to(torch.bfloat16))
+    graph.replay()
+    ref, ref_w, _ = buf.combine(y, handle, topk_weights=ex_w, bias=bias, apply_topk_weights=True)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref) and torch.equal(out_w, ref_w)
+
+
+def test_fp8_dispatch_then_bf16_combine():
+    """BASELINE config 4 at EP=1: FP8 (e4m3, per-128 scales) dispatch, BF16 combine."""
+    from deepep_amd.utils import per_token_cast_back, per_token_cast_to_fp8
+    T, H, K, E = 256, 7168, 8, 64
+    buf, idx, w, g = _ep1_setup(T, H, K, E, seed=4)
+    x = torch.randn((T, H), device='cuda', generator=g).to(torch.bfloat16)
+    xq = per_token_cast_to_fp8(x)
+    (ex_q, ex_sf), _, ex_w, handle, _ = buf.dispatch(xq, topk_idx=idx, topk_weights=w, num_experts=E,
+                                                     do_expand=True)
+    meta = handle.recv_src_metadata
+    tok = (meta[:, 0] % T).long()
+    for k in range(K):
+        rows = meta[:, 2 + k]
+        ok = rows >= 0
+        assert torch.equal(ex_q[rows[ok].long()].view(torch.uint8), xq[0][tok[ok]].view(torch.uint8))
+        assert torch.equal(ex_sf[rows[ok].long()], xq[1][tok[ok]])
+    y = per_token_cast_back(ex_q, ex_sf)                     # "expert output" = dequantised input
+    out, out_w, _ = buf.combine(y, handle, topk_weights=ex_w)
+    torch.cuda.synchronize()
+    part, _ = oracle.phase_a(_u16(y), meta.cpu().numpy(), K, True)
+    recv = np.zeros((1, T, H), np.uint16)
+    recv[0, meta[:, 0].cpu().numpy() % T] = part
+    ref, _ = oracle.phase_b(recv, None, idx.cpu().numpy(), E, 1, True, True)
+    assert np.array_equal(_u16(out), ref)
+    assert torch.equal(out_w, w)

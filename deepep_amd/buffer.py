@@ -26,7 +26,7 @@ import torch.distributed as dist
 
 from .event import EventHandle, EventOverlap
 from .handle import CombinePlan, EPHandle, epilogue_tables, single_reduction_tables, weight_table
-from .kernels import MODE_EPILOGUE, MODE_FUSED, MODE_LOCAL
+from .kernels import MODE_EPILOGUE, MODE_FUSED, MODE_LOCAL, RowLayout
 from .utils import align, ceil_div, value_or
 
 topk_idx_t = torch.int32 if int(os.environ.get('EP_NUM_TOPK_IDX_BITS', 64)) == 32 else torch.int64
@@ -341,102 +341,75 @@ class ElasticBuffer:
         K = num_topk
         epr = num_experts // R
         compute_stream = self._prologue(previous_event, allocate_on_comm_stream)
+        kern = self.kernels
         with self._stream_ctx():
             dev = x.device
-            # --- routing: destination ranks of every token, send order (rank, ascending token)
-            rank_of = torch.where(topk_idx >= 0, torch.div(topk_idx, epr, rounding_mode='floor'),
-                                  torch.full_like(topk_idx, -1))
-            is_to = (rank_of.unsqueeze(-1) == torch.arange(R, device=dev).view(1, 1, R)).any(dim=1)   # [T, R]
-            send_counts = is_to.sum(dim=0)
-            dst_slot = torch.where(is_to, torch.cumsum(is_to.to(torch.int64), 0) - 1,
-                                   torch.full(is_to.shape, -1, dtype=torch.int64, device=dev)).to(torch.int32)
-            pairs = is_to.t().nonzero()                                   # sorted by (dst rank, token)
-            send_tok = pairs[:, 1]
-            # --- counts exchange (host sync: all_to_all sizes are host values)
+            stream = torch.cuda.current_stream() if self.use_cuda else None
+            idx64 = topk_idx if topk_idx.dtype == torch.int64 else topk_idx.to(torch.int64)
+            idx64 = idx64.contiguous()
+            w = topk_weights.contiguous() if topk_weights is not None else None
+            # --- send side: destination slots (deterministic ranks), one packed row per (token, dest)
+            dst_slot = torch.empty((T, R), dtype=torch.int32, device=dev)
+            send_counts = torch.empty((R,), dtype=torch.int32, device=dev)
+            kern.dispatch_route(idx64, num_experts, R, dst_slot, send_counts, stream=stream)
             recv_counts_t = torch.empty_like(send_counts)
             self._a2a(recv_counts_t, send_counts)
-            send_counts_l = [int(v) for v in send_counts.tolist()]
+            send_counts_l = [int(v) for v in send_counts.tolist()]          # host sync, as do_cpu_sync
             recv_counts_l = [int(v) for v in recv_counts_t.tolist()]
             N = sum(recv_counts_l)
-            # --- one packed byte row per (token, destination): [x | sf | topk_idx | weights | src idx]
-            w = topk_weights if topk_weights is not None else torch.zeros(topk_idx.shape, dtype=torch.float32, device=dev)
-            src_global = (r * num_max_tokens_per_rank + torch.arange(T, device=dev)).to(torch.int32)
-            fields = [x.contiguous().view(torch.uint8).view(T, -1)]
-            if sf is not None:
-                fields.append(sf.contiguous().view(torch.uint8).view(T, -1))
-            fields += [topk_idx.contiguous().view(torch.uint8).view(T, -1),
-                       w.contiguous().view(torch.uint8).view(T, -1),
-                       src_global.view(torch.uint8).view(T, -1)]
-            widths = [f.shape[1] for f in fields]
-            row_bytes = sum(widths)
-            pad = (-row_bytes) % 16
-            if pad:
-                fields.append(torch.zeros((T, pad), dtype=torch.uint8, device=dev))
-            packed = torch.cat(fields, dim=1)[send_tok]
-            recv_packed = torch.empty((N, row_bytes + pad), dtype=torch.uint8, device=dev)
-            self._a2a(recv_packed, packed, recv_counts_l, send_counts_l)
-            off = 0
-            views = []
-            for wd in widths:
-                views.append(recv_packed[:, off:off + wd])
-                off += wd
-            it = iter(views)
-            recv_x = next(it).contiguous().view(x.dtype).view(N, H)
-            recv_sf = next(it).contiguous().view(sf.dtype).view(N, -1) if sf is not None else None
-            recv_idx_g = next(it).contiguous().view(topk_idx.dtype).view(N, K)
-            recv_w = next(it).contiguous().view(torch.float32).view(N, K)
-            recv_src = next(it).contiguous().view(torch.int32).view(N)
-            # --- local view of the received tokens
-            in_r = (recv_idx_g >= r * epr) & (recv_idx_g < (r + 1) * epr)
-            recv_topk_idx = torch.where(in_r, recv_idx_g - r * epr, torch.full_like(recv_idx_g, -1))
-            src_rank = torch.repeat_interleave(torch.arange(R, device=dev, dtype=torch.int32),
-                                               torch.tensor(recv_counts_l, device=dev, dtype=torch.int64))
-            lanes = torch.arange(K, device=dev, dtype=torch.int32).view(1, K)
-            master = torch.where(in_r, lanes, torch.full_like(lanes, -1)).amax(dim=1)
-            meta = torch.full((N, K + 2), -1, dtype=torch.int32, device=dev)
-            meta[:, 0] = recv_src
-            meta[:, 1] = src_rank * K + master
-            counts = torch.zeros(epr, dtype=torch.int64, device=dev)
-            if N:
-                counts.scatter_add_(0, recv_topk_idx[in_r], torch.ones_like(recv_topk_idx[in_r]))
-            counts_l = [int(v) for v in counts.tolist()]
+            x_bytes = x.contiguous().view(torch.uint8).view(T, H * x.element_size())
+            sf_bytes = sf.contiguous().view(torch.uint8).view(T, -1) if sf is not None else None
+            layout = RowLayout.make(x_bytes.shape[1], sf_bytes.shape[1] if sf is not None else 0, K)
+            offsets = [0] * R
+            for i in range(1, R):
+                offsets[i] = offsets[i - 1] + send_counts_l[i - 1]
+            send_offsets = torch.tensor(offsets, dtype=torch.int32, device=dev)
+            packed = torch.empty((sum(send_counts_l), layout.row_bytes), dtype=torch.uint8, device=dev)
+            kern.dispatch_pack(x_bytes, sf_bytes, idx64, w, r * num_max_tokens_per_rank, dst_slot, send_offsets,
+                               packed, layout, stream=stream)
+            if R == 1:
+                recv_packed = packed
+            else:
+                recv_packed = torch.empty((N, layout.row_bytes), dtype=torch.uint8, device=dev)
+                self._a2a(recv_packed, packed, recv_counts_l, send_counts_l)
+            # --- receive side (dispatch_copy_epilogue_impl): metadata, expert layout, copies
+            psum_rank = torch.tensor(recv_counts_l, dtype=torch.int64).cumsum(0).to(torch.int32).to(dev)
+            meta = torch.empty((N, K + 2), dtype=torch.int32, device=dev)
+            out_idx = None if do_expand else torch.empty((N, K), dtype=torch.int64, device=dev)
+            nblocks = (N + 255) // 256
+            block_counts = torch.empty((nblocks, epr), dtype=torch.int32, device=dev)
+            kern.dispatch_count(recv_packed, layout, N, r, epr, psum_rank, meta, out_idx, block_counts, stream=stream)
+            expert_counts = torch.empty((epr,), dtype=torch.int32, device=dev)
+            psum_expert = torch.empty((epr,), dtype=torch.int32, device=dev)
+            kern.dispatch_scan(block_counts, epr, expert_alignment, do_expand, expert_counts, psum_expert,
+                               stream=stream)
+            counts_l = [int(v) for v in expert_counts.tolist()]
             aligned_l = [align(c, expert_alignment) for c in counts_l]
             if cumulative_local_expert_recv_stats is not None:
-                cumulative_local_expert_recv_stats += counts.to(cumulative_local_expert_recv_stats.dtype)
-            num_unaligned = counts.to(torch.int32)
-            if not do_expand:
-                psum_expert = torch.tensor(aligned_l, dtype=torch.int64).cumsum(0).to(torch.int32).to(dev)
-                num_expanded = N
-                out_x, out_sf, out_idx, out_w = recv_x, recv_sf, recv_topk_idx, (recv_w if topk_weights is not None else None)
-            else:
-                starts = [0] * epr
-                for e in range(1, epr):
-                    starts[e] = starts[e - 1] + aligned_l[e - 1]
-                starts_t = torch.tensor(starts, dtype=torch.int64, device=dev)
-                psum_expert = (starts_t + counts).to(torch.int32)
+                cumulative_local_expert_recv_stats += expert_counts.to(cumulative_local_expert_recv_stats.dtype)
+            num_unaligned = expert_counts
+            self._before_epilogue(previous_event_before_epilogue)
+            if do_expand:
                 num_expanded = sum(aligned_l)
-                # expanded rows grouped by expert, ascending received token inside an expert
-                ii, kk = in_r.nonzero(as_tuple=True)                     # row-major: ascending token
-                ee = recv_topk_idx[ii, kk]
-                order = torch.argsort(ee * max(N, 1) + ii, stable=True)
-                ii, kk, ee = ii[order], kk[order], ee[order]
-                first = torch.cumsum(counts, 0) - counts
-                rank_in_e = torch.arange(ii.numel(), device=dev) - first[ee]
-                rows = starts_t[ee] + rank_in_e
-                meta[ii, 2 + kk] = rows.to(torch.int32)
+                kern.dispatch_slots(recv_packed, layout, N, r, epr, block_counts, meta, stream=stream)
                 alloc = torch.zeros if do_zero_padding else torch.empty
-                out_x = alloc((num_expanded, H), dtype=x.dtype, device=dev)
-                out_x[rows] = recv_x[ii]
-                out_sf = None
-                if sf is not None:
-                    out_sf = alloc((num_expanded, recv_sf.shape[1]), dtype=sf.dtype, device=dev)
-                    out_sf[rows] = recv_sf[ii]
-                out_idx = None
-                out_w = None
-                if topk_weights is not None:
-                    out_w = torch.zeros((num_expanded,), dtype=torch.float32, device=dev)
-                    out_w[rows] = recv_w[ii, kk]
-            psum_rank = torch.tensor(recv_counts_l, dtype=torch.int64).cumsum(0).to(torch.int32).to(dev)
+                n_rows = num_expanded
+            else:
+                num_expanded = N
+                meta[:, 2:] = -1
+                alloc = torch.empty
+                n_rows = N
+            out_x = alloc((n_rows, H), dtype=x.dtype, device=dev)
+            out_sf = alloc((n_rows, sf.shape[1]), dtype=sf.dtype, device=dev) if sf is not None else None
+            out_w = None
+            if topk_weights is not None:
+                out_w = (torch.zeros((n_rows,), dtype=torch.float32, device=dev) if do_expand else
+                         torch.empty((N, K), dtype=torch.float32, device=dev))
+            kern.dispatch_copy(recv_packed, layout, N, meta, do_expand,
+                               out_x.view(torch.uint8), out_sf.view(torch.uint8) if out_sf is not None else None,
+                               out_w, stream=stream)
+            if out_idx is not None and topk_idx.dtype != torch.int64:
+                out_idx = out_idx.to(topk_idx.dtype)
             num_recv = N
             if not do_cpu_sync and handle is None:
                 # Worst-case shapes, as the reference allocates without a CPU sync (buffer.hpp:1065-1070)
@@ -448,11 +421,11 @@ class ElasticBuffer:
                     if out_w is not None:
                         out_w = torch.cat([out_w, torch.zeros((worst - N, K), dtype=torch.float32, device=dev)])
                     if out_sf is not None:
-                        out_sf = torch.cat([out_sf, torch.zeros((worst - N, out_sf.shape[1]), dtype=out_sf.dtype, device=dev)])
+                        out_sf = torch.cat([out_sf, torch.zeros((worst - N, out_sf.shape[1]), dtype=out_sf.dtype,
+                                                                device=dev)])
                     num_expanded = worst
                 num_recv = worst
             cloned_idx = topk_idx.clone() if do_handle_copy else topk_idx
-        self._before_epilogue(previous_event_before_epilogue)
         event = self._epilogue([x, sf, topk_idx, topk_weights, out_x, out_sf, out_idx, out_w, meta],
                                compute_stream, allocate_on_comm_stream, async_with_compute_stream)
         is_cached = handle is not None

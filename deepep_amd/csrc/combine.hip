@@ -366,6 +366,11 @@ __global__ void local_plan_kernel(const int32_t* meta, int num_recv, int num_top
 
 extern "C" {
 
+// Error reporting shared with dispatch.hip (not part of the public C-ABI).
+__attribute__((visibility("hidden"))) int deepep_amd_set_error(int code, const char* msg) {
+    return set_error(code, "%s", msg);
+}
+
 int deepep_amd_abi_version(void) { return DEEPEP_AMD_ABI_VERSION; }
 
 const char* deepep_amd_last_error(void) { return g_last_error; }

@@ -1,0 +1,366 @@
+// dispatch.hip -- the handle producer of the combine path (ElasticBuffer.dispatch) on MI355X.
+//
+// Reference (paths in /root/reference):
+//   dispatch_impl                deep_ep/include/deep_ep/impls/dispatch.cuh:17-409
+//     notify: per-rank / per-expert counts, slot per destination (:79-258, :336-351)
+//     push:   [hidden | sf | topk_idx | weights | src_global_idx] per (token, destination) (:373-392)
+//   dispatch_copy_epilogue_impl  deep_ep/include/deep_ep/impls/dispatch_copy_epilogue.cuh:11-323
+//     recv_x / recv_sf / recv_topk_weights, expanded rows grouped by local expert (:112-123),
+//     recv_src_metadata = {src_global_idx, src_rank * K + master_topk, slot_0..slot_{K-1}} (:188-207)
+//
+// Design (MI355X-first): the exchange between ranks is one RCCL all_to_all_single of packed byte
+// rows (host side); these kernels are the byte work around it.  The slot a token gets inside a
+// destination / an expert is its rank among earlier tokens (ascending token order), computed with
+// block scans and per-wave ballot masks instead of atomics, so the receive order is deterministic:
+// grouped by source rank, ascending source token -- refs.dispatch's order and the reference's
+// deterministic mode -- which the combine plan relies on.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <stdio.h>
+
+#include "../../include/deepep_amd.h"
+
+extern "C" __attribute__((visibility("hidden"))) int deepep_amd_set_error(int code, const char* msg);
+
+namespace {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// ---------------------------------------------------------------- route: token -> destination slots
+// One workgroup of 1024 threads.  dst_slot[t][r] = #{t' < t : t' routed to r} or -1;
+// send_counts[r] = #{t : t routed to r}.  (dispatch.cuh:79-258 notify + slot assignment.)
+__global__ void __launch_bounds__(1024)
+route_kernel(const int64_t* __restrict__ topk_idx, int T, int K, int epr, int R,
+             int32_t* __restrict__ dst_slot, int32_t* __restrict__ send_counts) {
+    __shared__ int32_t s_scan[1024];
+    const int tid = threadIdx.x;
+    const int per = (T + 1023) / 1024;
+    const int t0 = tid * per, t1 = min(T, t0 + per);
+    for (int r = 0; r < R; ++r) {
+        int c = 0;
+        for (int t = t0; t < t1; ++t) {
+            bool hit = false;
+            for (int k = 0; k < K; ++k) {
+                const int64_t e = topk_idx[static_cast<int64_t>(t) * K + k];
+                hit |= e >= 0 && e / epr == r;
+            }
+            c += hit;
+        }
+        s_scan[tid] = c;
+        __syncthreads();
+        for (int off = 1; off < 1024; off <<= 1) {          // inclusive Hillis-Steele scan
+            const int v = tid >= off ? s_scan[tid - off] : 0;
+            __syncthreads();
+            s_scan[tid] += v;
+            __syncthreads();
+        }
+        int base = s_scan[tid] - c;
+        if (tid == 1023) send_counts[r] = s_scan[1023];
+        for (int t = t0; t < t1; ++t) {
+            bool hit = false;
+            for (int k = 0; k < K; ++k) {
+                const int64_t e = topk_idx[static_cast<int64_t>(t) * K + k];
+                hit |= e >= 0 && e / epr == r;
+            }
+            dst_slot[static_cast<int64_t>(t) * R + r] = hit ? base++ : -1;
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------- pack: one wave per token
+// packed row layout (bytes): [x | sf @sf_off | topk_idx (int64) @idx_off | weights @w_off | src @src_off]
+__global__ void __launch_bounds__(64)
+pack_kernel(const uint8_t* __restrict__ x, int64_t x_stride, int x_bytes,
+            const uint8_t* __restrict__ sf, int64_t sf_stride, int sf_bytes,
+            const int64_t* __restrict__ topk_idx, const float* __restrict__ topk_weights, int K,
+            int32_t src_base, const int32_t* __restrict__ dst_slot, const int32_t* __restrict__ send_offsets, int R,
+            uint8_t* __restrict__ packed, int64_t row_bytes, int sf_off, int idx_off, int w_off, int src_off) {
+    const int t = blockIdx.x, lane = threadIdx.x;
+    // lane r holds the destination row for rank r; the set bits of `dmask` are the destinations
+    int64_t my_row = -1;
+    if (lane < R) {
+        const int32_t s = dst_slot[static_cast<int64_t>(t) * R + lane];
+        if (s >= 0) my_row = static_cast<int64_t>(send_offsets[lane]) + s;
+    }
+    const uint64_t dmask = __ballot(my_row >= 0);
+    auto row_of = [&](int r) -> uint8_t* {
+        const int64_t lo = __builtin_amdgcn_readlane(static_cast<int>(my_row & 0xffffffff), r);
+        const int64_t hi = __builtin_amdgcn_readlane(static_cast<int>(my_row >> 32), r);
+        return packed + ((hi << 32) | (lo & 0xffffffff)) * row_bytes;
+    };
+    const u32x4* xs = reinterpret_cast<const u32x4*>(x + t * x_stride);
+    for (int v = lane; v < x_bytes / 16; v += 64) {
+        const u32x4 val = __builtin_nontemporal_load(xs + v);
+        for (uint64_t m = dmask; m; m &= m - 1)
+            reinterpret_cast<u32x4*>(row_of(__builtin_ctzll(m)))[v] = val;
+    }
+    for (int v = lane; v < sf_bytes / 4; v += 64) {
+        const uint32_t val = reinterpret_cast<const uint32_t*>(sf + t * sf_stride)[v];
+        for (uint64_t m = dmask; m; m &= m - 1)
+            reinterpret_cast<uint32_t*>(row_of(__builtin_ctzll(m)) + sf_off)[v] = val;
+    }
+    int64_t e = 0;
+    float w = 0.0f;
+    if (lane < K) {
+        e = topk_idx[static_cast<int64_t>(t) * K + lane];
+        w = topk_weights != nullptr ? topk_weights[static_cast<int64_t>(t) * K + lane] : 0.0f;
+    }
+    for (uint64_t m = dmask; m; m &= m - 1) {
+        uint8_t* row = row_of(__builtin_ctzll(m));
+        if (lane < K) {
+            reinterpret_cast<int64_t*>(row + idx_off)[lane] = e;
+            reinterpret_cast<float*>(row + w_off)[lane] = w;
+        }
+        if (lane == 0) *reinterpret_cast<int32_t*>(row + src_off) = src_base + t;
+    }
+}
+
+// ---------------------------------------------------------------- receive side
+__device__ __forceinline__ int local_expert(int64_t e, int rank, int epr) {
+    return (e >= static_cast<int64_t>(rank) * epr && e < static_cast<int64_t>(rank + 1) * epr)
+               ? static_cast<int>(e - static_cast<int64_t>(rank) * epr) : -1;
+}
+
+// One thread per received row, 256 rows per workgroup: metadata columns 0-1, the local top-k
+// indices (non-expanded recv_topk_idx) and per-workgroup expert histograms.
+__global__ void __launch_bounds__(256)
+count_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int idx_off, int src_off, int N, int K,
+             int rank, int epr, const int32_t* __restrict__ rank_psum, int R,
+             int32_t* __restrict__ meta, int64_t* __restrict__ recv_topk_idx, int32_t* __restrict__ block_counts) {
+    extern __shared__ int32_t s_hist[];                 // [epr]
+    for (int e = threadIdx.x; e < epr; e += 256) s_hist[e] = 0;
+    __syncthreads();
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < N) {
+        const uint8_t* row = packed + static_cast<int64_t>(i) * row_bytes;
+        const int64_t* idx = reinterpret_cast<const int64_t*>(row + idx_off);
+        int src_rank = 0;
+        while (src_rank < R - 1 && i >= rank_psum[src_rank]) ++src_rank;
+        int master = -1;
+        for (int k = 0; k < K; ++k) {
+            const int le = local_expert(idx[k], rank, epr);
+            if (le >= 0) {
+                master = k;
+                atomicAdd(&s_hist[le], 1);
+            }
+            if (recv_topk_idx != nullptr) recv_topk_idx[static_cast<int64_t>(i) * K + k] = le;
+        }
+        const int64_t mrow = static_cast<int64_t>(i) * (K + 2);
+        meta[mrow] = *reinterpret_cast<const int32_t*>(row + src_off);
+        meta[mrow + 1] = src_rank * K + master;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < epr; e += 256)
+        block_counts[static_cast<int64_t>(blockIdx.x) * epr + e] = s_hist[e];
+}
+
+// One thread per local expert: offsets of every workgroup inside the expert's group, expert starts
+// aligned to expert_alignment, and the handle's prefix sums (elastic.py:36-45 semantics).
+__global__ void __launch_bounds__(1024)
+scan_kernel(int32_t* __restrict__ block_counts, int nblocks, int epr, int align, int expanded,
+            int32_t* __restrict__ expert_counts, int32_t* __restrict__ psum_expert) {
+    __shared__ int32_t s_aligned[1024];
+    __shared__ int32_t s_start[1024];
+    const int e = threadIdx.x;
+    int total = 0;
+    if (e < epr) {
+        for (int b = 0; b < nblocks; ++b) {             // exclusive scan over workgroups, in place
+            const int c = block_counts[static_cast<int64_t>(b) * epr + e];
+            block_counts[static_cast<int64_t>(b) * epr + e] = total;
+            total += c;
+        }
+        expert_counts[e] = total;
+    }
+    s_aligned[e] = e < epr ? (total + align - 1) / align * align : 0;
+    __syncthreads();
+    if (e == 0) {                                       // epr <= 1024: a serial scan is fine here
+        int run = 0;
+        for (int j = 0; j < epr; ++j) {
+            s_start[j] = run;
+            run += s_aligned[j];
+        }
+    }
+    __syncthreads();
+    if (e < epr) {
+        psum_expert[e] = expanded ? s_start[e] + total : s_start[e] + s_aligned[e];
+        for (int b = 0; b < nblocks; ++b)
+            block_counts[static_cast<int64_t>(b) * epr + e] += s_start[e];
+    }
+}
+
+// Expanded slot of every (row, local lane): the expert group's offset for this workgroup plus the
+// number of earlier rows of the workgroup holding the same expert (per-wave 64-bit ballot masks in
+// LDS).  A token never holds one expert twice, so this is the ascending-token order.
+__global__ void __launch_bounds__(256)
+slots_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int idx_off, int N, int K, int rank, int epr,
+             const int32_t* __restrict__ block_offsets, int32_t* __restrict__ meta) {
+    extern __shared__ uint64_t s_bits[];                // [epr][4]
+    for (int j = threadIdx.x; j < epr * 4; j += 256) s_bits[j] = 0ull;
+    __syncthreads();
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t* idx = reinterpret_cast<const int64_t*>(packed + static_cast<int64_t>(i) * row_bytes + idx_off);
+    if (i < N)
+        for (int k = 0; k < K; ++k) {
+            const int le = local_expert(idx[k], rank, epr);
+            if (le >= 0) atomicOr(reinterpret_cast<unsigned long long*>(&s_bits[le * 4 + wave]), 1ull << lane);
+        }
+    __syncthreads();
+    if (i >= N) return;
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    for (int k = 0; k < K; ++k) {
+        const int le = local_expert(idx[k], rank, epr);
+        int slot = -1;
+        if (le >= 0) {
+            slot = block_offsets[static_cast<int64_t>(blockIdx.x) * epr + le];
+            for (int w = 0; w < wave; ++w) slot += __popcll(s_bits[le * 4 + w]);
+            slot += __popcll(s_bits[le * 4 + wave] & lt);
+        }
+        meta[static_cast<int64_t>(i) * (K + 2) + 2 + k] = slot;
+    }
+}
+
+// One wave per received row: x (and sf) to recv_x[i] (non-expanded) or to every local slot
+// (expanded); weights to recv_topk_weights[i][k] or [slot].
+__global__ void __launch_bounds__(64)
+copy_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int x_bytes, int sf_off, int sf_bytes, int w_off,
+            int N, int K, const int32_t* __restrict__ meta, int expanded,
+            uint8_t* __restrict__ recv_x, uint8_t* __restrict__ recv_sf, float* __restrict__ recv_w) {
+    const int i = blockIdx.x, lane = threadIdx.x;
+    const uint8_t* row = packed + static_cast<int64_t>(i) * row_bytes;
+    // lane k holds the destination row of lane k's slot (expanded) or lane 0 holds i
+    int32_t my_dst = -1;
+    if (expanded) {
+        if (lane < K) my_dst = meta[static_cast<int64_t>(i) * (K + 2) + 2 + lane];
+    } else if (lane == 0) {
+        my_dst = i;
+    }
+    const uint64_t dmask = __ballot(my_dst >= 0);
+    for (int v = lane; v < x_bytes / 16; v += 64) {
+        const u32x4 val = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(row) + v);
+        for (uint64_t m = dmask; m; m &= m - 1) {
+            const int64_t d = __builtin_amdgcn_readlane(my_dst, __builtin_ctzll(m));
+            reinterpret_cast<u32x4*>(recv_x + d * x_bytes)[v] = val;
+        }
+    }
+    if (recv_sf != nullptr)
+        for (int v = lane; v < sf_bytes / 4; v += 64) {
+            const uint32_t val = reinterpret_cast<const uint32_t*>(row + sf_off)[v];
+            for (uint64_t m = dmask; m; m &= m - 1) {
+                const int64_t d = __builtin_amdgcn_readlane(my_dst, __builtin_ctzll(m));
+                reinterpret_cast<uint32_t*>(recv_sf + d * sf_bytes)[v] = val;
+            }
+        }
+    if (recv_w != nullptr && lane < K) {
+        const float w = reinterpret_cast<const float*>(row + w_off)[lane];
+        if (expanded) {
+            if (my_dst >= 0) recv_w[my_dst] = w;
+        } else {
+            recv_w[static_cast<int64_t>(i) * K + lane] = w;
+        }
+    }
+}
+
+int launch_status(const char* what) {
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) {
+        char buf[256];
+        snprintf(buf, sizeof(buf), "%s launch failed: %s", what, hipGetErrorString(err));
+        return deepep_amd_set_error(DEEPEP_ERR_HIP, buf);
+    }
+    return DEEPEP_OK;
+}
+
+bool a16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+}  // namespace
+
+extern "C" {
+
+int deepep_dispatch_route(const int64_t* topk_idx, int num_tokens, int num_topk, int num_experts, int num_ranks,
+                          int32_t* dst_slot, int32_t* send_counts, deepep_stream_t stream) {
+    if (num_tokens < 0 || num_topk < 1 || num_topk > 32 || num_ranks < 1 || num_ranks > 64 ||
+        num_experts % num_ranks != 0 || send_counts == nullptr || (num_tokens > 0 && (dst_slot == nullptr || topk_idx == nullptr)))
+        return deepep_amd_set_error(DEEPEP_ERR_INVALID_ARG, "dispatch_route: invalid arguments");
+    hipLaunchKernelGGL(route_kernel, dim3(1), dim3(1024), 0, reinterpret_cast<hipStream_t>(stream),
+                       topk_idx, num_tokens, num_topk, num_experts / num_ranks, num_ranks, dst_slot, send_counts);
+    return launch_status("dispatch_route");
+}
+
+int deepep_dispatch_pack(const void* x, int64_t x_row_stride_bytes, int x_bytes,
+                         const void* sf, int64_t sf_row_stride_bytes, int sf_bytes,
+                         const int64_t* topk_idx, const float* topk_weights, int num_tokens, int num_topk,
+                         int32_t src_base, const int32_t* dst_slot, const int32_t* send_offsets, int num_ranks,
+                         void* packed, int64_t row_bytes, int sf_off, int idx_off, int w_off, int src_off,
+                         deepep_stream_t stream) {
+    if (num_tokens == 0) return DEEPEP_OK;
+    if (num_tokens < 0 || num_topk < 1 || num_topk > 32 || num_ranks < 1 || num_ranks > 64 || x_bytes % 16 ||
+        sf_bytes % 4 || row_bytes % 16 || !a16(x) || !a16(packed) || x_row_stride_bytes % 16 || idx_off % 8 ||
+        w_off % 4 || src_off % 4 || (sf_bytes > 0 && sf == nullptr))
+        return deepep_amd_set_error(DEEPEP_ERR_INVALID_ARG, "dispatch_pack: invalid arguments or alignment");
+    hipLaunchKernelGGL(pack_kernel, dim3(num_tokens), dim3(64), 0, reinterpret_cast<hipStream_t>(stream),
+                       static_cast<const uint8_t*>(x), x_row_stride_bytes, x_bytes,
+                       static_cast<const uint8_t*>(sf), sf_row_stride_bytes, sf_bytes,
+                       topk_idx, topk_weights, num_topk, src_base, dst_slot, send_offsets, num_ranks,
+                       static_cast<uint8_t*>(packed), row_bytes, sf_off, idx_off, w_off, src_off);
+    return launch_status("dispatch_pack");
+}
+
+int deepep_dispatch_count(const void* packed, int64_t row_bytes, int idx_off, int src_off, int num_recv, int num_topk,
+                          int rank, int num_local_experts, const int32_t* recv_rank_psum, int num_ranks,
+                          int32_t* src_metadata, int64_t* recv_topk_idx, int32_t* block_counts,
+                          deepep_stream_t stream) {
+    if (num_recv == 0) return DEEPEP_OK;                  // a rank that receives nothing
+    if (num_recv < 0 || num_topk < 1 || num_topk > 32 || num_local_experts < 1 || num_local_experts > 1024 ||
+        num_ranks < 1 || src_metadata == nullptr || block_counts == nullptr || packed == nullptr)
+        return deepep_amd_set_error(DEEPEP_ERR_INVALID_ARG, "dispatch_count: invalid arguments");
+    const int nblocks = (num_recv + 255) / 256;
+    hipLaunchKernelGGL(count_kernel, dim3(nblocks), dim3(256), num_local_experts * 4,
+                       reinterpret_cast<hipStream_t>(stream), static_cast<const uint8_t*>(packed), row_bytes,
+                       idx_off, src_off, num_recv, num_topk, rank, num_local_experts, recv_rank_psum, num_ranks,
+                       src_metadata, recv_topk_idx, block_counts);
+    return launch_status("dispatch_count");
+}
+
+int deepep_dispatch_scan(int32_t* block_counts, int num_blocks, int num_local_experts, int expert_alignment,
+                         int expanded, int32_t* expert_counts, int32_t* psum_expert, deepep_stream_t stream) {
+    if (num_blocks < 0 || num_local_experts < 1 || num_local_experts > 1024 || expert_alignment < 1 ||
+        expert_counts == nullptr || psum_expert == nullptr || (num_blocks > 0 && block_counts == nullptr))
+        return deepep_amd_set_error(DEEPEP_ERR_INVALID_ARG, "dispatch_scan: invalid arguments");
+    hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, reinterpret_cast<hipStream_t>(stream),
+                       block_counts, num_blocks, num_local_experts, expert_alignment, expanded,
+                       expert_counts, psum_expert);
+    return launch_status("dispatch_scan");
+}
+
+int deepep_dispatch_slots(const void* packed, int64_t row_bytes, int idx_off, int num_recv, int num_topk,
+                          int rank, int num_local_experts, const int32_t* block_offsets, int32_t* src_metadata,
+                          deepep_stream_t stream) {
+    if (num_recv == 0) return DEEPEP_OK;
+    if (num_recv < 0 || num_topk < 1 || num_topk > 32 || num_local_experts < 1 || num_local_experts > 1024 ||
+        packed == nullptr || block_offsets == nullptr || src_metadata == nullptr)
+        return deepep_amd_set_error(DEEPEP_ERR_INVALID_ARG, "dispatch_slots: invalid arguments");
+    const int nblocks = (num_recv + 255) / 256;
+    hipLaunchKernelGGL(slots_kernel, dim3(nblocks), dim3(256), num_local_experts * 4 * 8,
+                       reinterpret_cast<hipStream_t>(stream), static_cast<const uint8_t*>(packed), row_bytes,
+                       idx_off, num_recv, num_topk, rank, num_local_experts, block_offsets, src_metadata);
+    return launch_status("dispatch_slots");
+}
+
+int deepep_dispatch_copy(const void* packed, int64_t row_bytes, int x_bytes, int sf_off, int sf_bytes, int w_off,
+                         int num_recv, int num_topk, const int32_t* src_metadata, int expanded,
+                         void* recv_x, void* recv_sf, float* recv_topk_weights, deepep_stream_t stream) {
+    if (num_recv == 0) return DEEPEP_OK;
+    if (num_recv < 0 || num_topk < 1 || num_topk > 32 || x_bytes % 16 || row_bytes % 16 || !a16(packed) ||
+        !a16(recv_x) || (recv_sf != nullptr && sf_bytes % 4) || src_metadata == nullptr)
+        return deepep_amd_set_error(DEEPEP_ERR_INVALID_ARG, "dispatch_copy: invalid arguments or alignment");
+    hipLaunchKernelGGL(copy_kernel, dim3(num_recv), dim3(64), 0, reinterpret_cast<hipStream_t>(stream),
+                       static_cast<const uint8_t*>(packed), row_bytes, x_bytes, sf_off, sf_bytes, w_off,
+                       num_recv, num_topk, src_metadata, expanded, static_cast<uint8_t*>(recv_x),
+                       static_cast<uint8_t*>(recv_sf), recv_topk_weights);
+    return launch_status("dispatch_copy");
+}
+
+}  // extern "C"

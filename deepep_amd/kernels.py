@@ -5,14 +5,37 @@ tensors, checks dtypes/shapes/devices on the host (the checks of
 csrc/elastic/buffer.hpp:1200-1247 in the reference that concern the kernels), and
 passes raw device pointers plus the stream handle to libdeepep_amd.so.
 """
+from dataclasses import dataclass
 from typing import Optional
 
 import torch
 
 from . import _lib
 from ._lib import MODE_EPILOGUE, MODE_FUSED, MODE_LOCAL, ptr
+from .utils import align
 
-__all__ = ['HipKernels', 'MODE_LOCAL', 'MODE_EPILOGUE', 'MODE_FUSED']
+__all__ = ['HipKernels', 'RowLayout', 'MODE_LOCAL', 'MODE_EPILOGUE', 'MODE_FUSED']
+
+
+@dataclass(frozen=True)
+class RowLayout:
+    """Byte layout of one packed dispatch row (include/deepep_amd.h, dispatch section)."""
+    x_bytes: int
+    sf_bytes: int
+    num_topk: int
+    sf_off: int
+    idx_off: int
+    w_off: int
+    src_off: int
+    row_bytes: int
+
+    @staticmethod
+    def make(x_bytes: int, sf_bytes: int, num_topk: int) -> 'RowLayout':
+        sf_off = x_bytes
+        idx_off = align(sf_off + sf_bytes, 16)
+        w_off = idx_off + align(num_topk * 8, 16)
+        src_off = w_off + align(num_topk * 4, 16)
+        return RowLayout(x_bytes, sf_bytes, num_topk, sf_off, idx_off, w_off, src_off, src_off + 16)
 
 
 def _require(cond: bool, msg: str) -> None:
@@ -103,6 +126,56 @@ class HipKernels:
             ptr(src_metadata), num_recv_tokens, num_topk, num_max_tokens_per_rank, int(expanded),
             ptr(plan), plan.shape[1], num_tokens, ptr(topk_idx), ptr(wtable), _stream_handle(stream))
         _lib.check(rc, 'build_local_plan')
+
+    # ------------------------------------------------------------------ dispatch (handle producer)
+    def dispatch_route(self, topk_idx, num_experts, num_ranks, dst_slot, send_counts, stream=None):
+        _require(topk_idx.is_cuda and topk_idx.dtype == torch.int64 and topk_idx.is_contiguous(), 'topk_idx int64')
+        T, K = topk_idx.shape
+        rc = self.lib.deepep_dispatch_route(ptr(topk_idx), T, K, num_experts, num_ranks, ptr(dst_slot),
+                                            ptr(send_counts), _stream_handle(stream))
+        _lib.check(rc, 'dispatch_route')
+
+    def dispatch_pack(self, x_bytes, sf_bytes, topk_idx, topk_weights, src_base, dst_slot, send_offsets,
+                      packed, layout: RowLayout, stream=None):
+        """x_bytes / sf_bytes: [T, bytes] uint8 views (rows may be strided)."""
+        T, K = topk_idx.shape
+        rc = self.lib.deepep_dispatch_pack(
+            ptr(x_bytes), x_bytes.stride(0) if T else layout.x_bytes, layout.x_bytes,
+            ptr(sf_bytes), sf_bytes.stride(0) if sf_bytes is not None and T else 0, layout.sf_bytes,
+            ptr(topk_idx), ptr(topk_weights), T, K, src_base, ptr(dst_slot), ptr(send_offsets),
+            dst_slot.shape[1], ptr(packed), layout.row_bytes, layout.sf_off, layout.idx_off, layout.w_off,
+            layout.src_off, _stream_handle(stream))
+        _lib.check(rc, 'dispatch_pack')
+
+    def dispatch_count(self, packed, layout: RowLayout, num_recv, rank, num_local_experts, rank_psum, meta,
+                       recv_topk_idx, block_counts, stream=None):
+        rc = self.lib.deepep_dispatch_count(
+            ptr(packed), layout.row_bytes, layout.idx_off, layout.src_off, num_recv, layout.num_topk, rank,
+            num_local_experts, ptr(rank_psum), rank_psum.shape[0], ptr(meta), ptr(recv_topk_idx),
+            ptr(block_counts), _stream_handle(stream))
+        _lib.check(rc, 'dispatch_count')
+
+    def dispatch_scan(self, block_counts, num_local_experts, expert_alignment, expanded, expert_counts,
+                      psum_expert, stream=None):
+        rc = self.lib.deepep_dispatch_scan(ptr(block_counts), block_counts.shape[0], num_local_experts,
+                                           expert_alignment, int(expanded), ptr(expert_counts), ptr(psum_expert),
+                                           _stream_handle(stream))
+        _lib.check(rc, 'dispatch_scan')
+
+    def dispatch_slots(self, packed, layout: RowLayout, num_recv, rank, num_local_experts, block_offsets, meta,
+                       stream=None):
+        rc = self.lib.deepep_dispatch_slots(ptr(packed), layout.row_bytes, layout.idx_off, num_recv,
+                                            layout.num_topk, rank, num_local_experts, ptr(block_offsets),
+                                            ptr(meta), _stream_handle(stream))
+        _lib.check(rc, 'dispatch_slots')
+
+    def dispatch_copy(self, packed, layout: RowLayout, num_recv, meta, expanded, recv_x_bytes, recv_sf_bytes,
+                      recv_w, stream=None):
+        rc = self.lib.deepep_dispatch_copy(ptr(packed), layout.row_bytes, layout.x_bytes, layout.sf_off,
+                                           layout.sf_bytes, layout.w_off, num_recv, layout.num_topk, ptr(meta),
+                                           int(expanded), ptr(recv_x_bytes), ptr(recv_sf_bytes), ptr(recv_w),
+                                           _stream_handle(stream))
+        _lib.check(rc, 'dispatch_copy')
 
     def combine_buffer_size(self, num_max_tokens_per_rank: int, hidden: int, num_topk: int,
                             num_ranks: int, allow_multiple_reduction: bool) -> int:

@@ -26,6 +26,11 @@
  *       materialised once per handle
  *   deepep_combine_buffer_size
  *       ElasticBuffer::get_combine_buffer_size (csrc/elastic/buffer.hpp:616-650)
+ *   deepep_dispatch_route / _pack                    (the handle producer, send side)
+ *       dispatch_impl's notify, slot assignment and token push
+ *       (deep_ep/include/deep_ep/impls/dispatch.cuh:79-258, 336-392)
+ *   deepep_dispatch_count / _scan / _slots / _copy   (receive side)
+ *       dispatch_copy_epilogue_impl (deep_ep/include/deep_ep/impls/dispatch_copy_epilogue.cuh:11-323)
  * The Python-facing runtime call these serve is _C.ElasticBuffer.combine
  * (csrc/elastic/buffer.hpp:1179-1343), re-implemented in deepep_amd/buffer.py.
  */
@@ -116,6 +121,54 @@ int deepep_build_local_plan(const int32_t* src_metadata, int num_recv_tokens, in
  * The results are identical for every configuration; only the speed changes.
  */
 int deepep_set_launch_config(int vec_per_lane, int stage_lds, int store_policy);
+
+/* ------------------------------------------------------------------ dispatch
+ * Packed token row exchanged between ranks (byte offsets, all 16-byte aligned except as noted):
+ *   [x: x_bytes | sf @sf_off: sf_bytes | topk_idx int64[K] @idx_off | weights fp32[K] @w_off |
+ *    src_global_idx int32 @src_off], row_bytes % 16 == 0.
+ * Receive order: grouped by source rank, ascending source token (deterministic).
+ */
+
+/* dst_slot[t][r] = #{t' < t routed to rank r} or -1 (int32 [num_tokens][num_ranks]);
+ * send_counts[r] = tokens routed to rank r.  A token is routed to r when one of its top-k experts
+ * lives on r (experts_per_rank = num_experts / num_ranks). */
+int deepep_dispatch_route(const int64_t* topk_idx, int num_tokens, int num_topk, int num_experts, int num_ranks,
+                          int32_t* dst_slot, int32_t* send_counts, deepep_stream_t stream);
+
+/* Write packed row send_offsets[r] + dst_slot[t][r] for every (token t, destination r);
+ * src_global_idx = src_base + t.  topk_weights may be NULL (zeros are sent). */
+int deepep_dispatch_pack(const void* x, int64_t x_row_stride_bytes, int x_bytes,
+                         const void* sf, int64_t sf_row_stride_bytes, int sf_bytes,
+                         const int64_t* topk_idx, const float* topk_weights, int num_tokens, int num_topk,
+                         int32_t src_base, const int32_t* dst_slot, const int32_t* send_offsets, int num_ranks,
+                         void* packed, int64_t row_bytes, int sf_off, int idx_off, int w_off, int src_off,
+                         deepep_stream_t stream);
+
+/* Receive side, pass 1: src_metadata columns 0-1 ({src_global_idx, src_rank * K + master lane}),
+ * recv_topk_idx (local expert or -1, int64 [num_recv][K], may be NULL) and per-256-row expert
+ * histograms block_counts [ceil(num_recv / 256)][num_local_experts]. recv_rank_psum is the
+ * inclusive prefix sum of rows per source rank. */
+int deepep_dispatch_count(const void* packed, int64_t row_bytes, int idx_off, int src_off, int num_recv, int num_topk,
+                          int rank, int num_local_experts, const int32_t* recv_rank_psum, int num_ranks,
+                          int32_t* src_metadata, int64_t* recv_topk_idx, int32_t* block_counts,
+                          deepep_stream_t stream);
+
+/* Pass 2: block_counts becomes each 256-row block's first slot inside its expert group (expert
+ * groups start at aligned offsets); expert_counts = rows per expert; psum_expert as the reference
+ * handle's psum_num_recv_tokens_per_expert (expanded: aligned start + count; else inclusive aligned). */
+int deepep_dispatch_scan(int32_t* block_counts, int num_blocks, int num_local_experts, int expert_alignment,
+                         int expanded, int32_t* expert_counts, int32_t* psum_expert, deepep_stream_t stream);
+
+/* Pass 3 (expanded only): src_metadata columns 2.. = expanded row of every local slot, -1 elsewhere. */
+int deepep_dispatch_slots(const void* packed, int64_t row_bytes, int idx_off, int num_recv, int num_topk,
+                          int rank, int num_local_experts, const int32_t* block_offsets, int32_t* src_metadata,
+                          deepep_stream_t stream);
+
+/* Pass 4: recv_x / recv_sf rows (row i, or every local slot when expanded) and top-k weights
+ * ([num_recv][K] or, expanded, [slot]).  recv_sf / recv_topk_weights may be NULL. */
+int deepep_dispatch_copy(const void* packed, int64_t row_bytes, int x_bytes, int sf_off, int sf_bytes, int w_off,
+                         int num_recv, int num_topk, const int32_t* src_metadata, int expanded,
+                         void* recv_x, void* recv_sf, float* recv_topk_weights, deepep_stream_t stream);
 
 /* ElasticBuffer::get_combine_buffer_size for one node (num_scaleout_ranks == 1). */
 int64_t deepep_combine_buffer_size(int num_max_tokens_per_rank, int hidden, int num_topk,

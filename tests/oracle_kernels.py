@@ -52,3 +52,93 @@ class OracleKernels:
             k = torch.arange(num_topk).view(1, -1)
             ok = (topk_idx >= 0) & (inv.view(-1, 1) >= 0)
             wtable.copy_(torch.where(ok, inv.view(-1, 1) * num_topk + k, torch.full_like(topk_idx, -1)).to(torch.int32))
+
+    # ------------------------------------------------------------------ dispatch primitives (CPU stand-ins)
+    def dispatch_route(self, topk_idx, num_experts, num_ranks, dst_slot, send_counts, stream=None):
+        epr = num_experts // num_ranks
+        rank_of = torch.where(topk_idx >= 0, torch.div(topk_idx, epr, rounding_mode='floor'),
+                              torch.full_like(topk_idx, -1))
+        is_to = (rank_of.unsqueeze(-1) == torch.arange(num_ranks).view(1, 1, -1)).any(dim=1)
+        dst_slot.copy_(torch.where(is_to, torch.cumsum(is_to.to(torch.int64), 0) - 1,
+                                   torch.full(is_to.shape, -1, dtype=torch.int64)).to(torch.int32))
+        send_counts.copy_(is_to.sum(dim=0).to(torch.int32))
+
+    def dispatch_pack(self, x_bytes, sf_bytes, topk_idx, topk_weights, src_base, dst_slot, send_offsets,
+                      packed, layout, stream=None):
+        t_idx, r_idx = (dst_slot >= 0).nonzero(as_tuple=True)
+        dest = (send_offsets[r_idx] + dst_slot[t_idx, r_idx]).long()
+        K = layout.num_topk
+        packed[dest, :layout.x_bytes] = x_bytes[t_idx]
+        if sf_bytes is not None:
+            packed[dest, layout.sf_off:layout.sf_off + layout.sf_bytes] = sf_bytes[t_idx]
+        packed[dest, layout.idx_off:layout.idx_off + 8 * K] = topk_idx[t_idx].contiguous().view(torch.uint8).view(-1, 8 * K)
+        w = topk_weights if topk_weights is not None else torch.zeros(topk_idx.shape, dtype=torch.float32)
+        packed[dest, layout.w_off:layout.w_off + 4 * K] = w[t_idx].contiguous().view(torch.uint8).view(-1, 4 * K)
+        src = (src_base + t_idx).to(torch.int32)
+        packed[dest, layout.src_off:layout.src_off + 4] = src.view(torch.uint8).view(-1, 4)
+
+    @staticmethod
+    def _local(packed, layout, N, rank, epr):
+        K = layout.num_topk
+        idx = packed[:N, layout.idx_off:layout.idx_off + 8 * K].contiguous().view(torch.int64).view(N, K)
+        inr = (idx >= rank * epr) & (idx < (rank + 1) * epr)
+        return torch.where(inr, idx - rank * epr, torch.full_like(idx, -1))
+
+    def dispatch_count(self, packed, layout, num_recv, rank, num_local_experts, rank_psum, meta, recv_topk_idx,
+                       block_counts, stream=None):
+        N, K, epr = num_recv, layout.num_topk, num_local_experts
+        le = self._local(packed, layout, N, rank, epr)
+        src = packed[:N, layout.src_off:layout.src_off + 4].contiguous().view(torch.int32).view(N)
+        src_rank = torch.searchsorted(rank_psum.to(torch.int64), torch.arange(N), right=True).clamp(max=rank_psum.numel() - 1)
+        master = torch.where(le >= 0, torch.arange(K).view(1, K), torch.full_like(le, -1)).amax(dim=1)
+        meta[:N, 0] = src
+        meta[:N, 1] = (src_rank * K + master).to(torch.int32)
+        if recv_topk_idx is not None:
+            recv_topk_idx.copy_(le)
+        block_counts.zero_()
+        for b in range(block_counts.shape[0]):
+            chunk = le[b * 256:(b + 1) * 256]
+            chunk = chunk[chunk >= 0]
+            block_counts[b] += torch.bincount(chunk, minlength=epr).to(torch.int32)
+
+    def dispatch_scan(self, block_counts, num_local_experts, expert_alignment, expanded, expert_counts, psum_expert,
+                      stream=None):
+        counts = block_counts.sum(dim=0).to(torch.int64)
+        excl = torch.cumsum(block_counts.to(torch.int64), dim=0) - block_counts
+        aligned = (counts + expert_alignment - 1) // expert_alignment * expert_alignment
+        start = torch.cumsum(aligned, 0) - aligned
+        block_counts.copy_((excl + start.view(1, -1)).to(torch.int32))
+        expert_counts.copy_(counts.to(torch.int32))
+        psum_expert.copy_((start + counts if expanded else start + aligned).to(torch.int32))
+
+    def dispatch_slots(self, packed, layout, num_recv, rank, num_local_experts, block_offsets, meta, stream=None):
+        le = self._local(packed, layout, num_recv, rank, num_local_experts)
+        meta[:num_recv, 2:] = -1
+        for b in range(block_offsets.shape[0]):
+            run = block_offsets[b].clone()
+            for i in range(b * 256, min(num_recv, (b + 1) * 256)):
+                for k in range(layout.num_topk):
+                    e = int(le[i, k])
+                    if e >= 0:
+                        meta[i, 2 + k] = run[e]
+                        run[e] += 1
+
+    def dispatch_copy(self, packed, layout, num_recv, meta, expanded, recv_x_bytes, recv_sf_bytes, recv_w,
+                      stream=None):
+        N, K = num_recv, layout.num_topk
+        xs = packed[:N, :layout.x_bytes]
+        w = packed[:N, layout.w_off:layout.w_off + 4 * K].contiguous().view(torch.float32).view(N, K)
+        if not expanded:
+            recv_x_bytes[:N] = xs
+            if recv_sf_bytes is not None:
+                recv_sf_bytes[:N] = packed[:N, layout.sf_off:layout.sf_off + layout.sf_bytes]
+            if recv_w is not None:
+                recv_w[:N] = w
+            return
+        ii, kk = (meta[:N, 2:] >= 0).nonzero(as_tuple=True)
+        rows = meta[ii, 2 + kk].long()
+        recv_x_bytes[rows] = xs[ii]
+        if recv_sf_bytes is not None:
+            recv_sf_bytes[rows] = packed[ii, layout.sf_off:layout.sf_off + layout.sf_bytes]
+        if recv_w is not None:
+            recv_w[rows] = w[ii, kk]

@@ -209,6 +209,15 @@ def _buffer_case(rank, world, fixture, comm, results):
         recv_x, recv_idx, recv_w, handle, _ = buf.dispatch(x, topk_idx=idx, topk_weights=w, num_experts=E)
         n = handle.num_recv_tokens
         src = handle.recv_src_metadata[:n, 0].cpu().numpy()
+        if 'dispatch_recv_src_token_idx' in me:          # the HIP dispatch vs refs.dispatch (refs.py:10-123)
+            if not np.array_equal(src, me['dispatch_recv_src_token_idx']):
+                failures.append('dispatch order != refs.dispatch')
+            if not np.array_equal(recv_idx.cpu().numpy(), me['dispatch_recv_topk_idx']):
+                failures.append('recv_topk_idx != refs.dispatch')
+            if not np.array_equal(_u16(recv_x), me['dispatch_recv_x']):
+                failures.append('recv_x != refs.dispatch')
+            if not np.array_equal(recv_w.cpu().numpy(), me['dispatch_recv_topk_weights']):
+                failures.append('recv_topk_weights != refs.dispatch')
         local = np.stack([y_of(g) for g in src]) if n else np.zeros((0, K, H), np.uint16)
         local = np.where((recv_idx.cpu().numpy() == -1)[..., None], np.uint16(0), local)
         x_red = _bf16(ordered_accumulate(local)) if n else torch.empty((0, H), dtype=torch.bfloat16, device='cuda')

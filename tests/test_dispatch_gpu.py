@@ -1,0 +1,123 @@
+"""GPU parity of the HIP dispatch (the combine path's handle producer) against the CPU
+stand-in primitives and the reference's refs.dispatch fixtures, bitwise.
+
+Every rank of an R-rank dispatch is run on the one GPU; the all-to-all between the
+send and receive halves is done with device copies.  Checked: destination slots and
+counts, packed rows, recv_src_metadata, recv_topk_idx, expert counts / prefix sums,
+the expanded layout and the copied rows, weights and FP8 scale factors.
+"""
+import numpy as np
+import pytest
+import torch
+
+from tests.oracle_kernels import OracleKernels
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def hip():
+    from deepep_amd.kernels import HipKernels
+    return HipKernels()
+
+
+def _routing(T, E, K, R, masked, skew, gen):
+    scores = torch.rand((T, E), generator=gen)
+    if skew:
+        scores[:, :E // R] *= 3.0                       # rank 0's experts are hot
+    w, idx = torch.topk(scores, K, dim=-1, sorted=False)
+    idx = idx.to(torch.int64)
+    if masked:
+        idx[torch.rand(idx.shape, generator=gen) < masked] = -1
+        w = w.masked_fill(idx < 0, 0)
+    return idx, w
+
+
+def _run_dispatch(kern, dev, ranks, E, K, H, T_max, expanded, alignment, fp8):
+    """Both halves of the dispatch for every rank with `kern`; returns per-rank outputs on the CPU."""
+    from deepep_amd.kernels import RowLayout
+    R = len(ranks)
+    epr = E // R
+    sends = []
+    for r, (x, sf, idx, w) in enumerate(ranks):
+        T = idx.shape[0]
+        x, idx, w = x.to(dev), idx.to(dev), w.to(dev)
+        sf = sf.to(dev) if sf is not None else None
+        dst = torch.empty((T, R), dtype=torch.int32, device=dev)
+        cnt = torch.empty((R,), dtype=torch.int32, device=dev)
+        kern.dispatch_route(idx, E, R, dst, cnt)
+        cl = [int(v) for v in cnt.tolist()]
+        xb = x.view(torch.uint8).view(T, -1)
+        sb = sf.view(torch.uint8).view(T, -1) if sf is not None else None
+        layout = RowLayout.make(xb.shape[1], sb.shape[1] if sb is not None else 0, K)
+        offs = torch.tensor([sum(cl[:i]) for i in range(R)], dtype=torch.int32, device=dev)
+        packed = torch.zeros((sum(cl), layout.row_bytes), dtype=torch.uint8, device=dev)
+        kern.dispatch_pack(xb, sb, idx, w, r * T_max, dst, offs, packed, layout)
+        sends.append((dst.cpu(), cl, packed, layout))
+    outs = []
+    for r in range(R):
+        parts = [sends[s][2][sum(sends[s][1][:r]):sum(sends[s][1][:r + 1])] for s in range(R)]
+        layout = sends[r][3]
+        recv = torch.cat(parts) if parts else torch.zeros((0, layout.row_bytes), dtype=torch.uint8, device=dev)
+        N = recv.shape[0]
+        counts = [p.shape[0] for p in parts]
+        psum = torch.tensor(np.cumsum(counts), dtype=torch.int32, device=dev)
+        meta = torch.full((N, K + 2), -7, dtype=torch.int32, device=dev)
+        ridx = None if expanded else torch.empty((N, K), dtype=torch.int64, device=dev)
+        nb = (N + 255) // 256
+        bc = torch.empty((nb, epr), dtype=torch.int32, device=dev)
+        kern.dispatch_count(recv, layout, N, r, epr, psum, meta, ridx, bc)
+        ec = torch.empty((epr,), dtype=torch.int32, device=dev)
+        pe = torch.empty((epr,), dtype=torch.int32, device=dev)
+        kern.dispatch_scan(bc, epr, alignment, expanded, ec, pe)
+        aligned = [(int(c) + alignment - 1) // alignment * alignment for c in ec.tolist()]
+        if expanded:
+            kern.dispatch_slots(recv, layout, N, r, epr, bc, meta)
+            rows = sum(aligned)
+        else:
+            meta[:, 2:] = -1
+            rows = N
+        x0 = ranks[0][0]
+        rx = torch.zeros((rows, x0.shape[1]), dtype=x0.dtype, device=dev)
+        rsf = torch.zeros((rows, ranks[0][1].shape[1]), dtype=torch.float32, device=dev) if fp8 else None
+        rw = torch.zeros((rows,) if expanded else (N, K), dtype=torch.float32, device=dev)
+        kern.dispatch_copy(recv, layout, N, meta, expanded, rx.view(torch.uint8),
+                           rsf.view(torch.uint8) if rsf is not None else None, rw)
+        outs.append(dict(meta=meta.cpu(), ridx=None if ridx is None else ridx.cpu(), ec=ec.cpu(), pe=pe.cpu(),
+                         rx=rx.cpu(), rsf=None if rsf is None else rsf.cpu(), rw=rw.cpu(), dst=sends[r][0],
+                         cnt=sends[r][1]))
+    return outs
+
+
+@pytest.mark.parametrize('R,K,E,T,H,expanded,alignment,fp8,masked,skew', [
+    (1, 8, 64, 300, 7168, True, 1, False, 0.1, False),
+    (1, 2, 8, 128, 1024, False, 1, False, 0.1, False),
+    (4, 2, 16, 96, 512, True, 128, False, 0.15, False),
+    (8, 8, 64, 200, 256, True, 1, True, 0.1, False),
+    (8, 8, 256, 600, 7168, False, 1, False, 0.0, True),
+    (3, 6, 24, 257, 128, True, 4, False, 0.2, True),
+])
+def test_dispatch_primitives_match_cpu(hip, R, K, E, T, H, expanded, alignment, fp8, masked, skew):
+    from deepep_amd.utils import per_token_cast_to_fp8
+    gen = torch.Generator().manual_seed(R * 1000 + K)
+    ranks = []
+    for r in range(R):
+        idx, w = _routing(T - r, E, K, R, masked, skew, gen)
+        x = torch.randn((T - r, H), generator=gen).to(torch.bfloat16)
+        sf = None
+        if fp8:
+            x, sf = per_token_cast_to_fp8(x)
+        ranks.append((x, sf, idx, w))
+    got = _run_dispatch(hip, 'cuda', ranks, E, K, H, T, expanded, alignment, fp8)
+    exp = _run_dispatch(OracleKernels(), 'cpu', ranks, E, K, H, T, expanded, alignment, fp8)
+    for r in range(R):
+        g, e = got[r], exp[r]
+        assert torch.equal(g['dst'], e['dst']) and g['cnt'] == e['cnt'], f'rank {r} route'
+        assert torch.equal(g['meta'], e['meta']), f'rank {r} recv_src_metadata'
+        if not expanded:
+            assert torch.equal(g['ridx'], e['ridx']), f'rank {r} recv_topk_idx'
+        assert torch.equal(g['ec'], e['ec']) and torch.equal(g['pe'], e['pe']), f'rank {r} expert counts'
+        assert torch.equal(g['rx'].view(torch.uint8), e['rx'].view(torch.uint8)), f'rank {r} recv_x'
+        assert torch.equal(g['rw'], e['rw']), f'rank {r} weights'
+        if fp8:
+            assert torch.equal(g['rsf'], e['rsf']), f'rank {r} scale factors'

@@ -179,11 +179,24 @@ def main():
         torch.cuda.synchronize()
         kern_us = k0.elapsed_time(k1) * 1e3 / args.steps
         achieved = bytes_rank / (kern_us * 1e-6) / 1e9
+        # same-run memory reference: a device-to-device copy of the expanded rows (boxes differ by up
+        # to ~20 % in copy bandwidth; this contextualises `achieved`)
+        dst = torch.empty_like(y)
+        c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        dst.copy_(y)
+        c0.record(stream)
+        for _ in range(5):
+            dst.copy_(y)
+        c1.record(stream)
+        torch.cuda.synchronize()
+        copy_gbps = 2 * y.numel() * 2 * 5 / (c0.elapsed_time(c1) * 1e-3) / 1e9
+        del dst
         workload = f'combine_fused_{"weighted" if weighted else "plain"}_t{T}_h{H}_k{K}'
         roofline = dict(bound='hbm', achieved=round(achieved, 1), peak=HBM_PEAK_GBPS, unit='GB/s',
                         frac=round(achieved / HBM_PEAK_GBPS, 4), traffic=_pmc_traffic(workload),
                         kernel='combine_rows_kernel<FUSED>', kernel_us=round(kern_us, 2),
-                        bytes_per_launch=bytes_rank, in_region_us_per_step=round(comm_ms * 1e3, 2))
+                        bytes_per_launch=bytes_rank, in_region_us_per_step=round(comm_ms * 1e3, 2),
+                        same_run_d2d_copy_gbps=round(copy_gbps, 1))
 
     phases = None
     if world > 1:
@@ -211,6 +224,29 @@ def main():
                       exchange_gbps_per_rank=round(float(xb.item()) / world / (float(vals[1]) * 1e-3) / 1e9, 1),
                       note='max over ranks; reduce_only = algorithmic bytes of all ranks / (phase A + phase B); '
                            'exchange = off-rank partial rows + weights / exchange time, per rank')
+
+    # Handle producer: dispatch of the same batch, expanded layout.  Includes its
+    # host syncs (received-token counts), as the reference's dispatch with do_cpu_sync=True.
+    torch.cuda.synchronize()
+    dist.barrier()
+    n_disp = 10
+    x_disp = torch.randn((T, H), device=dev).to(torch.bfloat16)
+    if args.fp8_dispatch:
+        from deepep_amd.utils import per_token_cast_to_fp8
+        x_disp = per_token_cast_to_fp8(x_disp)
+    buf.dispatch(x_disp, topk_idx=topk_idx, topk_weights=topk_w, num_experts=E, do_expand=True)
+    torch.cuda.synchronize()
+    t_d = time.perf_counter()
+    for _ in range(n_disp):
+        buf.dispatch(x_disp, topk_idx=topk_idx, topk_weights=topk_w, num_experts=E, do_expand=True)
+    torch.cuda.synchronize()
+    t_d = (time.perf_counter() - t_d) / n_disp
+    elem = 1 if args.fp8_dispatch else 2
+    disp_bytes = T * H * elem + handle.num_expanded_tokens * H * elem     # read x once, write every expanded row
+    dispatch = dict(ms=round(t_d * 1e3, 3), gbps=round(disp_bytes / t_d / 1e9, 1),
+                    note='ElasticBuffer.dispatch(do_expand=True) wall time incl. host count syncs; '
+                         'bytes = x read once + expanded rows written')
+    del x_disp
 
     loopback = None
     if world == 1 and not args.no_loopback:
@@ -248,6 +284,7 @@ def main():
                        'tokens_per_rank': T, 'hidden': H, 'topk': K, 'experts': E,
                        'parallelism': f'ep{world}'},
             'roofline': roofline, 'cpu_baseline': cpu_baseline, 'loopback': loopback, 'phases': phases,
+            'dispatch': dispatch,
         }
         print(json.dumps(line), flush=True)
     dist.barrier()

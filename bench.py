@@ -222,7 +222,8 @@ def main():
                       phase_b_ms=round(float(vals[3]), 4),
                       reduce_only_gbps=round(total_bytes / (float(vals[0]) * 1e-3) / 1e9, 1),
                       exchange_gbps_per_rank=round(float(xb.item()) / world / (float(vals[1]) * 1e-3) / 1e9, 1),
-                      note='max over ranks; reduce_only = algorithmic bytes of all ranks / (phase A + phase B); '
+                      pipeline_chunks=buf._num_chunks(handle),
+                      note='phases measured unpipelined (1 chunk); `value` runs pipeline_chunks chunks; max over ranks; reduce_only = algorithmic bytes of all ranks / (phase A + phase B); '
                            'exchange = off-rank partial rows + weights / exchange time, per rank')
 
     # Handle producer: dispatch of the same batch, expanded layout.  Includes its

@@ -25,7 +25,7 @@ import torch
 import torch.distributed as dist
 
 from .event import EventHandle, EventOverlap
-from .handle import CombinePlan, EPHandle, epilogue_tables, single_reduction_tables, weight_table
+from .handle import CombinePlan, EPHandle, chunk_plans, epilogue_tables, single_reduction_tables, weight_table
 from .kernels import MODE_EPILOGUE, MODE_FUSED, MODE_LOCAL, RowLayout
 from .utils import align, ceil_div, value_or
 
@@ -448,8 +448,18 @@ class ElasticBuffer:
             bias_0, bias_1 = bias
         return bias_0, bias_1
 
-    def _plan(self, handle: EPHandle, single_reduction: bool) -> CombinePlan:
-        key = ('single' if single_reduction else 'multi', self.num_ranks)
+    def _num_chunks(self, handle: EPHandle) -> int:
+        """Pipeline depth of the EP > 1 combine: DEEPEP_COMBINE_CHUNKS, else 4 for batches of at
+        least 1024 tokens per rank (1 when phase instrumentation is on or on the CPU)."""
+        if self.num_ranks == 1 or self._phase_events is not None:
+            return 1
+        env = os.environ.get('DEEPEP_COMBINE_CHUNKS')
+        if env:
+            return max(1, int(env))
+        return 4 if self.use_cuda and handle.num_max_tokens_per_rank >= 1024 else 1
+
+    def _plan(self, handle: EPHandle, single_reduction: bool, num_chunks: int = 1) -> CombinePlan:
+        key = ('single' if single_reduction else 'multi', self.num_ranks) + ((num_chunks,) if num_chunks > 1 else ())
         plan = handle._combine_plans.get(key)
         if plan is not None:
             return plan
@@ -484,10 +494,82 @@ class ElasticBuffer:
             cs = csum[torch.tensor(bounds, device=csum.device)].tolist()
             plan.send_counts1 = [int(cs[i + 1] - cs[i]) for i in range(R)]
         else:
-            plan.table_b, plan.row_of_lane, plan.back_counts = epilogue_tables(handle.topk_idx, handle.num_experts, R)
-            plan.wtables = {}
+            plan.chunks = chunk_plans(meta, recv_counts, handle.topk_idx, handle.num_experts, R,
+                                      handle.num_max_tokens_per_rank, num_chunks, handle.do_expand)
+            if num_chunks == 1:
+                ch = plan.chunks[0]
+                plan.table_b, plan.row_of_lane, plan.back_counts = ch.table_b, ch.row_of_lane, ch.back_counts
+                plan.wtables = ch.wtables
         handle._combine_plans[key] = plan
         return plan
+
+    def _a2a_async(self, out: torch.Tensor, inp: torch.Tensor, out_splits: List[int], in_splits: List[int]):
+        """Row all-to-all that returns a waitable (RCCL runs it on its own stream; `wait()` makes the
+        current stream wait).  Tests on a single device replace this method."""
+        o = out.view(torch.uint8).view(out.shape[0], out.shape[1] * out.element_size())
+        i = inp.view(torch.uint8).view(inp.shape[0], inp.shape[1] * inp.element_size())
+        return dist.all_to_all_single(o, i, out_splits, in_splits, group=self.group, async_op=True)
+
+    def _combine_chunks(self, plan, x, expanded, row_w, wsrc, K, hidden, bias_0, bias_1, topk_weights,
+                        combined_x, combined_w, previous_event_before_epilogue, stream) -> None:
+        """EP > 1 combine, chunked: phase A (local reduce per received token) -> all-to-all of
+        packed rows [bf16 partial | fp32 top-k weights] -> phase B (epilogue + bias).  With more
+        than one chunk, phase A of chunk c+1 runs while RCCL moves chunk c and phase B of chunk
+        c runs on a second stream while RCCL moves chunk c+1."""
+        kern = self.kernels
+        w_elems = 0 if topk_weights is None else align(K * 4, 16) // 2
+        row_elems = hidden + w_elems
+        pipelined = len(plan.chunks) > 1 and self.use_cuda
+        if pipelined:
+            if getattr(self, '_stream_b', None) is None:
+                self._stream_b = torch.cuda.Stream(device=self.device)
+            stream_b = self._stream_b
+            stream_b.wait_stream(stream)                  # bias / outputs were produced before this call
+        in_flight = []
+        for ch in plan.chunks:
+            n_send = sum(ch.send_counts)
+            packed = torch.empty((n_send, row_elems), dtype=x.dtype, device=x.device)
+            partial_w = packed[:, hidden:].view(torch.float32)[:, :K] if w_elems else None
+            self._mark(stream)
+            kern.combine_reduce(MODE_LOCAL, x, packed[:, :hidden], n_send, table=ch.table_a, row_weights=row_w,
+                                wtable=ch.wtable_a, wsrc=wsrc, out_weights=partial_w, stream=stream)
+            self._mark(stream)
+            recv = torch.empty((sum(ch.back_counts), row_elems), dtype=x.dtype, device=x.device)
+            if pipelined:
+                work = self._a2a_async(recv, packed, ch.back_counts, ch.send_counts)
+            else:
+                self._all_to_all(recv, packed, ch.back_counts, ch.send_counts)
+                work = None
+            in_flight.append((ch, recv, packed, work))
+        self._before_epilogue(previous_event_before_epilogue)
+        if pipelined and previous_event_before_epilogue is not None:
+            previous_event_before_epilogue.stream_wait(stream_b)
+        for ch, recv, packed, work in in_flight:
+            ctx = torch.cuda.stream(stream_b) if pipelined else self._null_ctx()
+            with ctx:
+                sb = stream_b if pipelined else stream
+                if work is not None:
+                    work.wait()
+                wtable_b, recv_wsrc = None, None
+                if w_elems:
+                    key = (row_elems // 2, hidden // 2)
+                    if key not in ch.wtables:
+                        ch.wtables[key] = weight_table(ch.row_of_lane, *key)
+                    wtable_b = ch.wtables[key]
+                    recv_wsrc = recv.view(torch.float32).view(-1)
+                lo, hi = ch.lo, ch.hi
+                self._mark(sb)
+                kern.combine_reduce(MODE_EPILOGUE, recv[:, :hidden], combined_x[lo:hi], hi - lo, table=ch.table_b,
+                                    bias0=bias_0[lo:hi] if bias_0 is not None else None,
+                                    bias1=bias_1[lo:hi] if bias_1 is not None else None,
+                                    wtable=wtable_b, wsrc=recv_wsrc,
+                                    out_weights=combined_w[lo:hi] if combined_w is not None else None, stream=sb)
+                self._mark(sb)
+        if pipelined:
+            stream.wait_stream(stream_b)
+            for _, recv, packed, _ in in_flight:          # used on stream_b / the RCCL stream
+                recv.record_stream(stream_b)
+                packed.record_stream(stream_b)
 
     def combine(self,
                 x: torch.Tensor,
@@ -566,7 +648,8 @@ class ElasticBuffer:
             compute_stream = self._prologue(previous_event, allocate_on_comm_stream)
             stream = self.comm_stream
         with (self._null_ctx() if sync_mode else self._stream_ctx()):
-            plan = self._plan(handle, single_reduction)
+            num_chunks = self._num_chunks(handle) if not single_reduction else 1
+            plan = self._plan(handle, single_reduction, num_chunks)
             combined_x = torch.empty((T, hidden), dtype=x.dtype, device=x.device)
             combined_w = torch.empty((T, K), dtype=torch.float32, device=x.device) if topk_weights is not None else None
             row_w = topk_weights if apply_topk_weights else None
@@ -591,35 +674,8 @@ class ElasticBuffer:
                 kern.combine_reduce(MODE_EPILOGUE, recv, combined_x, T, table=plan.table_b1,
                                     bias0=bias_0, bias1=bias_1, stream=stream)
             else:
-                # One packed row per (token, expert rank): [bf16 partial | fp32 top-k weights], 16-byte
-                # aligned, so the partials and the weight pass-through move in ONE all-to-all.
-                n_recv = sum(plan.recv_counts)
-                w_elems = 0 if topk_weights is None else align(K * 4, 16) // 2
-                row_elems = hidden + w_elems
-                packed = torch.empty((n_recv, row_elems), dtype=x.dtype, device=x.device)
-                partial = packed[:, :hidden]
-                partial_w = packed[:, hidden:].view(torch.float32)[:, :K] if w_elems else None
-                table_a = meta[:n_recv, 2:] if expanded else None
-                self._mark(stream)
-                kern.combine_reduce(MODE_LOCAL, x, partial, n_recv, table=table_a, row_weights=row_w,
-                                    wtable=table_a, wsrc=wsrc, out_weights=partial_w, stream=stream)
-                self._mark(stream)
-                n_back = sum(plan.back_counts)
-                recv = torch.empty((n_back, row_elems), dtype=x.dtype, device=x.device)
-                self._all_to_all(recv, packed, plan.back_counts, plan.recv_counts)
-                wtable_b, recv_wsrc = None, None
-                if w_elems:
-                    key = (row_elems // 2, hidden // 2)
-                    if key not in plan.wtables:
-                        plan.wtables[key] = weight_table(plan.row_of_lane, *key)
-                    wtable_b = plan.wtables[key]
-                    recv_wsrc = recv.view(torch.float32).view(-1)
-                self._before_epilogue(previous_event_before_epilogue)
-                self._mark(stream)
-                kern.combine_reduce(MODE_EPILOGUE, recv[:, :hidden], combined_x, T, table=plan.table_b,
-                                    bias0=bias_0, bias1=bias_1, wtable=wtable_b, wsrc=recv_wsrc,
-                                    out_weights=combined_w, stream=stream)
-                self._mark(stream)
+                self._combine_chunks(plan, x, expanded, row_w, wsrc, K, hidden, bias_0, bias_1, topk_weights,
+                                     combined_x, combined_w, previous_event_before_epilogue, stream)
         event = None
         if not sync_mode:
             event = self._epilogue([x, topk_weights, bias_0, bias_1, meta, topk_idx, combined_x, combined_w, psum],

@@ -15,10 +15,24 @@ and of the reference's deterministic mode (elastic.py:117-131).  The source rank
 then compute where each of its tokens' partials lands after the exchange without
 any extra communication.
 """
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 from typing import List, Optional
 
 import torch
+
+
+@dataclass
+class ChunkPlan:
+    """One pipeline chunk of the EP > 1 combine: the source tokens [lo, hi) of every rank."""
+    lo: int
+    hi: int
+    table_a: Optional[torch.Tensor]          # expert side: [n, K] expanded slots, or [n, 1] received rows
+    wtable_a: Optional[torch.Tensor]         # expert side: [n, K] weight-source index
+    send_counts: List[int]                   # expert side: rows sent back to every source rank
+    back_counts: List[int]                   # source side: rows received from every expert rank
+    table_b: torch.Tensor                    # source side: [hi - lo, min(R, K)] rows of the chunk's receive buffer
+    row_of_lane: torch.Tensor                # source side: [hi - lo, K]
+    wtables: dict = field(default_factory=dict)
 
 
 @dataclass
@@ -36,6 +50,7 @@ class CombinePlan:
     table_b: Optional[torch.Tensor] = None            # [T, min(R, K)] rows of the receive buffer, master order
     row_of_lane: Optional[torch.Tensor] = None        # [T, K] receive row holding lane k's weight, or -1
     wtables: Optional[dict] = None                    # packed-row weight tables, keyed by (row floats, offset)
+    chunks: Optional[List[ChunkPlan]] = None          # pipelined exchange (phase A | all-to-all | phase B)
     # EP > 1, single reduction (allow_multiple_reduction=False, expanded): rows sent unreduced
     send_slots1: Optional[torch.Tensor] = None        # [N_send, 1] expanded rows in send order
     send_counts1: Optional[List[int]] = None
@@ -82,6 +97,44 @@ def weight_table(row_of_lane: torch.Tensor, row_floats: int, offset: int) -> tor
     idx = torch.where(row_of_lane >= 0, row_of_lane * row_floats + offset + k_idx, torch.full_like(row_of_lane, -1))
     assert int(idx.max().item()) < 2 ** 31 if idx.numel() else True
     return idx.to(torch.int32).contiguous()
+
+
+def chunk_plans(meta: torch.Tensor, recv_counts: List[int], topk_idx: torch.Tensor, num_experts: int,
+                num_ranks: int, num_max_tokens: int, num_chunks: int, expanded: bool) -> List[ChunkPlan]:
+    """Split the EP > 1 combine into chunks of source tokens so that phase A of chunk c+1, the
+    all-to-all of chunk c and phase B of chunk c-1 overlap.  Chunk c holds the source tokens
+    [c * B, (c + 1) * B) of every rank, B = ceil(num_max_tokens / num_chunks); on the expert side
+    those are, for every source rank, a contiguous run of its received rows (receive order is
+    (source rank, ascending token)), so the chunk's send buffer is again grouped by source rank."""
+    T, K = topk_idx.shape
+    R = num_ranks
+    dev = meta.device
+    n_recv = sum(recv_counts)
+    B = (num_max_tokens + num_chunks - 1) // num_chunks
+    m = meta[:n_recv]
+    chunk_of_row = torch.div(m[:, 0] % num_max_tokens, B, rounding_mode='floor')
+    src_rank = torch.div(m[:, 1], K, rounding_mode='floor')
+    plans = []
+    for c in range(num_chunks):
+        lo, hi = c * B, min((c + 1) * B, T)
+        rows = (chunk_of_row == c).nonzero().view(-1)
+        if expanded:
+            table_a = m[rows, 2:].contiguous()
+            wtable_a = table_a
+        elif num_chunks == 1:
+            table_a, wtable_a = None, None               # received row i is unit i
+        else:
+            table_a = rows.to(torch.int32).view(-1, 1).contiguous()
+            wtable_a = (rows.view(-1, 1) * K + torch.arange(K, device=dev).view(1, K)).to(torch.int32).contiguous()
+        send_counts = [int(v) for v in torch.bincount(src_rank[rows], minlength=R).tolist()]
+        if hi > lo:
+            table_b, row_of_lane, back_counts = epilogue_tables(topk_idx[lo:hi], num_experts, R)
+        else:
+            table_b = torch.empty((0, min(R, K)), dtype=torch.int32, device=dev)
+            row_of_lane = torch.empty((0, K), dtype=topk_idx.dtype, device=dev)
+            back_counts = [0] * R
+        plans.append(ChunkPlan(lo, max(lo, hi), table_a, wtable_a, send_counts, back_counts, table_b, row_of_lane))
+    return plans
 
 
 def single_reduction_tables(topk_idx: torch.Tensor, num_experts: int, num_ranks: int):

@@ -37,12 +37,13 @@ def _bf16_to_u16(t: torch.Tensor) -> np.ndarray:
     return t.contiguous().view(torch.int16).numpy().view(np.uint16)
 
 
-def _worker(rank, world, port, fixture, queue):
+def _worker(rank, world, port, fixture, queue, env=None):
     import sys
     sys.path.insert(0, ROOT)
     try:
         os.environ['MASTER_ADDR'] = '127.0.0.1'
         os.environ['MASTER_PORT'] = str(port)
+        os.environ.update(env or {})
         dist.init_process_group('gloo', rank=rank, world_size=world)
         from deepep_amd import ElasticBuffer
         from tests.oracle_kernels import OracleKernels
@@ -123,11 +124,11 @@ def _worker(rank, world, port, fixture, queue):
         queue.put((rank, [traceback.format_exc()]))
 
 
-def _spawn(fixture, world):
+def _spawn(fixture, world, env=None):
     ctx = mp.get_context('spawn')
     queue = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, fixture, queue)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, fixture, queue, env)) for r in range(world)]
     for p in procs:
         p.start()
     results = {}
@@ -156,12 +157,26 @@ def test_elastic_buffer_matches_golden(fixture, world):
     assert not bad, bad
 
 
-def _random_worker(rank, world, port, seed, queue):
+@pytest.mark.parametrize('fixture,world,chunks', [
+    ('f4_ep4_t96_h256_k2.npz', 4, 3),
+    ('f3_ep8_skew_t128_h64_k8.npz', 8, 5),
+])
+def test_chunked_combine_matches_golden(fixture, world, chunks):
+    """The EP > 1 combine split into source-token chunks (the pipelined schedule's plans) gives
+    the same bits as the one-shot exchange."""
+    results = _spawn(fixture, world, {'DEEPEP_COMBINE_CHUNKS': str(chunks)})
+    assert len(results) == world
+    bad = {r: f for r, f in results.items() if f}
+    assert not bad, bad
+
+
+def _random_worker(rank, world, port, seed, queue, env=None):
     import sys
     sys.path.insert(0, ROOT)
     try:
         os.environ['MASTER_ADDR'] = '127.0.0.1'
         os.environ['MASTER_PORT'] = str(port)
+        os.environ.update(env or {})
         dist.init_process_group('gloo', rank=rank, world_size=world)
         import oracle
         from deepep_amd import ElasticBuffer
@@ -212,13 +227,16 @@ def _random_worker(rank, world, port, seed, queue):
         queue.put((rank, [traceback.format_exc()]))
 
 
-@pytest.mark.parametrize('world', [2, 3])
-def test_random_routing_world(world):
-    """world_size 2 (and 3: a rank count that does not divide top-k) against oracle.combine_ep."""
+@pytest.mark.parametrize('world,chunks', [(2, 0), (3, 0), (2, 4)])
+def test_random_routing_world(world, chunks):
+    """world_size 2 (and 3: a rank count that does not divide top-k) against oracle.combine_ep;
+    (2, 4): the same exchange split into 4 source-token chunks."""
     ctx = mp.get_context('spawn')
     queue = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_random_worker, args=(r, world, port, 7 + world, queue)) for r in range(world)]
+    env = {'DEEPEP_COMBINE_CHUNKS': str(chunks)} if chunks else None
+    procs = [ctx.Process(target=_random_worker, args=(r, world, port, 7 + world, queue, env))
+             for r in range(world)]
     for p in procs:
         p.start()
     results = {}

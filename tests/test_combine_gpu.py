@@ -164,6 +164,13 @@ class _ThreadComm:
         self.bar.wait()
 
 
+class _Done:
+    """Completed work handle (the thread exchange synchronises the device before returning)."""
+
+    def wait(self):
+        return True
+
+
 class _FakeGroup:
     def __init__(self, rank, n, comm):
         self._rank, self._n, self.comm = rank, n, comm
@@ -197,6 +204,7 @@ def _buffer_case(rank, world, fixture, comm, results):
         buf = ElasticBuffer(grp, num_max_tokens_per_rank=T, hidden=H, num_topk=K)
         if world > 1:
             buf._a2a = lambda out, inp, os_=None, is_=None: comm.a2a(rank, out, inp, os_, is_)
+            buf._a2a_async = lambda out, inp, os_, is_: (comm.a2a(rank, out, inp, os_, is_), _Done())[1]
         idx = torch.from_numpy(me['topk_idx'].copy()).cuda()
         w = torch.from_numpy(me['topk_weights'].copy()).cuda()
         x = _bf16(me['x']) if 'x' in me else torch.randn((T, H), device='cuda').to(torch.bfloat16)
@@ -247,13 +255,17 @@ def _buffer_case(rank, world, fixture, comm, results):
         comm.bar.abort() if comm is not None else None
 
 
-@pytest.mark.parametrize('fixture,world', [
-    ('f1_ep1_t128_h1024_k2.npz', 1),
-    ('f4_ep4_t96_h256_k2.npz', 4),
-    ('f2_ep8_t64_h256_k8.npz', 8),
-    ('f3_ep8_skew_t128_h64_k8.npz', 8),
+@pytest.mark.parametrize('fixture,world,chunks', [
+    ('f1_ep1_t128_h1024_k2.npz', 1, 0),
+    ('f4_ep4_t96_h256_k2.npz', 4, 0),
+    ('f2_ep8_t64_h256_k8.npz', 8, 0),
+    ('f3_ep8_skew_t128_h64_k8.npz', 8, 0),
+    ('f4_ep4_t96_h256_k2.npz', 4, 3),        # pipelined: phase B of each chunk on the second stream
+    ('f3_ep8_skew_t128_h64_k8.npz', 8, 5),
 ])
-def test_elastic_buffer_golden_on_gpu(fixture, world):
+def test_elastic_buffer_golden_on_gpu(fixture, world, chunks, monkeypatch):
+    if chunks:
+        monkeypatch.setenv('DEEPEP_COMBINE_CHUNKS', str(chunks))
     comm = _ThreadComm(world) if world > 1 else None
     results = {}
     threads = [threading.Thread(target=_buffer_case, args=(r, world, fixture, comm, results)) for r in range(world)]

@@ -47,9 +47,55 @@ def _init_dist(n_gpus: int):
     return dist.get_rank(), dist.get_world_size()
 
 
-def _cpu_baseline(tokens: int, hidden: int, topk: int, min_seconds: float):
-    """PyTorch-CPU weighted sum (the reference's weighted semantics, refs/legacy) on a bounded
-    sample: `tokens` tokens x top-k x hidden, repeated for >= min_seconds."""
+def _cpu_threads() -> int:
+    return max(1, min(16, int(os.environ.get('OMP_NUM_THREADS', '16')), os.cpu_count() or 1))
+
+
+def _cpu_baseline(y: torch.Tensor, table: torch.Tensor, w: torch.Tensor, weighted: bool, min_seconds: float):
+    """The CPU oracle (oracle/combine_ref.c, the C restatement of the reference arithmetic; kind
+    "port") timed on the host cores over the SAME batch: the expanded rows, slot table and weights
+    copied to host memory (not cache-resident: ~0.94 GB), tokens split over threads, full passes
+    repeated for >= min_seconds."""
+    import ctypes
+    from concurrent.futures import ThreadPoolExecutor
+    import oracle
+    lib = oracle.rows_lib()
+    yh, th, wh = y.cpu(), table.cpu().contiguous(), w.cpu().contiguous()
+    T, K = th.shape
+    H = yh.shape[1]
+    out = torch.empty((T, H), dtype=torch.bfloat16)
+    out_w = torch.empty((T, K), dtype=torch.float32)
+    n_thr = _cpu_threads()
+    bounds = [(T * i // n_thr, T * (i + 1) // n_thr) for i in range(n_thr)]
+
+    def part(lo_hi):
+        lo, hi = lo_hi
+        rc = lib.oracle_combine_rows(
+            2, int(weighted), ctypes.c_void_p(yh.data_ptr()), yh.shape[0], H,
+            ctypes.c_void_p(th.data_ptr() + lo * K * 4), K, K, ctypes.c_void_p(wh.data_ptr()) if weighted else None,
+            None, None, ctypes.c_void_p(out.data_ptr() + lo * H * 2), H, hi - lo, H,
+            ctypes.c_void_p(th.data_ptr() + lo * K * 4), K, ctypes.c_void_p(wh.data_ptr()),
+            ctypes.c_void_p(out_w.data_ptr() + lo * K * 4), K, K)
+        assert rc == 0
+
+    valid = int((th >= 0).sum())
+    bytes_per = valid * H * 2 + T * H * 2 + valid * 4 + valid * 4
+    reps, t0 = 0, time.perf_counter()
+    with ThreadPoolExecutor(n_thr) as ex:
+        while True:
+            list(ex.map(part, bounds))
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= min_seconds:
+                break
+    return dict(value=round(bytes_per * reps / el / 1e9, 3), unit='GB/s', cores=n_thr, kind='port',
+                sample=f'{reps} full pass(es) of the bench batch ({T} tokens x top-{K} x hidden {H}, host copy) '
+                       f'through oracle_combine_rows (C restatement, fused {"weighted" if weighted else "plain"}), '
+                       f'{n_thr} threads, {el:.1f} s')
+
+
+def _cpu_torch(tokens: int, hidden: int, topk: int, min_seconds: float):
+    """BASELINE.md section 3's PyTorch-CPU weighted sum, [T, K, H] rows, same batch size."""
     g = torch.Generator().manual_seed(0)
     y = torch.randn((tokens, topk, hidden), generator=g).to(torch.bfloat16)
     w = torch.rand((tokens, topk), generator=g)
@@ -64,11 +110,9 @@ def _cpu_baseline(tokens: int, hidden: int, topk: int, min_seconds: float):
         if el >= min_seconds:
             break
     bytes_per = tokens * (topk * hidden * 2 + hidden * 2 + topk * 4 + topk * 4)
-    del out
-    return dict(value=round(bytes_per * reps / el / 1e9, 3), unit='GB/s', cores=torch.get_num_threads(),
-                kind='port',
-                sample=f'{reps} x ({tokens} tokens x top-{topk} x hidden {hidden}) bf16 weighted sum, '
-                       f'torch.addcmul_ fp32 loop on CPU, {el:.1f} s')
+    del out, y
+    return dict(value=round(bytes_per * reps / el / 1e9, 3), unit='GB/s', threads=torch.get_num_threads(),
+                sample=f'{reps} x ({tokens} tokens x top-{topk} x hidden {hidden}) torch.addcmul_ fp32 loop, {el:.1f} s')
 
 
 def _pmc_traffic(workload: str):
@@ -268,9 +312,11 @@ def main():
                         note='algorithmic bytes / (H2D of the expanded rows + combine + D2H of the output)')
         del host_y, host_out, dev_y
 
-    cpu_baseline = None
+    cpu_baseline = cpu_torch = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu_baseline = _cpu_baseline(1024, H, K, args.cpu_seconds)
+        plan = handle._combine_plans[('multi', 1)]
+        cpu_baseline = _cpu_baseline(y, plan.local_table, ex_w, weighted, args.cpu_seconds)
+        cpu_torch = _cpu_torch(T, H, K, args.cpu_seconds)
 
     if rank == 0:
         line = {
@@ -284,7 +330,8 @@ def main():
                                    f'{"gating-weighted" if weighted else "plain (reference semantics)"}',
                        'tokens_per_rank': T, 'hidden': H, 'topk': K, 'experts': E,
                        'parallelism': f'ep{world}'},
-            'roofline': roofline, 'cpu_baseline': cpu_baseline, 'loopback': loopback, 'phases': phases,
+            'roofline': roofline, 'cpu_baseline': cpu_baseline, 'cpu_torch': cpu_torch, 'loopback': loopback,
+            'phases': phases,
             'dispatch': dispatch,
         }
         print(json.dumps(line), flush=True)

@@ -115,6 +115,60 @@ def _cpu_torch(tokens: int, hidden: int, topk: int, min_seconds: float):
                 sample=f'{reps} x ({tokens} tokens x top-{topk} x hidden {hidden}) torch.addcmul_ fp32 loop, {el:.1f} s')
 
 
+def _bench_xgmi(buf, y, handle, ex_w, weighted, total_bytes, steps, warmup, dev):
+    """EP > 1 combine over the xGMI symmetric windows (DEEPEP_TRANSPORT=xgmi), timed like the main
+    loop and checked bit for bit against the default (RCCL) transport on the same batch.  Failures
+    (IPC, barrier timeout, mismatch) are reported, never raised: the main measurement stands."""
+    from deepep_amd import ElasticBuffer
+
+    def agree(ok: bool) -> bool:
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return bool(t.item())
+
+    ref, _, _ = buf.combine(y, handle, topk_weights=ex_w, apply_topk_weights=weighted)
+    torch.cuda.synchronize()
+    err = None
+    xb = None
+    try:
+        xb = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=buf.num_max_tokens_per_rank,
+                           hidden=y.shape[1], num_topk=handle.topk_idx.shape[1], explicitly_destroy=True,
+                           num_gpu_timeout_secs=10)
+        xb.transport = 'xgmi'
+        out, _, _ = xb.combine(y, handle, topk_weights=ex_w, apply_topk_weights=weighted)
+        torch.cuda.synchronize()
+        xb._sym.check()
+        equal = bool(torch.equal(out, ref))
+    except Exception as e:          # noqa: BLE001 -- reported in the JSON line
+        err, equal = f'{type(e).__name__}: {e}'[:300], False
+    if not agree(err is None):
+        return dict(error=err or 'failed on another rank')
+    equal_all = agree(equal)
+
+    def step():
+        return xb.combine(y, handle, topk_weights=ex_w, apply_topk_weights=weighted)
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    el = float(el.item())
+    timed_out = not agree(int(xb._sym.error_flag.item()) == 0)
+    xb.destroy()
+    return dict(value=round(total_bytes * steps / el / 1e9, 2), unit='GB/s', ms_per_step=round(el * 1e3 / steps, 4),
+                bitwise_equal_to_rccl=equal_all, barrier_timeout=timed_out,
+                note='same batch and bytes as `value`, DEEPEP_TRANSPORT=xgmi: phase A stores into the peers\' '
+                     'symmetric windows over xGMI, device barriers, phase B from the local window')
+
+
 def _pmc_traffic(workload: str):
     """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_traffic.py), if any."""
     path = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
@@ -255,8 +309,7 @@ def main():
         t_a = sum(ev[4 * i].elapsed_time(ev[4 * i + 1]) for i in range(n_ph)) / n_ph
         t_x = sum(ev[4 * i + 1].elapsed_time(ev[4 * i + 2]) for i in range(n_ph)) / n_ph
         t_b = sum(ev[4 * i + 2].elapsed_time(ev[4 * i + 3]) for i in range(n_ph)) / n_ph
-        plan = handle._combine_plans[('multi', world)]
-        sent_rows = sum(c for r_, c in enumerate(plan.recv_counts) if r_ != rank)
+        sent_rows = sum(c for r_, c in enumerate(handle._recv_counts) if r_ != rank)
         x_bytes = sent_rows * (H * 2 + K * 4)
         vals = torch.tensor([t_a + t_b, t_x, t_a, t_b], dtype=torch.float64, device=dev)
         dist.all_reduce(vals, op=dist.ReduceOp.MAX)
@@ -266,9 +319,13 @@ def main():
                       phase_b_ms=round(float(vals[3]), 4),
                       reduce_only_gbps=round(total_bytes / (float(vals[0]) * 1e-3) / 1e9, 1),
                       exchange_gbps_per_rank=round(float(xb.item()) / world / (float(vals[1]) * 1e-3) / 1e9, 1),
-                      pipeline_chunks=buf._num_chunks(handle),
+                      pipeline_chunks=buf._num_chunks(handle), transport=buf.transport,
                       note='phases measured unpipelined (1 chunk); `value` runs pipeline_chunks chunks; max over ranks; reduce_only = algorithmic bytes of all ranks / (phase A + phase B); '
                            'exchange = off-rank partial rows + weights / exchange time, per rank')
+
+    xgmi = None
+    if world > 1 and os.environ.get('DEEPEP_BENCH_XGMI', '1') != '0':
+        xgmi = _bench_xgmi(buf, y, handle, ex_w, weighted, total_bytes, args.steps, args.warmup, dev)
 
     # Handle producer: dispatch of the same batch, expanded layout.  Includes its
     # host syncs (received-token counts), as the reference's dispatch with do_cpu_sync=True.
@@ -331,7 +388,7 @@ def main():
                        'tokens_per_rank': T, 'hidden': H, 'topk': K, 'experts': E,
                        'parallelism': f'ep{world}'},
             'roofline': roofline, 'cpu_baseline': cpu_baseline, 'cpu_torch': cpu_torch, 'loopback': loopback,
-            'phases': phases,
+            'phases': phases, 'xgmi': xgmi,
             'dispatch': dispatch,
         }
         print(json.dumps(line), flush=True)

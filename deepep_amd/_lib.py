@@ -11,7 +11,7 @@ from typing import Optional
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('DEEPEP_AMD_LIB', os.path.join(_HERE, 'libdeepep_amd.so'))
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 MODE_LOCAL, MODE_EPILOGUE, MODE_FUSED = 0, 1, 2
 
@@ -48,6 +48,14 @@ SIGNATURES = {
     'deepep_dispatch_scan': (_I, [_P, _I, _I, _I, _I, _P, _P, _P]),
     'deepep_dispatch_slots': (_I, [_P, _I64, _I, _I, _I, _I, _I, _P, _P, _P]),
     'deepep_dispatch_copy': (_I, [_P, _I64, _I, _I, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P]),
+    'deepep_sym_alloc': (_I, [_I64, ctypes.POINTER(ctypes.c_void_p)]),
+    'deepep_sym_free': (_I, [_P]),
+    'deepep_sym_export': (_I, [_P, _P]),
+    'deepep_sym_import': (_I, [_P, ctypes.POINTER(ctypes.c_void_p)]),
+    'deepep_sym_close': (_I, [_P]),
+    'deepep_sym_barrier': (_I, [_P, _I, _I, _I64, _I64, _P, _P]),
+    'deepep_combine_reduce_scatter': (_I, [_I, _P, _I64, _I64, _P, _I64, _I, _P, _P, _I, _I, _P, _I64, _P, _I,
+                                           _I64, _P, _P]),
 }
 
 

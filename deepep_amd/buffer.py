@@ -25,7 +25,8 @@ import torch
 import torch.distributed as dist
 
 from .event import EventHandle, EventOverlap
-from .handle import CombinePlan, EPHandle, chunk_plans, epilogue_tables, single_reduction_tables, weight_table
+from .handle import (CombinePlan, EPHandle, chunk_plans, epilogue_tables, single_reduction_tables, weight_table,
+                     window_tables)
 from .kernels import MODE_EPILOGUE, MODE_FUSED, MODE_LOCAL, RowLayout
 from .utils import align, ceil_div, value_or
 
@@ -111,6 +112,12 @@ class ElasticBuffer:
         self._kernels = None
         self.runtime = self           # non-None while alive (the reference keeps its C++ runtime here)
         self._phase_events = None     # optional list: bench instrumentation of the EP > 1 phases
+        # EP > 1 combine transport: 'rccl' (all-to-all of packed partial rows, the default) or 'xgmi'
+        # (phase A stores straight into the owners' symmetric windows, deepep_amd/symmetric.py)
+        self.transport = os.environ.get('DEEPEP_TRANSPORT', 'rccl')
+        _assert(self.transport in ('rccl', 'xgmi'), 'DEEPEP_TRANSPORT must be rccl or xgmi')
+        self._sym = None
+        self._sym_exchange = None     # test hook: ranks sharing one process exchange window bases directly
         self._group_barrier()
 
     def _group_barrier(self) -> None:
@@ -137,6 +144,10 @@ class ElasticBuffer:
         if self.runtime is not None:
             if self.use_cuda:
                 torch.cuda.synchronize()
+            if self._sym is not None:
+                self._group_barrier()             # no peer still stores into this rank's window
+                self._sym.destroy()
+                self._sym = None
             self.runtime = None
 
     @staticmethod
@@ -571,6 +582,82 @@ class ElasticBuffer:
                 recv.record_stream(stream_b)
                 packed.record_stream(stream_b)
 
+    # ------------------------------------------------------------------ EP > 1 over xGMI windows
+    def _window(self, row_bytes: int):
+        """The symmetric window, sized for min(R, K) receive slots x T_max rows (buffer.hpp:616-633);
+        allocated on first use (collective: every rank reaches the same combine)."""
+        slots = self._window_slots
+        need = slots * self.num_max_tokens_per_rank * row_bytes
+        if self._sym is not None and self._sym.data_bytes >= need:
+            return self._sym
+        from .symmetric import SymmetricBuffer
+        if self._sym is not None:
+            self._group_barrier()
+            self._sym.destroy()
+        self._sym = SymmetricBuffer(self.group, self.rank_idx, self.num_ranks, need, self.device,
+                                    exchange=self._sym_exchange, timeout_s=self.num_gpu_timeout_secs)
+        return self._sym
+
+    def _combine_xgmi(self, handle, x, expanded, row_w, wsrc, K, hidden, bias_0, bias_1, topk_weights,
+                      combined_x, combined_w, previous_event_before_epilogue, stream) -> None:
+        """EP > 1 combine over the symmetric windows (the reference's NVLink design on xGMI):
+        barrier (peers done reading their windows) -> phase A storing every partial and its top-k
+        weights straight into the owner's window row slot * T_max + t (combine.cuh:96-106, 215-226)
+        -> barrier (all partials landed, comm.cuh:88-129) -> phase B over the local window."""
+        R, r = self.num_ranks, self.rank_idx
+        T_max = handle.num_max_tokens_per_rank
+        T = handle.topk_idx.shape[0]
+        rank_layout = R <= K                              # use_rank_layout, combine_utils.cuh:8-13
+        self._window_slots = min(R, K)
+        row_bytes = align(hidden * 2, 16) + align(K * 4, 16)
+        sym = self._window(row_bytes)
+        key = ('xgmi', R, row_bytes)
+        plan = handle._combine_plans.get(key)
+        if plan is None:
+            plan = CombinePlan(num_ranks=R, num_tokens=T, num_topk=K, expanded=expanded)
+            meta = handle.recv_src_metadata
+            recv_counts = handle._recv_counts
+            if recv_counts is None:
+                psum = [0] + [int(v) for v in handle.psum_num_recv_tokens_per_scaleup_rank.tolist()]
+                recv_counts = [psum[i + 1] - psum[i] for i in range(R)]
+            n_recv = sum(recv_counts)
+            plan.recv_counts = recv_counts
+            m = meta[:n_recv].to(torch.int64)
+            src_rank = torch.div(m[:, 1], K, rounding_mode='floor')
+            slot = torch.full_like(src_rank, r) if rank_layout else m[:, 1] % K
+            row = slot * T_max + m[:, 0] % T_max
+            plan.out_rows = (sym.data_bases_dev[src_rank] + row * row_bytes).contiguous()
+            plan.table_b, plan.row_of_lane = window_tables(handle.topk_idx, handle.num_experts, R, T_max, rank_layout)
+            plan.wtables = {}
+            plan.window_row_bytes = row_bytes
+            handle._combine_plans[key] = plan
+        n_recv = sum(plan.recv_counts)
+        meta = handle.recv_src_metadata
+        table_a = meta[:n_recv, 2:] if expanded else None
+        kern = self.kernels
+        sym.barrier(stream)
+        self._mark(stream)
+        kern.combine_reduce_scatter(x, n_recv, plan.out_rows, table=table_a, row_weights=row_w,
+                                    wtable=table_a, wsrc=wsrc, num_weights=K if topk_weights is not None else 0,
+                                    weights_offset=align(hidden * 2, 16), stream=stream)
+        self._mark(stream)
+        sym.barrier(stream)
+        self._before_epilogue(previous_event_before_epilogue)
+        n_rows = self._window_slots * T_max
+        rows = sym.data[:n_rows * row_bytes].view(torch.bfloat16).view(n_rows, row_bytes // 2)
+        wtable_b, recv_wsrc = None, None
+        if topk_weights is not None:
+            wkey = (row_bytes // 4, align(hidden * 2, 16) // 4)
+            if wkey not in plan.wtables:
+                plan.wtables[wkey] = weight_table(plan.row_of_lane, *wkey)
+            wtable_b = plan.wtables[wkey]
+            recv_wsrc = sym.data[:n_rows * row_bytes].view(torch.float32)
+        self._mark(stream)
+        kern.combine_reduce(MODE_EPILOGUE, rows[:, :hidden], combined_x, T, table=plan.table_b,
+                            bias0=bias_0, bias1=bias_1, wtable=wtable_b, wsrc=recv_wsrc,
+                            out_weights=combined_w, stream=stream)
+        self._mark(stream)
+
     def combine(self,
                 x: torch.Tensor,
                 handle: EPHandle,
@@ -648,8 +735,9 @@ class ElasticBuffer:
             compute_stream = self._prologue(previous_event, allocate_on_comm_stream)
             stream = self.comm_stream
         with (self._null_ctx() if sync_mode else self._stream_ctx()):
+            use_xgmi = R > 1 and not single_reduction and self.transport == 'xgmi' and self.use_cuda
             num_chunks = self._num_chunks(handle) if not single_reduction else 1
-            plan = self._plan(handle, single_reduction, num_chunks)
+            plan = None if use_xgmi else self._plan(handle, single_reduction, num_chunks)
             combined_x = torch.empty((T, hidden), dtype=x.dtype, device=x.device)
             combined_w = torch.empty((T, K), dtype=torch.float32, device=x.device) if topk_weights is not None else None
             row_w = topk_weights if apply_topk_weights else None
@@ -673,6 +761,9 @@ class ElasticBuffer:
                 self._before_epilogue(previous_event_before_epilogue)
                 kern.combine_reduce(MODE_EPILOGUE, recv, combined_x, T, table=plan.table_b1,
                                     bias0=bias_0, bias1=bias_1, stream=stream)
+            elif use_xgmi:
+                self._combine_xgmi(handle, x, expanded, row_w, wsrc, K, hidden, bias_0, bias_1, topk_weights,
+                                   combined_x, combined_w, previous_event_before_epilogue, stream)
             else:
                 self._combine_chunks(plan, x, expanded, row_w, wsrc, K, hidden, bias_0, bias_1, topk_weights,
                                      combined_x, combined_w, previous_event_before_epilogue, stream)

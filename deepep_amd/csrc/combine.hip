@@ -94,6 +94,8 @@ struct Params {
     int64_t out_weights_stride;  // floats between consecutive units' weight rows
     int units_per_block;
     int32_t* error_flag;
+    const uint64_t* out_rows;    // scatter (phase A over xGMI): byte address of unit u's output row, or NULL
+    int64_t weights_offset;      // scatter: byte offset of the weights inside the output row
 };
 
 // acc[8*v + e] += element e of the 16-byte vector (8 bf16)
@@ -192,10 +194,15 @@ combine_rows_kernel(const Params p) {
 
     // ---- top-k weight pass-through (combine.cuh:215-226, combine_reduce_epilogue.cuh:127-141),
     //      written once per unit by the wave owning chunk 0
-    if (c == 0 && p.out_weights != nullptr && lane < p.num_weights) {
+    uint16_t* const out_row = p.out_rows != nullptr ? reinterpret_cast<uint16_t*>(p.out_rows[u])
+                                                     : p.out + u * p.out_stride;
+    if (c == 0 && p.num_weights > 0 && lane < p.num_weights) {
         const int64_t i = p.wtable == nullptr ? u * p.num_weights + lane
                                               : static_cast<int64_t>(p.wtable[u * p.wtable_stride + lane]);
-        p.out_weights[u * p.out_weights_stride + lane] = i >= 0 ? p.wsrc[i] : 0.0f;
+        float* const ow = p.out_rows != nullptr
+                              ? reinterpret_cast<float*>(reinterpret_cast<char*>(out_row) + p.weights_offset)
+                              : p.out_weights + u * p.out_weights_stride;
+        ow[lane] = i >= 0 ? p.wsrc[i] : 0.0f;
     }
 
     int vidx[kVPT];
@@ -292,7 +299,7 @@ combine_rows_kernel(const Params p) {
         }
     }
 
-    const __amdgpu_buffer_rsrc_t orow = row_rsrc(p.out + u * p.out_stride, p.hidden * 2);
+    const __amdgpu_buffer_rsrc_t orow = row_rsrc(out_row, p.hidden * 2);
 #pragma unroll
     for (int v = 0; v < kVPT; ++v)
         __builtin_amdgcn_raw_buffer_store_b128(result[v], orow, vidx[v] * 16, 0, kStoreAux);
@@ -362,6 +369,8 @@ __global__ void local_plan_kernel(const int32_t* meta, int num_recv, int num_top
                 topk_idx[static_cast<int64_t>(t) * num_topk + k] >= 0 ? i * num_topk + k : -1;
 }
 
+int launch_combine(int mode, int weighted, const Params& p, deepep_stream_t stream);
+
 }  // namespace
 
 extern "C" {
@@ -430,15 +439,76 @@ int deepep_combine_reduce(int mode, int weighted,
     p.wtable_stride = wtable_stride;
     p.wsrc = wsrc;
     p.out_weights = out_weights;
-    p.num_weights = num_weights;
+    p.num_weights = out_weights != nullptr ? num_weights : 0;
     p.out_weights_stride = out_weights_stride;
     p.units_per_block = units_per_block;
     p.error_flag = error_flag;
+    p.out_rows = nullptr;
+    p.weights_offset = 0;
 
+    (void)units_per_block;                                  // kept in the ABI; items, not units, are tiled
+    return launch_combine(mode, weighted, p, stream);
+}
+
+int deepep_combine_reduce_scatter(int weighted,
+                                  const void* src, int64_t num_src_rows, int64_t src_row_stride,
+                                  const int32_t* table, int64_t table_stride, int table_width,
+                                  const float* row_weights,
+                                  const uint64_t* out_rows, int num_units, int hidden,
+                                  const int32_t* wtable, int64_t wtable_stride,
+                                  const float* wsrc, int num_weights, int64_t weights_offset,
+                                  int32_t* error_flag, deepep_stream_t stream) {
+    if (num_units < 0 || hidden < 0)
+        return set_error(DEEPEP_ERR_INVALID_ARG, "negative size (num_units=%d, hidden=%d)", num_units, hidden);
+    if (num_units == 0) return DEEPEP_OK;
+    if (hidden % 8 != 0)
+        return set_error(DEEPEP_ERR_INVALID_ARG, "hidden (%d) * sizeof(bf16) must be a multiple of 16 bytes", hidden);
+    if (out_rows == nullptr || (src == nullptr && num_src_rows > 0) || !aligned16(src))
+        return set_error(DEEPEP_ERR_INVALID_ARG, "null out_rows / unaligned src");
+    if (src_row_stride % 8 != 0 || src_row_stride < hidden)
+        return set_error(DEEPEP_ERR_INVALID_ARG, "src row stride must be >= hidden and a multiple of 8 elements");
+    if (table != nullptr && (table_width < 1 || table_width > kMaxWidth || table_stride < table_width))
+        return set_error(DEEPEP_ERR_INVALID_ARG, "table width %d outside [1, %d] or stride too small", table_width, kMaxWidth);
+    if (weighted && row_weights == nullptr)
+        return set_error(DEEPEP_ERR_INVALID_ARG, "weighted reduction needs row weights");
+    if (num_weights > 0 && (wsrc == nullptr || num_weights > kMaxWidth || weights_offset < int64_t(hidden) * 2 ||
+                            weights_offset % 4 != 0))
+        return set_error(DEEPEP_ERR_INVALID_ARG, "weights need wsrc, num_weights <= %d and an offset past the row", kMaxWidth);
+    Params p;
+    p.src = static_cast<const uint16_t*>(src);
+    p.num_src_rows = num_src_rows;
+    p.src_stride = src_row_stride;
+    p.table = table;
+    p.table_stride = table_stride;
+    p.table_width = table_width;
+    p.row_weights = row_weights;
+    p.bias0 = nullptr;
+    p.bias1 = nullptr;
+    p.out = nullptr;
+    p.out_stride = 0;
+    p.num_units = num_units;
+    p.hidden = hidden;
+    p.wtable = wtable;
+    p.wtable_stride = wtable_stride;
+    p.wsrc = wsrc;
+    p.out_weights = nullptr;
+    p.num_weights = num_weights > 0 ? num_weights : 0;
+    p.out_weights_stride = 0;
+    p.units_per_block = 0;
+    p.error_flag = error_flag;
+    p.out_rows = out_rows;
+    p.weights_offset = weights_offset;
+    return launch_combine(DEEPEP_MODE_LOCAL, weighted, p, stream);
+}
+
+}  // extern "C"
+
+namespace {
+
+int launch_combine(int mode, int weighted, const Params& p, deepep_stream_t stream) {
     // Launch shape: one wave per (unit, 64 x vpt x 16-byte column chunk) item, 4 items per
     // workgroup; at hidden 7168 a token is 7 items of 2 KiB per source row.
-    (void)units_per_block;                                  // kept in the ABI; items, not units, are tiled
-    const int nvec = hidden / 8;
+    const int nvec = p.hidden / 8;
     int vpt = g_config.vec_per_lane > 0 ? g_config.vec_per_lane : (nvec >= 128 ? 2 : 1);
     if (vpt != 1 && vpt != 2) vpt = 2;
     const bool lds = g_config.stage_lds >= 0 ? g_config.stage_lds != 0 : true;
@@ -458,6 +528,10 @@ int deepep_combine_reduce(int mode, int weighted,
         return set_error(DEEPEP_ERR_HIP, "combine launch failed: %s", hipGetErrorString(err));
     return DEEPEP_OK;
 }
+
+}  // namespace
+
+extern "C" {
 
 int deepep_build_local_plan(const int32_t* src_metadata, int num_recv_tokens, int num_topk,
                             int num_max_tokens_per_rank, int expanded,

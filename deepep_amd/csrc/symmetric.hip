@@ -1,0 +1,127 @@
+// symmetric.hip -- the symmetric receive buffer over xGMI and its device barrier.
+//
+// Reference (paths in /root/reference):
+//   NCCLSymmetricMemoryContext: one registered window per rank, every peer's window
+//   load/store-addressable over NVLink            csrc/elastic/nccl.cu:62-153, buffer.hpp:181-208
+//   gpu_barrier / nvlink_barrier_wo_local_sync:
+//   per-rank signal slots written by every peer   deep_ep/include/deep_ep/common/comm.cuh:88-129, 208-264
+//
+// MI355X design: the window is one hipExtMallocWithFlags(hipDeviceMallocUncached) allocation per
+// rank, exported with hipIpcGetMemHandle and opened by every peer with hipIpcOpenMemHandle; the
+// fabric (xGMI) makes the peer's HBM load/store addressable from kernels.  Uncached (MTYPE UC)
+// memory is used because a peer's stores land in this GPU's HBM behind its L2; nothing of the
+// window is ever cached, so no invalidation protocol is needed between the writers' kernels and
+// the reader's.  The barrier is a one-workgroup kernel: thread s publishes `epoch` into rank s's
+// flag slot [rank] with a system-scope release store and then waits, with a system-scope acquire
+// load, until its own slot [s] reaches `epoch`.  Epochs only grow, so flags never need resetting.
+// A wall-clock timeout (the reference's num_gpu_timeout_secs, comm.cuh:30-54) sets bit 2 of the
+// error flag and lets the kernel finish instead of trapping, so a lost peer never hangs the GPU.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "../../include/deepep_amd.h"
+
+extern "C" int deepep_amd_set_error(int code, const char* msg);
+
+namespace {
+
+int hip_fail(hipError_t e, const char* what) {
+    char buf[256];
+    snprintf(buf, sizeof(buf), "%s: %s", what, hipGetErrorString(e));
+    return deepep_amd_set_error(DEEPEP_ERR_HIP, buf);
+}
+
+__global__ void __launch_bounds__(64)
+sym_barrier_kernel(const uint64_t* peer_flags, int rank, int num_ranks, int64_t epoch, int64_t timeout_ticks,
+                   int32_t* error_flag) {
+    const int s = static_cast<int>(threadIdx.x);
+    if (s >= num_ranks) return;
+    __threadfence_system();
+    int64_t* theirs = reinterpret_cast<int64_t*>(peer_flags[s]);
+    __hip_atomic_store(theirs + rank, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    const int64_t* mine = reinterpret_cast<const int64_t*>(peer_flags[rank]);
+    const uint64_t t0 = wall_clock64();
+    while (__hip_atomic_load(mine + s, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
+        if (static_cast<int64_t>(wall_clock64() - t0) > timeout_ticks) {
+            if (error_flag != nullptr) atomicOr(error_flag, 2);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+    __threadfence_system();
+}
+
+}  // namespace
+
+extern "C" {
+
+int deepep_sym_alloc(int64_t bytes, void** ptr) {
+    if (ptr == nullptr || bytes <= 0) return deepep_amd_set_error(DEEPEP_ERR_INVALID_ARG, "sym_alloc: bad size");
+    *ptr = nullptr;
+    hipError_t e = hipExtMallocWithFlags(ptr, static_cast<size_t>(bytes), hipDeviceMallocUncached);
+    if (e != hipSuccess) return hip_fail(e, "hipExtMallocWithFlags(uncached)");
+    // Null-stream memset + null-stream sync (not a device-wide sync: ranks that share a process
+    // may already have barrier kernels waiting on other streams).
+    e = hipMemsetAsync(*ptr, 0, static_cast<size_t>(bytes), nullptr);
+    if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+    if (e != hipSuccess) {
+        (void)hipFree(*ptr);
+        *ptr = nullptr;
+        return hip_fail(e, "hipMemset(symmetric buffer)");
+    }
+    return DEEPEP_OK;
+}
+
+int deepep_sym_free(void* ptr) {
+    if (ptr == nullptr) return DEEPEP_OK;
+    const hipError_t e = hipFree(ptr);
+    return e == hipSuccess ? DEEPEP_OK : hip_fail(e, "hipFree(symmetric buffer)");
+}
+
+int deepep_sym_export(void* ptr, void* handle) {
+    static_assert(sizeof(hipIpcMemHandle_t) <= DEEPEP_IPC_HANDLE_BYTES, "IPC handle size");
+    if (ptr == nullptr || handle == nullptr) return deepep_amd_set_error(DEEPEP_ERR_INVALID_ARG, "sym_export: null");
+    hipIpcMemHandle_t h;
+    const hipError_t e = hipIpcGetMemHandle(&h, ptr);
+    if (e != hipSuccess) return hip_fail(e, "hipIpcGetMemHandle");
+    memset(handle, 0, DEEPEP_IPC_HANDLE_BYTES);
+    memcpy(handle, &h, sizeof(h));
+    return DEEPEP_OK;
+}
+
+int deepep_sym_import(const void* handle, void** ptr) {
+    if (ptr == nullptr || handle == nullptr) return deepep_amd_set_error(DEEPEP_ERR_INVALID_ARG, "sym_import: null");
+    hipIpcMemHandle_t h;
+    memcpy(&h, handle, sizeof(h));
+    *ptr = nullptr;
+    const hipError_t e = hipIpcOpenMemHandle(ptr, h, hipIpcMemLazyEnablePeerAccess);
+    return e == hipSuccess ? DEEPEP_OK : hip_fail(e, "hipIpcOpenMemHandle");
+}
+
+int deepep_sym_close(void* ptr) {
+    if (ptr == nullptr) return DEEPEP_OK;
+    const hipError_t e = hipIpcCloseMemHandle(ptr);
+    return e == hipSuccess ? DEEPEP_OK : hip_fail(e, "hipIpcCloseMemHandle");
+}
+
+int deepep_sym_barrier(const uint64_t* peer_flags, int rank, int num_ranks, int64_t epoch, int64_t timeout_us,
+                       int32_t* error_flag, deepep_stream_t stream) {
+    if (peer_flags == nullptr || num_ranks < 1 || num_ranks > 64 || rank < 0 || rank >= num_ranks || epoch < 1)
+        return deepep_amd_set_error(DEEPEP_ERR_INVALID_ARG, "sym_barrier: bad arguments");
+    static thread_local int64_t ticks_per_us = 0;
+    if (ticks_per_us == 0) {
+        int dev = 0, khz = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e == hipSuccess) e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
+        if (e != hipSuccess) return hip_fail(e, "wall clock rate");
+        ticks_per_us = khz > 1000 ? khz / 1000 : 1;
+    }
+    const int64_t ticks = (timeout_us > 0 ? timeout_us : 100000000LL) * ticks_per_us;
+    hipLaunchKernelGGL(sym_barrier_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream),
+                       peer_flags, rank, num_ranks, epoch, ticks, error_flag);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? DEEPEP_OK : hip_fail(e, "barrier launch");
+}
+
+}  // extern "C"

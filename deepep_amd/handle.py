@@ -51,6 +51,9 @@ class CombinePlan:
     row_of_lane: Optional[torch.Tensor] = None        # [T, K] receive row holding lane k's weight, or -1
     wtables: Optional[dict] = None                    # packed-row weight tables, keyed by (row floats, offset)
     chunks: Optional[List[ChunkPlan]] = None          # pipelined exchange (phase A | all-to-all | phase B)
+    # EP > 1 over the xGMI symmetric windows
+    out_rows: Optional[torch.Tensor] = None           # [N_recv] int64 byte address of each partial's row
+    window_row_bytes: int = 0
     # EP > 1, single reduction (allow_multiple_reduction=False, expanded): rows sent unreduced
     send_slots1: Optional[torch.Tensor] = None        # [N_send, 1] expanded rows in send order
     send_counts1: Optional[List[int]] = None
@@ -97,6 +100,34 @@ def weight_table(row_of_lane: torch.Tensor, row_floats: int, offset: int) -> tor
     idx = torch.where(row_of_lane >= 0, row_of_lane * row_floats + offset + k_idx, torch.full_like(row_of_lane, -1))
     assert int(idx.max().item()) < 2 ** 31 if idx.numel() else True
     return idx.to(torch.int32).contiguous()
+
+
+def window_tables(topk_idx: torch.Tensor, num_experts: int, num_ranks: int, num_max_tokens: int,
+                  rank_layout: bool):
+    """Source-side tables for the xGMI transport, where partials land in this rank's symmetric
+    window at row slot * T_max + t (slot = expert rank under the rank layout, else the dedup
+    master lane; combine.cuh:96-106, combine_utils.cuh:8-13).  Returns table_b [T, min(R, K)]
+    (rows in ascending dedup-master-lane order, combine_reduce_epilogue.cuh:74-95) and
+    row_of_lane [T, K] (the row holding lane k's weight, or -1)."""
+    T, K = topk_idx.shape
+    R = num_ranks
+    dev = topk_idx.device
+    epr = num_experts // R
+    rank_of = torch.where(topk_idx >= 0, torch.div(topk_idx, epr, rounding_mode='floor'),
+                          torch.full_like(topk_idx, -1))
+    ranks = torch.arange(R, device=dev)
+    hit = rank_of.unsqueeze(-1) == ranks.view(1, 1, R)                 # [T, K, R]
+    is_to = hit.any(dim=1)                                              # [T, R]
+    lanes = torch.arange(K, device=dev).view(1, K, 1)
+    master = torch.where(hit, lanes, torch.full_like(lanes, -1)).amax(dim=1)      # [T, R]
+    slot = ranks.view(1, R).expand(T, R) if rank_layout else master
+    t_idx = torch.arange(T, device=dev).view(T, 1)
+    row = torch.where(is_to, slot * num_max_tokens + t_idx, torch.full_like(master, -1))
+    key = torch.where(is_to, master, K + ranks.view(1, R))
+    order = torch.argsort(key, dim=1, stable=True)[:, :min(R, K)]
+    table_b = row.gather(1, order).to(torch.int32).contiguous()
+    row_of_lane = torch.where(rank_of >= 0, row.gather(1, rank_of.clamp(min=0)), torch.full_like(rank_of, -1))
+    return table_b, row_of_lane.contiguous()
 
 
 def chunk_plans(meta: torch.Tensor, recv_counts: List[int], topk_idx: torch.Tensor, num_experts: int,

@@ -115,6 +115,29 @@ class HipKernels:
             _stream_handle(stream))
         _lib.check(rc, 'combine_reduce')
 
+    def combine_reduce_scatter(self, src: torch.Tensor, num_units: int, out_rows: torch.Tensor,
+                               table: Optional[torch.Tensor] = None, row_weights: Optional[torch.Tensor] = None,
+                               wtable: Optional[torch.Tensor] = None, wsrc: Optional[torch.Tensor] = None,
+                               num_weights: int = 0, weights_offset: int = 0,
+                               error_flag: Optional[torch.Tensor] = None, stream=None) -> None:
+        """Phase A storing unit u's row at byte address out_rows[u] (a peer window over xGMI)."""
+        _require(src.is_cuda and src.dtype == torch.bfloat16 and src.dim() == 2 and src.stride(1) == 1,
+                 'combine rows must be 2-D bf16 on the GPU with unit column stride')
+        _require(out_rows.is_cuda and out_rows.dtype == torch.int64 and out_rows.is_contiguous() and
+                 out_rows.shape[0] >= num_units, 'out_rows must be int64 [num_units] on the GPU')
+        t, t_stride, t_width = _table_view(table)
+        w, w_stride, _ = _table_view(wtable)
+        if num_weights:
+            _require(wsrc is not None and wsrc.dtype == torch.float32 and wsrc.dim() == 1, 'weight source')
+        if row_weights is not None:
+            _require(row_weights.dtype == torch.float32 and row_weights.is_contiguous(), 'row weights')
+        hidden = src.shape[1]
+        rc = self.lib.deepep_combine_reduce_scatter(
+            int(row_weights is not None), ptr(src), src.shape[0], src.stride(0) if src.shape[0] > 0 else hidden,
+            ptr(t), t_stride, t_width, ptr(row_weights), ptr(out_rows), num_units, hidden,
+            ptr(w), w_stride, ptr(wsrc), num_weights, weights_offset, ptr(error_flag), _stream_handle(stream))
+        _lib.check(rc, 'combine_reduce_scatter')
+
     def build_local_plan(self, src_metadata: torch.Tensor, num_recv_tokens: int, num_topk: int,
                          num_max_tokens_per_rank: int, expanded: bool, plan: torch.Tensor,
                          num_tokens: int, topk_idx: Optional[torch.Tensor] = None,

@@ -1,0 +1,101 @@
+"""Symmetric receive buffer over xGMI and its device barrier.
+
+Replaces the reference's NCCLSymmetricMemoryContext (csrc/elastic/nccl.cu:62-153,
+csrc/elastic/buffer.hpp:181-208: one window per rank, every peer's window addressable
+from kernels) and gpu_barrier (deep_ep/include/deep_ep/common/comm.cuh:88-129).
+
+Every rank allocates one uncached device window (deepep_sym_alloc), exports it with
+HIP IPC, and opens every peer's window (deepep_sym_import); kernels then store into a
+peer's HBM over xGMI.  Layout of a window:
+
+    [0, HEADER_BYTES)        int64 flags[num_ranks]: barrier epochs written by the peers
+    [HEADER_BYTES, ...)      data: the combine receive rows (see ElasticBuffer._combine_xgmi)
+"""
+import ctypes
+from typing import Callable, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from . import _lib
+
+HEADER_BYTES = 64 * 1024
+
+
+class _DeviceArray:
+    """Wrap a raw device allocation as a torch tensor without copying (__cuda_array_interface__)."""
+
+    def __init__(self, address: int, nbytes: int):
+        self.__cuda_array_interface__ = {'shape': (nbytes,), 'typestr': '|u1', 'data': (address, False),
+                                         'version': 3, 'strides': None}
+
+
+class SymmetricBuffer:
+    """One window per rank, mapped into every peer; `barrier(stream)` is a device-side group barrier.
+
+    exchange: optional hook `exchange(local_base) -> [base of every rank]` for ranks that share a
+    process (the single-GPU thread simulation); by default IPC handles are all-gathered over `group`.
+    """
+
+    def __init__(self, group, rank: int, num_ranks: int, data_bytes: int, device: torch.device,
+                 exchange: Optional[Callable[[int], List[int]]] = None, timeout_s: float = 100.0):
+        self.lib = _lib.load()
+        self.rank, self.num_ranks = rank, num_ranks
+        self.device = device
+        self.data_bytes = int(data_bytes)
+        self.timeout_us = int(timeout_s * 1e6)
+        p = ctypes.c_void_p()
+        _lib.check(self.lib.deepep_sym_alloc(HEADER_BYTES + self.data_bytes, ctypes.byref(p)), 'sym_alloc')
+        self.base = int(p.value)
+        self._imported: List[int] = []
+        if exchange is not None:
+            bases = [int(b) for b in exchange(self.base)]
+        else:
+            bases = self._ipc_exchange(group)
+        assert len(bases) == num_ranks and bases[rank] == self.base
+        self.bases = bases
+        self.bases_dev = torch.tensor(bases, dtype=torch.int64, device=device)     # flags live at offset 0
+        self.data_bases_dev = self.bases_dev + HEADER_BYTES
+        self.data = torch.as_tensor(_DeviceArray(self.base + HEADER_BYTES, self.data_bytes), device=device)
+        self.error_flag = torch.zeros((1,), dtype=torch.int32, device=device)
+        self.epoch = 0
+
+    def _ipc_exchange(self, group) -> List[int]:
+        handle = ctypes.create_string_buffer(64)
+        _lib.check(self.lib.deepep_sym_export(ctypes.c_void_p(self.base), handle), 'sym_export')
+        handles: List[Optional[bytes]] = [None] * self.num_ranks
+        dist.all_gather_object(handles, handle.raw, group=group)
+        bases = []
+        for s, h in enumerate(handles):
+            if s == self.rank:
+                bases.append(self.base)
+                continue
+            p = ctypes.c_void_p()
+            _lib.check(self.lib.deepep_sym_import(ctypes.create_string_buffer(h, 64), ctypes.byref(p)), 'sym_import')
+            self._imported.append(int(p.value))
+            bases.append(int(p.value))
+        return bases
+
+    def barrier(self, stream) -> None:
+        """Device-side group barrier on `stream` (all ranks must call it the same number of times)."""
+        self.epoch += 1
+        handle = stream.cuda_stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        _lib.check(self.lib.deepep_sym_barrier(self.bases_dev.data_ptr(), self.rank, self.num_ranks, self.epoch,
+                                               self.timeout_us, self.error_flag.data_ptr(), handle), 'sym_barrier')
+
+    def check(self) -> None:
+        """Raise if a barrier timed out (host sync)."""
+        v = int(self.error_flag.item())
+        if v:
+            raise RuntimeError(f'deepep_amd: symmetric buffer error flag {v} (2 = barrier timeout)')
+
+    def destroy(self) -> None:
+        if self.base is None:
+            return
+        torch.cuda.synchronize(self.device)
+        self.data = None
+        for p in self._imported:
+            _lib.check(self.lib.deepep_sym_close(ctypes.c_void_p(p)), 'sym_close')
+        self._imported = []
+        _lib.check(self.lib.deepep_sym_free(ctypes.c_void_p(self.base)), 'sym_free')
+        self.base = None

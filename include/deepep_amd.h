@@ -45,7 +45,7 @@ extern "C" {
 
 typedef struct ihipStream_t* deepep_stream_t;   /* == hipStream_t */
 
-#define DEEPEP_AMD_ABI_VERSION 2
+#define DEEPEP_AMD_ABI_VERSION 3
 
 #define DEEPEP_OK               0
 #define DEEPEP_ERR_INVALID_ARG  (-1)
@@ -169,6 +169,41 @@ int deepep_dispatch_slots(const void* packed, int64_t row_bytes, int idx_off, in
 int deepep_dispatch_copy(const void* packed, int64_t row_bytes, int x_bytes, int sf_off, int sf_bytes, int w_off,
                          int num_recv, int num_topk, const int32_t* src_metadata, int expanded,
                          void* recv_x, void* recv_sf, float* recv_topk_weights, deepep_stream_t stream);
+
+/* ------------------------------------------------------------------ symmetric buffer over xGMI
+ * Replaces the reference's NCCLSymmetricMemoryContext (csrc/elastic/nccl.cu:62-153, buffer.hpp:181-208)
+ * and its device barrier (deep_ep/include/deep_ep/common/comm.cuh:88-129).  One uncached device
+ * allocation per rank, exported/imported with HIP IPC; kernels on any rank load/store a peer's
+ * window over xGMI. */
+#define DEEPEP_IPC_HANDLE_BYTES 64
+
+int deepep_sym_alloc(int64_t bytes, void** ptr);            /* zero-filled, hipDeviceMallocUncached */
+int deepep_sym_free(void* ptr);
+int deepep_sym_export(void* ptr, void* handle);             /* handle: DEEPEP_IPC_HANDLE_BYTES bytes */
+int deepep_sym_import(const void* handle, void** ptr);      /* a peer's window, mapped into this process */
+int deepep_sym_close(void* ptr);
+
+/* Group barrier on the stream: peer_flags (device, uint64 [num_ranks]) holds the address of every
+ * rank's int64 flag array (num_ranks slots, in its window).  Rank r stores `epoch` into slot [r] of
+ * every rank's array (system-scope release) and waits until its own slots all reach `epoch`
+ * (system-scope acquire); epochs must grow by one per call.  After timeout_us (<= 0: 100 s) the
+ * wait gives up and sets bit 2 of *error_flag (comm.cuh:30-54 traps instead). */
+int deepep_sym_barrier(const uint64_t* peer_flags, int rank, int num_ranks, int64_t epoch, int64_t timeout_us,
+                       int32_t* error_flag, deepep_stream_t stream);
+
+/* Phase A writing straight into the owners' receive rows (combine_impl's NVLink push,
+ * combine.cuh:96-106, 125-176, 215-226): the reduce of deepep_combine_reduce(DEEPEP_MODE_LOCAL, ...)
+ * with unit u's bf16 row stored at byte address out_rows[u] (any rank's window, 16-byte aligned)
+ * and, when num_weights > 0, its top-k weights (the wtable / wsrc pass-through rule above) at
+ * out_rows[u] + weights_offset. */
+int deepep_combine_reduce_scatter(int weighted,
+                                  const void* src, int64_t num_src_rows, int64_t src_row_stride,
+                                  const int32_t* table, int64_t table_stride, int table_width,
+                                  const float* row_weights,
+                                  const uint64_t* out_rows, int num_units, int hidden,
+                                  const int32_t* wtable, int64_t wtable_stride,
+                                  const float* wsrc, int num_weights, int64_t weights_offset,
+                                  int32_t* error_flag, deepep_stream_t stream);
 
 /* ElasticBuffer::get_combine_buffer_size for one node (num_scaleout_ranks == 1). */
 int64_t deepep_combine_buffer_size(int num_max_tokens_per_rank, int hidden, int num_topk,

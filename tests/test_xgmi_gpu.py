@@ -1,0 +1,134 @@
+"""The xGMI transport (symmetric windows + device barrier, deepep_amd/symmetric.py) on the GPU.
+
+World-size 2 and 4 run as separate processes sharing the box's one GPU: every rank opens its
+peers' windows through HIP IPC, phase A stores partial rows straight into the owners' windows
+and the device barrier orders the phases -- the same code path as on an 8-GPU node, with the
+peer stores landing in the same HBM instead of crossing xGMI.  Results are compared bitwise with
+oracle.combine_ep (the CPU restatement pinned to refs.combine) and with the RCCL-path combine.
+"""
+import os
+import socket
+import sys
+import traceback
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def _u16(t: torch.Tensor) -> np.ndarray:
+    return t.detach().cpu().contiguous().view(torch.int16).numpy().view(np.uint16)
+
+
+def _bf16(a: np.ndarray, dev) -> torch.Tensor:
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.int16)).view(torch.bfloat16).to(dev)
+
+
+def _worker(rank, world, port, seed, T, H, K, queue):
+    sys.path.insert(0, ROOT)
+    try:
+        os.environ['MASTER_ADDR'] = '127.0.0.1'
+        os.environ['MASTER_PORT'] = str(port)
+        import torch.distributed as dist
+        torch.cuda.set_device(0)
+        dist.init_process_group('gloo', rank=rank, world_size=world)
+        import oracle
+        from deepep_amd import ElasticBuffer
+        dev = torch.device('cuda', 0)
+        E = 8 * world
+        rng = np.random.default_rng(seed)
+        idx_all, w_all, y_all, b_all = [], [], [], []
+        for r in range(world):
+            idx = np.stack([rng.permutation(E)[:K] for _ in range(T)]).astype(np.int64)
+            idx[rng.random((T, K)) < 0.15] = -1
+            idx[0] = -1                                   # a token routed nowhere
+            w = rng.random((T, K)).astype(np.float32) * (idx >= 0)
+            y = oracle.f32_to_bf16(rng.standard_normal((T, K, H)).astype(np.float32))
+            y[idx < 0] = 0
+            idx_all.append(idx), w_all.append(w), y_all.append(y)
+            b_all.append(oracle.f32_to_bf16(rng.standard_normal((T, H)).astype(np.float32)))
+        disp = oracle.simulate_dispatch(idx_all, E, T)
+        x_exp_all, w_exp_all = [], []
+        for r, d in enumerate(disp):
+            xe = np.zeros((d['num_expanded'], H), np.uint16)
+            we = np.zeros((d['num_expanded'],), np.float32)
+            for row, (g, k) in enumerate(d['expanded_src']):
+                s, t = divmod(int(g), T)
+                xe[row], we[row] = y_all[s][t, k], w_all[s][t, k]
+            x_exp_all.append(xe), w_exp_all.append(we)
+        failures = []
+        bufs = {}
+        for transport in ('xgmi', 'rccl'):
+            os.environ['DEEPEP_TRANSPORT'] = transport
+            bufs[transport] = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=T, hidden=H, num_topk=K,
+                                            explicitly_destroy=True, num_gpu_timeout_secs=20)
+        x = torch.zeros((T, H), dtype=torch.bfloat16, device=dev)
+        buf = bufs['xgmi']
+        _, _, ex_w, handle, _ = buf.dispatch(x, topk_idx=torch.from_numpy(idx_all[rank]).to(dev),
+                                             topk_weights=torch.from_numpy(w_all[rank]).to(dev),
+                                             num_experts=E, do_expand=True)
+        if not np.array_equal(handle.recv_src_metadata.cpu().numpy(), disp[rank]['src_metadata']):
+            failures.append('recv_src_metadata differs from the oracle dispatch')
+        for nb in (0, 1):
+            expect = oracle.combine_ep(x_exp_all, [d['src_metadata'] for d in disp], idx_all, E, T, expanded=True,
+                                       topk_weights_per_rank=w_exp_all,
+                                       bias_per_rank=[(b if nb else None, None) for b in b_all])
+            bias = _bf16(b_all[rank], dev) if nb else None
+            for it in range(3):                           # repeated calls reuse the windows (epochs)
+                for transport, b in bufs.items():
+                    out, out_w, _ = b.combine(_bf16(x_exp_all[rank], dev), handle, topk_weights=ex_w, bias=bias)
+                    torch.cuda.current_stream().synchronize()
+                    if not np.array_equal(_u16(out), expect[rank][0]):
+                        failures.append(f'{transport} combined_x (bias {nb}, call {it})')
+                    if not np.array_equal(out_w.cpu().numpy(), expect[rank][1]):
+                        failures.append(f'{transport} combined_topk_weights (bias {nb}, call {it})')
+        # gating-weighted variant: xGMI and RCCL paths agree bit for bit
+        outs = {}
+        for transport, b in bufs.items():
+            outs[transport], _, _ = b.combine(_bf16(x_exp_all[rank], dev), handle, topk_weights=ex_w,
+                                              apply_topk_weights=True)
+        if not torch.equal(outs['xgmi'], outs['rccl']):
+            failures.append('weighted: xgmi != rccl')
+        if bufs['xgmi']._sym is None:
+            failures.append('xgmi transport did not create its window')
+        else:
+            bufs['xgmi']._sym.check()
+        for b in bufs.values():
+            b.destroy()
+        queue.put((rank, failures))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:
+        queue.put((rank, [traceback.format_exc()]))
+
+
+@pytest.mark.parametrize('world,T,H,K', [(2, 96, 1024, 8), (4, 64, 7168, 8), (4, 80, 256, 2)])
+def test_xgmi_transport_matches_oracle(world, T, H, K):
+    ctx = mp.get_context('spawn')
+    queue = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, 100 + world + K, T, H, K, queue))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    results = {}
+    try:
+        for _ in range(world):
+            rank, failures = queue.get(timeout=300)
+            results[rank] = failures
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    assert len(results) == world and not any(results.values()), results

@@ -41,13 +41,14 @@ SIGNATURES = {
     'deepep_build_local_plan': (_I, [_P, _I, _I, _I, _I, _P, _I, _I, _P, _P, _P]),
     'deepep_set_launch_config': (_I, [_I, _I, _I]),
     'deepep_combine_buffer_size': (_I64, [_I, _I, _I, _I, _I]),
-    'deepep_dispatch_route': (_I, [_P, _I, _I, _I, _I, _P, _P, _P]),
+    'deepep_dispatch_route': (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P]),
     'deepep_dispatch_pack': (_I, [_P, _I64, _I, _P, _I64, _I, _P, _P, _I, _I, _I, _P, _P, _I,
                                   _P, _I64, _I, _I, _I, _I, _P]),
     'deepep_dispatch_count': (_I, [_P, _I64, _I, _I, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P]),
     'deepep_dispatch_scan': (_I, [_P, _I, _I, _I, _I, _P, _P, _P]),
     'deepep_dispatch_slots': (_I, [_P, _I64, _I, _I, _I, _I, _I, _P, _P, _P]),
-    'deepep_dispatch_copy': (_I, [_P, _I64, _I, _I, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P]),
+    'deepep_dispatch_copy': (_I, [_P, _I64, _I, _I, _I, _I, _I, _I, _P, _I, _P, _I64, _P, _I64, _I,
+                                  _P, _P, _P, _P]),
     'deepep_sym_alloc': (_I, [_I64, ctypes.POINTER(ctypes.c_void_p)]),
     'deepep_sym_free': (_I, [_P]),
     'deepep_sym_export': (_I, [_P, _P]),

@@ -363,28 +363,32 @@ class ElasticBuffer:
             dst_slot = torch.empty((T, R), dtype=torch.int32, device=dev)
             send_counts = torch.empty((R,), dtype=torch.int32, device=dev)
             kern.dispatch_route(idx64, num_experts, R, dst_slot, send_counts, stream=stream)
-            recv_counts_t = torch.empty_like(send_counts)
-            self._a2a(recv_counts_t, send_counts)
-            send_counts_l = [int(v) for v in send_counts.tolist()]          # host sync, as do_cpu_sync
-            recv_counts_l = [int(v) for v in recv_counts_t.tolist()]
+            if R == 1:
+                recv_counts_t = send_counts
+            else:
+                recv_counts_t = torch.empty_like(send_counts)
+                self._a2a(recv_counts_t, send_counts)
+            counts_l = [int(v) for v in torch.cat([send_counts, recv_counts_t]).tolist()]   # host sync, as do_cpu_sync
+            send_counts_l, recv_counts_l = counts_l[:R], counts_l[R:]
             N = sum(recv_counts_l)
             x_bytes = x.contiguous().view(torch.uint8).view(T, H * x.element_size())
             sf_bytes = sf.contiguous().view(torch.uint8).view(T, -1) if sf is not None else None
-            layout = RowLayout.make(x_bytes.shape[1], sf_bytes.shape[1] if sf is not None else 0, K)
-            offsets = [0] * R
-            for i in range(1, R):
-                offsets[i] = offsets[i - 1] + send_counts_l[i - 1]
-            send_offsets = torch.tensor(offsets, dtype=torch.int32, device=dev)
+            # One rank: nothing is exchanged, so the packed rows carry only the routing metadata and
+            # the copy reads x (and the scale factors) once, straight from the caller's tensors.
+            direct = R == 1
+            layout = (RowLayout.make(0, 0, K) if direct else
+                      RowLayout.make(x_bytes.shape[1], sf_bytes.shape[1] if sf is not None else 0, K))
+            send_offsets = (torch.cumsum(send_counts, 0) - send_counts).to(torch.int32)
             packed = torch.empty((sum(send_counts_l), layout.row_bytes), dtype=torch.uint8, device=dev)
-            kern.dispatch_pack(x_bytes, sf_bytes, idx64, w, r * num_max_tokens_per_rank, dst_slot, send_offsets,
-                               packed, layout, stream=stream)
+            kern.dispatch_pack(x_bytes[:, :0] if direct else x_bytes, None if direct else sf_bytes, idx64, w,
+                               r * num_max_tokens_per_rank, dst_slot, send_offsets, packed, layout, stream=stream)
             if R == 1:
                 recv_packed = packed
             else:
                 recv_packed = torch.empty((N, layout.row_bytes), dtype=torch.uint8, device=dev)
                 self._a2a(recv_packed, packed, recv_counts_l, send_counts_l)
             # --- receive side (dispatch_copy_epilogue_impl): metadata, expert layout, copies
-            psum_rank = torch.tensor(recv_counts_l, dtype=torch.int64).cumsum(0).to(torch.int32).to(dev)
+            psum_rank = torch.cumsum(recv_counts_t, 0).to(torch.int32)
             meta = torch.empty((N, K + 2), dtype=torch.int32, device=dev)
             out_idx = None if do_expand else torch.empty((N, K), dtype=torch.int64, device=dev)
             nblocks = (N + 255) // 256
@@ -418,7 +422,9 @@ class ElasticBuffer:
                          torch.empty((N, K), dtype=torch.float32, device=dev))
             kern.dispatch_copy(recv_packed, layout, N, meta, do_expand,
                                out_x.view(torch.uint8), out_sf.view(torch.uint8) if out_sf is not None else None,
-                               out_w, stream=stream)
+                               out_w, x_direct=x_bytes if direct else None,
+                               sf_direct=sf_bytes if direct else None, num_max_tokens=num_max_tokens_per_rank,
+                               stream=stream)
             if out_idx is not None and topk_idx.dtype != torch.int64:
                 out_idx = out_idx.to(topk_idx.dtype)
             num_recv = N

@@ -19,6 +19,8 @@
 
 #include <stdio.h>
 
+#include <algorithm>
+
 #include "../../include/deepep_amd.h"
 
 extern "C" __attribute__((visibility("hidden"))) int deepep_amd_set_error(int code, const char* msg);
@@ -28,44 +30,69 @@ namespace {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // ---------------------------------------------------------------- route: token -> destination slots
-// One workgroup of 1024 threads.  dst_slot[t][r] = #{t' < t : t' routed to r} or -1;
-// send_counts[r] = #{t : t routed to r}.  (dispatch.cuh:79-258 notify + slot assignment.)
-__global__ void __launch_bounds__(1024)
-route_kernel(const int64_t* __restrict__ topk_idx, int T, int K, int epr, int R,
-             int32_t* __restrict__ dst_slot, int32_t* __restrict__ send_counts) {
-    __shared__ int32_t s_scan[1024];
-    const int tid = threadIdx.x;
-    const int per = (T + 1023) / 1024;
-    const int t0 = tid * per, t1 = min(T, t0 + per);
+// dst_slot[t][r] = #{t' < t : t' routed to r} or -1; send_counts[r] = #{t : t routed to r}
+// (dispatch.cuh:79-258 notify + slot assignment).  Two passes over 256-token blocks, one thread
+// per token: (1) per-block counts per destination rank; (2) each block sums the counts of the
+// blocks before it and ranks its tokens with per-wave ballots -- deterministic, no atomics on
+// global memory, and every launch spreads over ceil(T / 256) workgroups.
+__device__ __forceinline__ uint64_t route_mask(const int64_t* __restrict__ topk_idx, int t, int T, int K, int epr) {
+    uint64_t mask = 0;
+    if (t < T)
+        for (int k = 0; k < K; ++k) {
+            const int64_t e = topk_idx[static_cast<int64_t>(t) * K + k];
+            if (e >= 0) mask |= 1ull << static_cast<int>(e / epr);
+        }
+    return mask;
+}
+
+__global__ void __launch_bounds__(256)
+route_count_kernel(const int64_t* __restrict__ topk_idx, int T, int K, int epr, int R,
+                   int32_t* __restrict__ block_counts) {
+    __shared__ int32_t s_cnt[4][64];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const uint64_t mask = route_mask(topk_idx, blockIdx.x * 256 + tid, T, K, epr);
     for (int r = 0; r < R; ++r) {
-        int c = 0;
-        for (int t = t0; t < t1; ++t) {
-            bool hit = false;
-            for (int k = 0; k < K; ++k) {
-                const int64_t e = topk_idx[static_cast<int64_t>(t) * K + k];
-                hit |= e >= 0 && e / epr == r;
-            }
-            c += hit;
+        const int c = __popcll(__ballot((mask >> r) & 1ull));
+        if (lane == 0) s_cnt[wave][r] = c;
+    }
+    __syncthreads();
+    if (tid < R)
+        block_counts[static_cast<int64_t>(blockIdx.x) * R + tid] = s_cnt[0][tid] + s_cnt[1][tid] + s_cnt[2][tid] +
+                                                                   s_cnt[3][tid];
+}
+
+__global__ void __launch_bounds__(256)
+route_assign_kernel(const int64_t* __restrict__ topk_idx, int T, int K, int epr, int R,
+                    const int32_t* __restrict__ block_counts, int32_t* __restrict__ dst_slot,
+                    int32_t* __restrict__ send_counts) {
+    __shared__ int32_t s_base[64];
+    __shared__ int32_t s_cnt[4][64];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int b = blockIdx.x, nb = gridDim.x;
+    if (tid < R) {
+        int base = 0;
+        for (int j = 0; j < b; ++j) base += block_counts[static_cast<int64_t>(j) * R + tid];
+        s_base[tid] = base;
+        if (b == nb - 1) send_counts[tid] = base + block_counts[static_cast<int64_t>(b) * R + tid];
+    }
+    const int t = b * 256 + tid;
+    const uint64_t mask = route_mask(topk_idx, t, T, K, epr);
+    for (int r = 0; r < R; ++r) {
+        const int c = __popcll(__ballot((mask >> r) & 1ull));
+        if (lane == 0) s_cnt[wave][r] = c;
+    }
+    __syncthreads();
+    if (t >= T) return;
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    for (int r = 0; r < R; ++r) {
+        const bool hit = (mask >> r) & 1ull;
+        const uint64_t bal = __ballot(hit);
+        int slot = -1;
+        if (hit) {
+            slot = s_base[r] + __popcll(bal & lt);
+            for (int w = 0; w < wave; ++w) slot += s_cnt[w][r];
         }
-        s_scan[tid] = c;
-        __syncthreads();
-        for (int off = 1; off < 1024; off <<= 1) {          // inclusive Hillis-Steele scan
-            const int v = tid >= off ? s_scan[tid - off] : 0;
-            __syncthreads();
-            s_scan[tid] += v;
-            __syncthreads();
-        }
-        int base = s_scan[tid] - c;
-        if (tid == 1023) send_counts[r] = s_scan[1023];
-        for (int t = t0; t < t1; ++t) {
-            bool hit = false;
-            for (int k = 0; k < K; ++k) {
-                const int64_t e = topk_idx[static_cast<int64_t>(t) * K + k];
-                hit |= e >= 0 && e / epr == r;
-            }
-            dst_slot[static_cast<int64_t>(t) * R + r] = hit ? base++ : -1;
-        }
-        __syncthreads();
+        dst_slot[static_cast<int64_t>(t) * R + r] = slot;
     }
 }
 
@@ -157,36 +184,50 @@ count_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int idx_off,
 }
 
 // One thread per local expert: offsets of every workgroup inside the expert's group, expert starts
-// aligned to expert_alignment, and the handle's prefix sums (elastic.py:36-45 semantics).
+// aligned to expert_alignment, and the handle's prefix sums (elastic.py:36-45 semantics).  The
+// per-block counts are read 16 at a time so the loads of a thread are in flight together.
 __global__ void __launch_bounds__(1024)
 scan_kernel(int32_t* __restrict__ block_counts, int nblocks, int epr, int align, int expanded,
             int32_t* __restrict__ expert_counts, int32_t* __restrict__ psum_expert) {
+    constexpr int kBatch = 16;
     __shared__ int32_t s_aligned[1024];
-    __shared__ int32_t s_start[1024];
     const int e = threadIdx.x;
     int total = 0;
     if (e < epr) {
-        for (int b = 0; b < nblocks; ++b) {             // exclusive scan over workgroups, in place
-            const int c = block_counts[static_cast<int64_t>(b) * epr + e];
-            block_counts[static_cast<int64_t>(b) * epr + e] = total;
-            total += c;
+        for (int b0 = 0; b0 < nblocks; b0 += kBatch) {
+            int c[kBatch];
+#pragma unroll
+            for (int j = 0; j < kBatch; ++j)
+                c[j] = b0 + j < nblocks ? block_counts[static_cast<int64_t>(b0 + j) * epr + e] : 0;
+#pragma unroll
+            for (int j = 0; j < kBatch; ++j) total += c[j];
         }
         expert_counts[e] = total;
     }
     s_aligned[e] = e < epr ? (total + align - 1) / align * align : 0;
     __syncthreads();
-    if (e == 0) {                                       // epr <= 1024: a serial scan is fine here
-        int run = 0;
-        for (int j = 0; j < epr; ++j) {
-            s_start[j] = run;
-            run += s_aligned[j];
-        }
+    for (int off = 1; off < 1024; off <<= 1) {          // inclusive scan of the aligned group sizes
+        const int v = e >= off ? s_aligned[e - off] : 0;
+        __syncthreads();
+        s_aligned[e] += v;
+        __syncthreads();
     }
-    __syncthreads();
+    const int aligned = e < epr ? (total + align - 1) / align * align : 0;
+    const int start = s_aligned[e] - aligned;
     if (e < epr) {
-        psum_expert[e] = expanded ? s_start[e] + total : s_start[e] + s_aligned[e];
-        for (int b = 0; b < nblocks; ++b)
-            block_counts[static_cast<int64_t>(b) * epr + e] += s_start[e];
+        psum_expert[e] = expanded ? start + total : start + aligned;
+        int run = start;
+        for (int b0 = 0; b0 < nblocks; b0 += kBatch) {
+            int c[kBatch];
+#pragma unroll
+            for (int j = 0; j < kBatch; ++j)
+                c[j] = b0 + j < nblocks ? block_counts[static_cast<int64_t>(b0 + j) * epr + e] : 0;
+#pragma unroll
+            for (int j = 0; j < kBatch; ++j) {
+                if (b0 + j < nblocks) block_counts[static_cast<int64_t>(b0 + j) * epr + e] = run;
+                run += c[j];
+            }
+        }
     }
 }
 
@@ -222,32 +263,58 @@ slots_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int idx_off,
     }
 }
 
-// One wave per received row: x (and sf) to recv_x[i] (non-expanded) or to every local slot
-// (expanded); weights to recv_topk_weights[i][k] or [slot].
-__global__ void __launch_bounds__(64)
+// x (and sf) of received row i to recv_x[i] (non-expanded) or to every local slot (expanded);
+// weights to recv_topk_weights[i][k] or [slot].  Work item = (row, 2 KiB column chunk): one wave
+// per item, 4 items per 256-thread workgroup (the combine kernel's tiling, mirrored: one load, up
+// to K stores per lane and vector).  The x rows come from the packed receive row, or -- one rank,
+// nothing exchanged -- straight from the sender's x / sf (x_direct: row = src_global_idx %
+// num_max_tokens), so x is read once.  Row stores are write-through buffer stores (sc1).
+__global__ void __launch_bounds__(256)
 copy_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int x_bytes, int sf_off, int sf_bytes, int w_off,
             int N, int K, const int32_t* __restrict__ meta, int expanded,
+            const uint8_t* __restrict__ x_direct, int64_t x_direct_stride,
+            const uint8_t* __restrict__ sf_direct, int64_t sf_direct_stride, int num_max_tokens,
             uint8_t* __restrict__ recv_x, uint8_t* __restrict__ recv_sf, float* __restrict__ recv_w) {
-    const int i = blockIdx.x, lane = threadIdx.x;
-    const uint8_t* row = packed + static_cast<int64_t>(i) * row_bytes;
+    constexpr int kChunkVecs = 128;                        // 64 lanes x 2 x 16 B
+    const int lane = threadIdx.x & 63;
+    const int nvec = x_bytes / 16;
+    const int nchunks = max(1, (nvec + kChunkVecs - 1) / kChunkVecs);
+    const int64_t it = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+    if (it >= static_cast<int64_t>(N) * nchunks) return;
+    const int64_t i = it / nchunks;
+    const int c = static_cast<int>(it - i * nchunks);
+    const uint8_t* row = packed + i * row_bytes;
+    const uint8_t* xs = row;
+    const uint8_t* sfs = row + sf_off;
+    if (x_direct != nullptr) {
+        const int64_t t = meta[i * (K + 2)] % num_max_tokens;
+        xs = x_direct + t * x_direct_stride;
+        sfs = sf_direct != nullptr ? sf_direct + t * sf_direct_stride : nullptr;
+    }
     // lane k holds the destination row of lane k's slot (expanded) or lane 0 holds i
     int32_t my_dst = -1;
     if (expanded) {
-        if (lane < K) my_dst = meta[static_cast<int64_t>(i) * (K + 2) + 2 + lane];
+        if (lane < K) my_dst = meta[i * (K + 2) + 2 + lane];
     } else if (lane == 0) {
-        my_dst = i;
+        my_dst = static_cast<int32_t>(i);
     }
     const uint64_t dmask = __ballot(my_dst >= 0);
-    for (int v = lane; v < x_bytes / 16; v += 64) {
-        const u32x4 val = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(row) + v);
-        for (uint64_t m = dmask; m; m &= m - 1) {
-            const int64_t d = __builtin_amdgcn_readlane(my_dst, __builtin_ctzll(m));
-            reinterpret_cast<u32x4*>(recv_x + d * x_bytes)[v] = val;
-        }
+    const int v0 = c * kChunkVecs + lane, v1 = v0 + 64;
+    const u32x4 zero = {0u, 0u, 0u, 0u};
+    const u32x4 a0 = v0 < nvec ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(xs) + v0) : zero;
+    const u32x4 a1 = v1 < nvec ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(xs) + v1) : zero;
+    for (uint64_t m = dmask; m; m &= m - 1) {
+        const int64_t d = __builtin_amdgcn_readlane(my_dst, __builtin_ctzll(m));
+        // the descriptor's range check drops the lanes past the row end
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(recv_x + d * x_bytes, 0, x_bytes,
+                                                                            0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(a0, rs, v0 * 16, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(a1, rs, v1 * 16, 0, 16);
     }
-    if (recv_sf != nullptr)
+    if (c != 0) return;
+    if (recv_sf != nullptr && sfs != nullptr)
         for (int v = lane; v < sf_bytes / 4; v += 64) {
-            const uint32_t val = reinterpret_cast<const uint32_t*>(row + sf_off)[v];
+            const uint32_t val = reinterpret_cast<const uint32_t*>(sfs)[v];
             for (uint64_t m = dmask; m; m &= m - 1) {
                 const int64_t d = __builtin_amdgcn_readlane(my_dst, __builtin_ctzll(m));
                 reinterpret_cast<uint32_t*>(recv_sf + d * sf_bytes)[v] = val;
@@ -258,7 +325,7 @@ copy_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int x_bytes, 
         if (expanded) {
             if (my_dst >= 0) recv_w[my_dst] = w;
         } else {
-            recv_w[static_cast<int64_t>(i) * K + lane] = w;
+            recv_w[i * K + lane] = w;
         }
     }
 }
@@ -280,12 +347,22 @@ bool a16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 extern "C" {
 
 int deepep_dispatch_route(const int64_t* topk_idx, int num_tokens, int num_topk, int num_experts, int num_ranks,
-                          int32_t* dst_slot, int32_t* send_counts, deepep_stream_t stream) {
+                          int32_t* dst_slot, int32_t* send_counts, int32_t* block_counts, deepep_stream_t stream) {
     if (num_tokens < 0 || num_topk < 1 || num_topk > 32 || num_ranks < 1 || num_ranks > 64 ||
-        num_experts % num_ranks != 0 || send_counts == nullptr || (num_tokens > 0 && (dst_slot == nullptr || topk_idx == nullptr)))
+        num_experts % num_ranks != 0 || send_counts == nullptr ||
+        (num_tokens > 0 && (dst_slot == nullptr || topk_idx == nullptr || block_counts == nullptr)))
         return deepep_amd_set_error(DEEPEP_ERR_INVALID_ARG, "dispatch_route: invalid arguments");
-    hipLaunchKernelGGL(route_kernel, dim3(1), dim3(1024), 0, reinterpret_cast<hipStream_t>(stream),
-                       topk_idx, num_tokens, num_topk, num_experts / num_ranks, num_ranks, dst_slot, send_counts);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (num_tokens == 0) {
+        const hipError_t e = hipMemsetAsync(send_counts, 0, sizeof(int32_t) * num_ranks, s);
+        return e == hipSuccess ? DEEPEP_OK : launch_status("dispatch_route memset");
+    }
+    const int nb = (num_tokens + 255) / 256;
+    const int epr = num_experts / num_ranks;
+    hipLaunchKernelGGL(route_count_kernel, dim3(nb), dim3(256), 0, s, topk_idx, num_tokens, num_topk, epr, num_ranks,
+                       block_counts);
+    hipLaunchKernelGGL(route_assign_kernel, dim3(nb), dim3(256), 0, s, topk_idx, num_tokens, num_topk, epr, num_ranks,
+                       block_counts, dst_slot, send_counts);
     return launch_status("dispatch_route");
 }
 
@@ -351,15 +428,24 @@ int deepep_dispatch_slots(const void* packed, int64_t row_bytes, int idx_off, in
 
 int deepep_dispatch_copy(const void* packed, int64_t row_bytes, int x_bytes, int sf_off, int sf_bytes, int w_off,
                          int num_recv, int num_topk, const int32_t* src_metadata, int expanded,
+                         const void* x_direct, int64_t x_direct_stride_bytes,
+                         const void* sf_direct, int64_t sf_direct_stride_bytes, int num_max_tokens,
                          void* recv_x, void* recv_sf, float* recv_topk_weights, deepep_stream_t stream) {
     if (num_recv == 0) return DEEPEP_OK;
     if (num_recv < 0 || num_topk < 1 || num_topk > 32 || x_bytes % 16 || row_bytes % 16 || !a16(packed) ||
-        !a16(recv_x) || (recv_sf != nullptr && sf_bytes % 4) || src_metadata == nullptr)
+        !a16(recv_x) || (recv_sf != nullptr && sf_bytes % 4) || src_metadata == nullptr ||
+        (x_direct != nullptr && (!a16(x_direct) || x_direct_stride_bytes % 16 || num_max_tokens < 1 ||
+                                 (recv_sf != nullptr && sf_direct == nullptr))))
         return deepep_amd_set_error(DEEPEP_ERR_INVALID_ARG, "dispatch_copy: invalid arguments or alignment");
-    hipLaunchKernelGGL(copy_kernel, dim3(num_recv), dim3(64), 0, reinterpret_cast<hipStream_t>(stream),
+    const int64_t nchunks = std::max<int64_t>(1, (x_bytes / 16 + 127) / 128);
+    const int64_t items = static_cast<int64_t>(num_recv) * nchunks;
+    hipLaunchKernelGGL(copy_kernel, dim3(static_cast<unsigned>((items + 3) / 4)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream),
                        static_cast<const uint8_t*>(packed), row_bytes, x_bytes, sf_off, sf_bytes, w_off,
-                       num_recv, num_topk, src_metadata, expanded, static_cast<uint8_t*>(recv_x),
-                       static_cast<uint8_t*>(recv_sf), recv_topk_weights);
+                       num_recv, num_topk, src_metadata, expanded,
+                       static_cast<const uint8_t*>(x_direct), x_direct_stride_bytes,
+                       static_cast<const uint8_t*>(sf_direct), sf_direct_stride_bytes, num_max_tokens,
+                       static_cast<uint8_t*>(recv_x), static_cast<uint8_t*>(recv_sf), recv_topk_weights);
     return launch_status("dispatch_copy");
 }
 

@@ -154,8 +154,9 @@ class HipKernels:
     def dispatch_route(self, topk_idx, num_experts, num_ranks, dst_slot, send_counts, stream=None):
         _require(topk_idx.is_cuda and topk_idx.dtype == torch.int64 and topk_idx.is_contiguous(), 'topk_idx int64')
         T, K = topk_idx.shape
+        block_counts = torch.empty((max(1, (T + 255) // 256) * num_ranks,), dtype=torch.int32, device=topk_idx.device)
         rc = self.lib.deepep_dispatch_route(ptr(topk_idx), T, K, num_experts, num_ranks, ptr(dst_slot),
-                                            ptr(send_counts), _stream_handle(stream))
+                                            ptr(send_counts), ptr(block_counts), _stream_handle(stream))
         _lib.check(rc, 'dispatch_route')
 
     def dispatch_pack(self, x_bytes, sf_bytes, topk_idx, topk_weights, src_base, dst_slot, send_offsets,
@@ -193,10 +194,18 @@ class HipKernels:
         _lib.check(rc, 'dispatch_slots')
 
     def dispatch_copy(self, packed, layout: RowLayout, num_recv, meta, expanded, recv_x_bytes, recv_sf_bytes,
-                      recv_w, stream=None):
-        rc = self.lib.deepep_dispatch_copy(ptr(packed), layout.row_bytes, layout.x_bytes, layout.sf_off,
-                                           layout.sf_bytes, layout.w_off, num_recv, layout.num_topk, ptr(meta),
-                                           int(expanded), ptr(recv_x_bytes), ptr(recv_sf_bytes), ptr(recv_w),
+                      recv_w, x_direct=None, sf_direct=None, num_max_tokens: int = 0, stream=None):
+        """x_direct / sf_direct: [T, bytes] uint8 views of the sender's rows (one rank: the packed rows
+        then carry only metadata and row i's x is x_direct[src_metadata[i][0] % num_max_tokens])."""
+        x_bytes = x_direct.shape[1] if x_direct is not None else layout.x_bytes
+        sf_bytes = sf_direct.shape[1] if sf_direct is not None else layout.sf_bytes
+        rc = self.lib.deepep_dispatch_copy(ptr(packed), layout.row_bytes, x_bytes, layout.sf_off,
+                                           sf_bytes, layout.w_off, num_recv, layout.num_topk, ptr(meta),
+                                           int(expanded),
+                                           ptr(x_direct), x_direct.stride(0) if x_direct is not None else 0,
+                                           ptr(sf_direct), sf_direct.stride(0) if sf_direct is not None else 0,
+                                           num_max_tokens,
+                                           ptr(recv_x_bytes), ptr(recv_sf_bytes), ptr(recv_w),
                                            _stream_handle(stream))
         _lib.check(rc, 'dispatch_copy')
 

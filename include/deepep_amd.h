@@ -131,9 +131,10 @@ int deepep_set_launch_config(int vec_per_lane, int stage_lds, int store_policy);
 
 /* dst_slot[t][r] = #{t' < t routed to rank r} or -1 (int32 [num_tokens][num_ranks]);
  * send_counts[r] = tokens routed to rank r.  A token is routed to r when one of its top-k experts
- * lives on r (experts_per_rank = num_experts / num_ranks). */
+ * lives on r (experts_per_rank = num_experts / num_ranks).  block_counts: int32 scratch of
+ * ceil(num_tokens / 256) * num_ranks entries. */
 int deepep_dispatch_route(const int64_t* topk_idx, int num_tokens, int num_topk, int num_experts, int num_ranks,
-                          int32_t* dst_slot, int32_t* send_counts, deepep_stream_t stream);
+                          int32_t* dst_slot, int32_t* send_counts, int32_t* block_counts, deepep_stream_t stream);
 
 /* Write packed row send_offsets[r] + dst_slot[t][r] for every (token t, destination r);
  * src_global_idx = src_base + t.  topk_weights may be NULL (zeros are sent). */
@@ -165,9 +166,13 @@ int deepep_dispatch_slots(const void* packed, int64_t row_bytes, int idx_off, in
                           deepep_stream_t stream);
 
 /* Pass 4: recv_x / recv_sf rows (row i, or every local slot when expanded) and top-k weights
- * ([num_recv][K] or, expanded, [slot]).  recv_sf / recv_topk_weights may be NULL. */
+ * ([num_recv][K] or, expanded, [slot]).  recv_sf / recv_topk_weights may be NULL.  With x_direct
+ * (one rank: nothing was exchanged, the packed rows carry only metadata) the x / sf bytes of row i
+ * are read from x_direct / sf_direct at row src_metadata[i][0] % num_max_tokens. */
 int deepep_dispatch_copy(const void* packed, int64_t row_bytes, int x_bytes, int sf_off, int sf_bytes, int w_off,
                          int num_recv, int num_topk, const int32_t* src_metadata, int expanded,
+                         const void* x_direct, int64_t x_direct_stride_bytes,
+                         const void* sf_direct, int64_t sf_direct_stride_bytes, int num_max_tokens,
                          void* recv_x, void* recv_sf, float* recv_topk_weights, deepep_stream_t stream);
 
 /* ------------------------------------------------------------------ symmetric buffer over xGMI

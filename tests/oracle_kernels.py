@@ -124,14 +124,20 @@ class OracleKernels:
                         run[e] += 1
 
     def dispatch_copy(self, packed, layout, num_recv, meta, expanded, recv_x_bytes, recv_sf_bytes, recv_w,
-                      stream=None):
+                      x_direct=None, sf_direct=None, num_max_tokens=0, stream=None):
         N, K = num_recv, layout.num_topk
-        xs = packed[:N, :layout.x_bytes]
+        if x_direct is not None:
+            t = (meta[:N, 0].long() % num_max_tokens)
+            xs = x_direct[t]
+            sfs = sf_direct[t] if sf_direct is not None else None
+        else:
+            xs = packed[:N, :layout.x_bytes]
+            sfs = packed[:N, layout.sf_off:layout.sf_off + layout.sf_bytes]
         w = packed[:N, layout.w_off:layout.w_off + 4 * K].contiguous().view(torch.float32).view(N, K)
         if not expanded:
             recv_x_bytes[:N] = xs
             if recv_sf_bytes is not None:
-                recv_sf_bytes[:N] = packed[:N, layout.sf_off:layout.sf_off + layout.sf_bytes]
+                recv_sf_bytes[:N] = sfs
             if recv_w is not None:
                 recv_w[:N] = w
             return
@@ -139,6 +145,6 @@ class OracleKernels:
         rows = meta[ii, 2 + kk].long()
         recv_x_bytes[rows] = xs[ii]
         if recv_sf_bytes is not None:
-            recv_sf_bytes[rows] = packed[ii, layout.sf_off:layout.sf_off + layout.sf_bytes]
+            recv_sf_bytes[rows] = sfs[ii]
         if recv_w is not None:
             recv_w[rows] = w[ii, kk]

@@ -33,8 +33,9 @@ def _routing(T, E, K, R, masked, skew, gen):
     return idx, w
 
 
-def _run_dispatch(kern, dev, ranks, E, K, H, T_max, expanded, alignment, fp8):
-    """Both halves of the dispatch for every rank with `kern`; returns per-rank outputs on the CPU."""
+def _run_dispatch(kern, dev, ranks, E, K, H, T_max, expanded, alignment, fp8, direct=False):
+    """Both halves of the dispatch for every rank with `kern`; returns per-rank outputs on the CPU.
+    direct (one rank): metadata-only packed rows, the copy reads x / sf from the sender's tensors."""
     from deepep_amd.kernels import RowLayout
     R = len(ranks)
     epr = E // R
@@ -49,11 +50,13 @@ def _run_dispatch(kern, dev, ranks, E, K, H, T_max, expanded, alignment, fp8):
         cl = [int(v) for v in cnt.tolist()]
         xb = x.view(torch.uint8).view(T, -1)
         sb = sf.view(torch.uint8).view(T, -1) if sf is not None else None
-        layout = RowLayout.make(xb.shape[1], sb.shape[1] if sb is not None else 0, K)
+        layout = (RowLayout.make(0, 0, K) if direct else
+                  RowLayout.make(xb.shape[1], sb.shape[1] if sb is not None else 0, K))
         offs = torch.tensor([sum(cl[:i]) for i in range(R)], dtype=torch.int32, device=dev)
         packed = torch.zeros((sum(cl), layout.row_bytes), dtype=torch.uint8, device=dev)
-        kern.dispatch_pack(xb, sb, idx, w, r * T_max, dst, offs, packed, layout)
-        sends.append((dst.cpu(), cl, packed, layout))
+        kern.dispatch_pack(xb[:, :0] if direct else xb, None if direct else sb, idx, w, r * T_max, dst, offs,
+                           packed, layout)
+        sends.append((dst.cpu(), cl, packed, layout, xb, sb))
     outs = []
     for r in range(R):
         parts = [sends[s][2][sum(sends[s][1][:r]):sum(sends[s][1][:r + 1])] for s in range(R)]
@@ -72,8 +75,8 @@ def _run_dispatch(kern, dev, ranks, E, K, H, T_max, expanded, alignment, fp8):
         kern.dispatch_scan(bc, epr, alignment, expanded, ec, pe)
         aligned = [(int(c) + alignment - 1) // alignment * alignment for c in ec.tolist()]
         if expanded:
-            kern.dispatch_slots(recv, layout, N, r, epr, bc, meta)
             rows = sum(aligned)
+            kern.dispatch_slots(recv, layout, N, r, epr, bc, meta)
         else:
             meta[:, 2:] = -1
             rows = N
@@ -82,7 +85,9 @@ def _run_dispatch(kern, dev, ranks, E, K, H, T_max, expanded, alignment, fp8):
         rsf = torch.zeros((rows, ranks[0][1].shape[1]), dtype=torch.float32, device=dev) if fp8 else None
         rw = torch.zeros((rows,) if expanded else (N, K), dtype=torch.float32, device=dev)
         kern.dispatch_copy(recv, layout, N, meta, expanded, rx.view(torch.uint8),
-                           rsf.view(torch.uint8) if rsf is not None else None, rw)
+                           rsf.view(torch.uint8) if rsf is not None else None, rw,
+                           x_direct=sends[r][4] if direct else None, sf_direct=sends[r][5] if direct else None,
+                           num_max_tokens=T_max)
         outs.append(dict(meta=meta.cpu(), ridx=None if ridx is None else ridx.cpu(), ec=ec.cpu(), pe=pe.cpu(),
                          rx=rx.cpu(), rsf=None if rsf is None else rsf.cpu(), rw=rw.cpu(), dst=sends[r][0],
                          cnt=sends[r][1]))
@@ -121,3 +126,28 @@ def test_dispatch_primitives_match_cpu(hip, R, K, E, T, H, expanded, alignment, 
         assert torch.equal(g['rw'], e['rw']), f'rank {r} weights'
         if fp8:
             assert torch.equal(g['rsf'], e['rsf']), f'rank {r} scale factors'
+
+
+@pytest.mark.parametrize('K,E,T,H,expanded,fp8', [
+    (8, 64, 300, 7168, True, False),
+    (2, 8, 128, 1024, False, False),
+    (8, 32, 257, 512, True, True),
+    (4, 16, 200, 256, False, True),
+])
+def test_dispatch_direct_copy_one_rank(hip, K, E, T, H, expanded, fp8):
+    """One rank: the metadata-only pack + direct copy gives the same handle and rows as the packed path."""
+    from deepep_amd.utils import per_token_cast_to_fp8
+    gen = torch.Generator().manual_seed(K * 100 + T)
+    idx, w = _routing(T, E, K, 1, 0.1, False, gen)
+    x = torch.randn((T, H), generator=gen).to(torch.bfloat16)
+    sf = None
+    if fp8:
+        x, sf = per_token_cast_to_fp8(x)
+    ranks = [(x, sf, idx, w)]
+    got = _run_dispatch(hip, 'cuda', ranks, E, K, H, T, expanded, 1, fp8, direct=True)[0]
+    exp = _run_dispatch(OracleKernels(), 'cpu', ranks, E, K, H, T, expanded, 1, fp8)[0]
+    assert torch.equal(got['meta'], exp['meta'])
+    assert torch.equal(got['rx'].view(torch.uint8), exp['rx'].view(torch.uint8))
+    assert torch.equal(got['rw'], exp['rw'])
+    if fp8:
+        assert torch.equal(got['rsf'], exp['rsf'])

@@ -16,8 +16,8 @@ def stats(path, out):
     rows = list(csv.DictReader(open(path)))
     lines = ['| kernel | calls | avg us | min us | max us | share % |', '|---|---|---|---|---|---|']
     for r in rows[:12]:
-        name = r['Name']
-        short = name.split('(')[0][:90] if 'combine_rows_kernel' not in name else name.split('((anonymous')[0]
+        name = r['Name'].replace('(anonymous namespace)::', '')
+        short = name.split('(')[0][:90]
         lines.append(f"| `{short}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.2f} | {float(r['MinNs']) / 1e3:.2f} | "
                      f"{float(r['MaxNs']) / 1e3:.2f} | {float(r['Percentage']):.1f} |")
     open(out, 'w').write('\n'.join(lines) + '\n')

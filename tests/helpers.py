@@ -72,3 +72,90 @@ def build_combine_inputs(fx, expert_alignment: int = 1):
         per_rank.append(dict(meta=meta, x_exp=x_exp, w_exp=w_exp, x_red=x_red, w2d=w2d,
                              num_expanded=d['num_expanded'], src_global_idx=d['src_global_idx']))
     return ranks, per_rank
+
+
+def dispatch_mode_checks(buf, x, topk_idx, topk_weights, num_experts: int, num_max_tokens: int,
+                         expert_alignment: int, do_cpu_sync: bool, do_handle_copy: bool) -> List[str]:
+    """The dispatch-mode checks of the reference test (tests/elastic/test_ep.py:143-177, 355-466):
+    cached dispatch (handle reuse), cached expanded dispatch with zero padding, handle copy,
+    deterministic repeat, the cumulative per-expert counter, per-expert prefix sums, and
+    do_cpu_sync=False worst-case shapes.  Works for any kernel provider and device; returns the
+    list of failed checks."""
+    import torch
+    fails = []
+    args = dict(topk_idx=topk_idx, topk_weights=topk_weights, num_experts=num_experts,
+                num_max_tokens_per_rank=num_max_tokens, expert_alignment=expert_alignment,
+                do_handle_copy=do_handle_copy, do_cpu_sync=do_cpu_sync)
+    recv_x, recv_idx, recv_w, handle, _ = buf.dispatch(x, **args)
+    ex_x, ex_idx, ex_w, ex_handle, _ = buf.dispatch(x, do_expand=True, **args)
+    c_x, c_idx, c_w, c_handle, _ = buf.dispatch(x, handle=handle)
+    ce_x, _, ce_w, _, _ = buf.dispatch(x, topk_weights=topk_weights, do_expand=True, do_zero_padding=True,
+                                       handle=ex_handle)
+
+    def rows(t):
+        return t[0] if isinstance(t, tuple) else t
+
+    def same(a, b):
+        if isinstance(a, tuple):
+            return all(torch.equal(p, q) for p, q in zip(a, b))
+        return torch.equal(a.view(torch.uint8) if a.dtype != torch.bool else a,
+                           b.view(torch.uint8) if b.dtype != torch.bool else b)
+
+    def head(t, n):
+        return tuple(p[:n] for p in t) if isinstance(t, tuple) else t[:n]
+
+    n = int(handle.psum_num_recv_tokens_per_scaleup_rank[-1].item())
+    if (topk_idx.data_ptr() != handle.topk_idx.data_ptr()) != do_handle_copy:
+        fails.append('handle copy')
+    if handle.topk_idx.data_ptr() != c_handle.topk_idx.data_ptr():
+        fails.append('cached handle does not share topk_idx')
+    if ex_idx is not None:
+        fails.append('expanded dispatch returned recv_topk_idx')
+    if not do_cpu_sync:
+        worst = num_max_tokens * buf.num_ranks
+        if rows(recv_x).shape[0] != worst or handle.recv_src_metadata.shape[0] != worst:
+            fails.append('do_cpu_sync=False shapes are not worst-case')
+    recv_x, recv_idx, recv_w = head(recv_x, n), recv_idx[:n], recv_w[:n]
+    meta, ex_meta = handle.recv_src_metadata[:n], ex_handle.recv_src_metadata[:n]
+    if not (same(head(c_x, n), recv_x) and torch.equal(c_idx[:n], recv_idx) and c_w is None):
+        fails.append('cached dispatch differs')
+    if not torch.equal(handle.dst_buffer_slot_idx, c_handle.dst_buffer_slot_idx) or \
+            handle.num_recv_tokens_per_expert_list != c_handle.num_recv_tokens_per_expert_list:
+        fails.append('cached handle differs')
+    slots = ex_meta[:, 2:]
+    valid = slots[slots >= 0].long()
+    def pick(t, idx):
+        return tuple(p[idx] for p in t) if isinstance(t, tuple) else t[idx]
+
+    if not (same(pick(ce_x, valid), pick(ex_x, valid)) and torch.equal(ce_w[valid], ex_w[valid])):
+        fails.append('cached expanded dispatch differs on valid rows')
+    epr = num_experts // buf.num_ranks
+    psum = [0] + [int(v) for v in ex_handle.psum_num_recv_tokens_per_expert.tolist()]
+    for e in range(epr):
+        start = psum[e + 1]
+        end = (start + expert_alignment - 1) // expert_alignment * expert_alignment
+        if bool((rows(ce_x)[start:end].float() != 0).any()) or bool((ce_w[start:end] != 0).any()):
+            fails.append(f'zero padding of expert {e}')
+            break
+    # deterministic repeat
+    r2 = buf.dispatch(x, **args)
+    if not (same(head(r2[0], n), recv_x) and torch.equal(r2[1][:n], recv_idx) and
+            torch.equal(r2[3].recv_src_metadata[:n], meta)):
+        fails.append('dispatch is not deterministic')
+    # cumulative per-expert counter and prefix sums (test_ep.py:446-462)
+    stats = torch.zeros((epr,), dtype=torch.int32, device=recv_idx.device)
+    buf.dispatch(x, cumulative_local_expert_recv_stats=stats, **args)
+    npsum = [0] + [int(v) for v in handle.psum_num_recv_tokens_per_expert.tolist()]
+    for e in range(epr):
+        ref = int((recv_idx == e).sum().item())
+        aligned = (ref + expert_alignment - 1) // expert_alignment * expert_alignment
+        if do_cpu_sync and (int(stats[e].item()) != ref or handle.num_recv_tokens_per_expert_list[e] != aligned):
+            fails.append(f'expert {e} counter')
+            break
+        al_prev = (psum[e] + expert_alignment - 1) // expert_alignment * expert_alignment
+        if npsum[e + 1] - npsum[e] != aligned or psum[e + 1] - al_prev != ref:
+            fails.append(f'expert {e} prefix sums')
+            break
+    if ex_handle.recv_src_metadata.shape[0] != (n if do_cpu_sync else num_max_tokens * buf.num_ranks):
+        fails.append('expanded metadata rows')
+    return fails

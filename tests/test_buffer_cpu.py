@@ -250,3 +250,54 @@ def test_random_routing_world(world, chunks):
             if p.is_alive():
                 p.kill()
     assert len(results) == world and not any(results.values()), results
+
+
+def _modes_worker(rank, world, port, alignment, do_cpu_sync, do_handle_copy, queue):
+    import sys
+    sys.path.insert(0, ROOT)
+    try:
+        os.environ['MASTER_ADDR'] = '127.0.0.1'
+        os.environ['MASTER_PORT'] = str(port)
+        dist.init_process_group('gloo', rank=rank, world_size=world)
+        from deepep_amd import ElasticBuffer
+        from tests.helpers import dispatch_mode_checks
+        from tests.oracle_kernels import OracleKernels
+        T, H, K, E = 40, 64, 4, 4 * world
+        g = torch.Generator().manual_seed(rank + 11)
+        scores = torch.rand((T, E), generator=g)
+        w, idx = torch.topk(scores, K, dim=-1, sorted=False)
+        idx = idx.to(torch.int64)
+        idx[torch.rand(idx.shape, generator=g) < 0.2] = -1
+        w = w.masked_fill(idx < 0, 0)
+        x = torch.randn((T, H), generator=g).to(torch.bfloat16)
+        buf = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=T, hidden=H, num_topk=K)
+        buf._kernels = OracleKernels()
+        queue.put((rank, dispatch_mode_checks(buf, x, idx, w, E, T, alignment, do_cpu_sync, do_handle_copy)))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:
+        queue.put((rank, [traceback.format_exc()]))
+
+
+@pytest.mark.parametrize('alignment,do_cpu_sync,do_handle_copy', [(1, True, True), (4, True, False), (8, False, True)])
+def test_dispatch_modes_world2(alignment, do_cpu_sync, do_handle_copy):
+    """Cached / cached-expanded-zero-padded / deterministic / counter / no-CPU-sync dispatch
+    (tests/elastic/test_ep.py:143-177, 355-466) over 2 gloo ranks."""
+    ctx = mp.get_context('spawn')
+    queue = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_modes_worker, args=(r, 2, port, alignment, do_cpu_sync, do_handle_copy, queue))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    results = {}
+    try:
+        for _ in range(2):
+            rank, failures = queue.get(timeout=240)
+            results[rank] = failures
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    assert len(results) == 2 and not any(results.values()), results

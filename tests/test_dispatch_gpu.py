@@ -151,3 +151,33 @@ def test_dispatch_direct_copy_one_rank(hip, K, E, T, H, expanded, fp8):
     assert torch.equal(got['rw'], exp['rw'])
     if fp8:
         assert torch.equal(got['rsf'], exp['rsf'])
+
+
+@pytest.mark.parametrize('alignment,do_cpu_sync,do_handle_copy,fp8', [
+    (1, True, True, False), (128, True, False, False), (4, False, True, False), (1, True, True, True)])
+def test_dispatch_modes_on_gpu(alignment, do_cpu_sync, do_handle_copy, fp8):
+    """ElasticBuffer.dispatch modes with the HIP kernels (EP = 1): cached, cached expanded with zero
+    padding, handle copy, deterministic repeat, the per-expert counter, no CPU sync
+    (tests/elastic/test_ep.py:143-177, 355-466)."""
+    import os
+    import torch.distributed as dist
+    from deepep_amd import ElasticBuffer
+    from deepep_amd.utils import per_token_cast_to_fp8
+    from tests.helpers import dispatch_mode_checks
+    if not dist.is_initialized():
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        os.environ.setdefault('MASTER_PORT', '29544')
+        dist.init_process_group('gloo', rank=0, world_size=1)
+    T, H, K, E = 1000, 2048, 8, 64
+    g = torch.Generator(device='cuda').manual_seed(alignment + 7)
+    scores = torch.rand((T, E), device='cuda', generator=g)
+    w, idx = torch.topk(scores, K, dim=-1, sorted=False)
+    idx = idx.to(torch.int64)
+    idx[torch.rand(idx.shape, device='cuda', generator=g) < 0.1] = -1
+    w = w.masked_fill(idx < 0, 0)
+    x = torch.randn((T, H), device='cuda', generator=g).to(torch.bfloat16)
+    if fp8:
+        x = per_token_cast_to_fp8(x)
+    buf = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=T, hidden=H, num_topk=K)
+    fails = dispatch_mode_checks(buf, x, idx, w, E, T, alignment, do_cpu_sync, do_handle_copy)
+    assert not fails, fails

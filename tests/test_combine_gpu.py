@@ -101,7 +101,7 @@ def _run(kern, mode, weighted, units, width, hidden, nb, seed, identity=False, s
 
 @pytest.mark.parametrize('mode', [MODE_LOCAL, MODE_EPILOGUE, MODE_FUSED])
 @pytest.mark.parametrize('width', [1, 2, 3, 8, 17, 32])
-@pytest.mark.parametrize('hidden', [64, 520, 7168])
+@pytest.mark.parametrize('hidden', [64, 520, 2056, 7168])
 def test_kernel_modes_widths(kern, mode, width, hidden):
     nbs = [0] if mode == MODE_LOCAL else [0, 1, 2]
     for nb in nbs:
@@ -121,6 +121,53 @@ def test_kernel_identity_table_and_special_values(kern, mode):
 def test_kernel_units_per_block(kern, upb):
     _run(kern, MODE_FUSED, False, 53, 8, 7168, 1, seed=upb, upb=upb)
     _run(kern, MODE_LOCAL, True, 53, 8, 7168, 0, seed=upb + 1, upb=upb, wt=False)
+
+
+@pytest.mark.parametrize('cfg', [(1, 0, 0), (1, 1, 1), (2, 0, 1), (2, 1, 0), (2, 0, 2), (0, -1, -1)])
+def test_kernel_launch_configs_identical(kern, cfg):
+    """Every deepep_set_launch_config variant (vector width, LDS staging, store policy) gives the
+    same bits (the tuning knobs of tools/kbench.py)."""
+    assert kern.lib.deepep_set_launch_config(*cfg) == 0
+    try:
+        for mode in (MODE_LOCAL, MODE_EPILOGUE, MODE_FUSED):
+            _run(kern, mode, False, 29, 8, 2056, 0 if mode == MODE_LOCAL else 2, seed=sum(cfg) + 2 + mode)
+            if mode != MODE_EPILOGUE:
+                _run(kern, mode, True, 29, 8, 7168, 0 if mode == MODE_LOCAL else 1, seed=sum(cfg) + 2 + 3 * mode)
+    finally:
+        kern.lib.deepep_set_launch_config(0, -1, -1)
+
+
+@pytest.mark.parametrize('weighted,hidden', [(False, 7168), (True, 520), (False, 64)])
+def test_kernel_reduce_scatter_rows(kern, weighted, hidden):
+    """deepep_combine_reduce_scatter (phase A of the xGMI transport) = the LOCAL reduce with each
+    unit's row and weights stored at an arbitrary 16-byte aligned address."""
+    rng = np.random.default_rng(hidden + weighted)
+    units, width, K = 41, 8, 8
+    nsrc = units * width
+    src = _random_rows(rng, nsrc, hidden)
+    table = rng.integers(0, nsrc, size=(units, width)).astype(np.int32)
+    table[rng.random((units, width)) < 0.3] = -1
+    table[0] = -1
+    row_w = rng.random(nsrc).astype(np.float32)
+    row_bytes = hidden * 2 + 48                    # weights at hidden * 2 + 16
+    perm = rng.permutation(units)
+    win = torch.zeros((units * row_bytes,), dtype=torch.uint8, device='cuda')
+    addr = torch.tensor([win.data_ptr() + int(p) * row_bytes for p in perm], dtype=torch.int64, device='cuda')
+    g_src, g_tab = _bf16(src), torch.from_numpy(table).cuda()
+    g_w = torch.from_numpy(row_w).cuda()
+    kern.combine_reduce_scatter(g_src, units, addr, table=g_tab, row_weights=g_w if weighted else None,
+                                wtable=g_tab, wsrc=g_w, num_weights=K, weights_offset=hidden * 2 + 16)
+    torch.cuda.synchronize()
+    out = torch.empty((units, hidden), dtype=torch.bfloat16)
+    out_w = torch.empty((units, K))
+    OracleKernels().combine_reduce(MODE_LOCAL, g_src.cpu(), out, units, table=g_tab.cpu(),
+                                   row_weights=g_w.cpu() if weighted else None, wtable=g_tab.cpu(), wsrc=g_w.cpu(),
+                                   out_weights=out_w)
+    rows = win.cpu().view(units, row_bytes)[torch.from_numpy(perm)]
+    got = rows[:, :hidden * 2].contiguous().view(torch.bfloat16)
+    got_w = rows[:, hidden * 2 + 16:hidden * 2 + 16 + 4 * K].contiguous().view(torch.float32)
+    assert np.array_equal(_u16(got), _u16(out))
+    assert torch.equal(got_w, out_w)
 
 
 def test_kernel_empty_and_errors(kern):
@@ -278,18 +325,24 @@ def test_elastic_buffer_golden_on_gpu(fixture, world, chunks, monkeypatch):
     assert not bad, bad
 
 
-@pytest.mark.parametrize('weighted', [False, True])
-def test_config2_full_size_bitwise(weighted):
-    """BASELINE config 2: EP=1, 8192 tokens, hidden 7168, top-8, E=256; full output vs the oracle."""
+@pytest.mark.parametrize('weighted,T,skew', [(False, 8192, 1.0), (True, 8192, 1.0), (False, 16384, 4.0)])
+def test_config2_full_size_bitwise(weighted, T, skew):
+    """BASELINE config 2: EP=1, 8192 tokens, hidden 7168, top-8, E=256; full output vs the oracle.
+    (16384, skew 4): config 5's per-rank batch and routing skew (get_unbalanced_scores) on one GPU."""
     import torch.distributed as dist
     from deepep_amd import ElasticBuffer
     if not dist.is_initialized():
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
         os.environ.setdefault('MASTER_PORT', '29542')
         dist.init_process_group('gloo', rank=0, world_size=1)
-    T, H, K, E = 8192, 7168, 8, 256
+    H, K, E = 7168, 8, 256
     g = torch.Generator(device='cuda').manual_seed(11)
-    scores = torch.rand((T, E), device='cuda', generator=g)
+    if skew != 1.0:
+        from deepep_amd.utils import get_unbalanced_scores
+        torch.manual_seed(11)
+        scores = get_unbalanced_scores(T, E, 8, K, skew, device='cuda')
+    else:
+        scores = torch.rand((T, E), device='cuda', generator=g)
     w, idx = torch.topk(scores, K, dim=-1, sorted=False)
     idx = idx.to(torch.int64)
     buf = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=T, hidden=H, num_topk=K)

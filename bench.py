@@ -4,8 +4,10 @@ BF16 top-k weighted reduce) at 1/2/4/8 MI355X").
 One step = one ElasticBuffer.combine over one synthetic batch already resident in HBM:
 8192 tokens/rank x hidden 7168 x top-8 over 256 experts (BASELINE configs 2 and 3),
 expanded layout, gating-weighted (apply_topk_weights=True), weights passed through.
-At N = 1 the combine is one fused HIP launch; at N > 1 it is phase A -> RCCL all-to-all
-over xGMI -> phase B.
+At N = 1 the combine is one fused HIP launch; at N > 1 it is phase A -> exchange over xGMI ->
+phase B, with two transports timed on the same batch (RCCL all-to-all, pipelined; direct stores
+into the peers' symmetric windows): `value` is the faster one whose output matched the other bit
+for bit, named in config.transport, with both numbers in the line.
 
 Algorithmic bytes per token: K*H*2 (rows read) + H*2 (row written)
 + K*4 (slot index) + K*4 (fp32 weight), with K = the token's valid top-k slots.
@@ -369,6 +371,17 @@ def main():
                         note='algorithmic bytes / (H2D of the expanded rows + combine + D2H of the output)')
         del host_y, host_out, dev_y
 
+    # EP > 1: both transports are complete implementations of the same combine, timed with the same
+    # protocol on the same batch; `value` is the faster one whose output matched the other bit for
+    # bit, and `config.transport` names it (both numbers stay in the line).
+    transport = buf.transport if world > 1 else None
+    rccl = None
+    if world > 1:
+        rccl = dict(value=round(value, 2), ms_per_step=round(ms_per_step, 4))
+        if (xgmi is not None and 'value' in xgmi and xgmi['bitwise_equal_to_rccl'] and not xgmi['barrier_timeout']
+                and xgmi['value'] > value):
+            value, ms_per_step, transport = xgmi['value'], xgmi['ms_per_step'], 'xgmi'
+
     cpu_baseline = cpu_torch = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         plan = handle._combine_plans[('multi', 1)]
@@ -386,9 +399,9 @@ def main():
                                    f'{"FP8 dispatch, " if args.fp8_dispatch else ""}expanded layout, '
                                    f'{"gating-weighted" if weighted else "plain (reference semantics)"}',
                        'tokens_per_rank': T, 'hidden': H, 'topk': K, 'experts': E,
-                       'parallelism': f'ep{world}'},
+                       'parallelism': f'ep{world}', 'transport': transport},
             'roofline': roofline, 'cpu_baseline': cpu_baseline, 'cpu_torch': cpu_torch, 'loopback': loopback,
-            'phases': phases, 'xgmi': xgmi,
+            'phases': phases, 'rccl': rccl, 'xgmi': xgmi,
             'dispatch': dispatch,
         }
         print(json.dumps(line), flush=True)

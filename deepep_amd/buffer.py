@@ -359,17 +359,28 @@ class ElasticBuffer:
             idx64 = topk_idx if topk_idx.dtype == torch.int64 else topk_idx.to(torch.int64)
             idx64 = idx64.contiguous()
             w = topk_weights.contiguous() if topk_weights is not None else None
-            # --- send side: destination slots (deterministic ranks), one packed row per (token, dest)
-            dst_slot = torch.empty((T, R), dtype=torch.int32, device=dev)
-            send_counts = torch.empty((R,), dtype=torch.int32, device=dev)
-            kern.dispatch_route(idx64, num_experts, R, dst_slot, send_counts, stream=stream)
-            if R == 1:
-                recv_counts_t = send_counts
+            # A cached handle already holds the routing (slots, counts, metadata, expert layout): the
+            # dispatch is then pack -> exchange -> copy, with no host sync (graph-capturable at EP = 1),
+            # as the reference's cached mode skips its notify phase (elastic.py:855-1033).
+            cached = handle if handle is not None and handle._send_counts is not None else None
+            if cached is not None:
+                _assert(do_expand == handle.do_expand, 'do_expand must match the cached handle')
+                dst_slot = cached.dst_buffer_slot_idx
+                send_counts_l, recv_counts_l = cached._send_counts, cached._recv_counts
+                send_offsets = cached._send_offsets
             else:
-                recv_counts_t = torch.empty_like(send_counts)
-                self._a2a(recv_counts_t, send_counts)
-            counts_l = [int(v) for v in torch.cat([send_counts, recv_counts_t]).tolist()]   # host sync, as do_cpu_sync
-            send_counts_l, recv_counts_l = counts_l[:R], counts_l[R:]
+                # --- send side: destination slots (deterministic ranks), one packed row per (token, dest)
+                dst_slot = torch.empty((T, R), dtype=torch.int32, device=dev)
+                send_counts = torch.empty((R,), dtype=torch.int32, device=dev)
+                kern.dispatch_route(idx64, num_experts, R, dst_slot, send_counts, stream=stream)
+                if R == 1:
+                    recv_counts_t = send_counts
+                else:
+                    recv_counts_t = torch.empty_like(send_counts)
+                    self._a2a(recv_counts_t, send_counts)
+                counts_l = [int(v) for v in torch.cat([send_counts, recv_counts_t]).tolist()]   # host sync
+                send_counts_l, recv_counts_l = counts_l[:R], counts_l[R:]
+                send_offsets = (torch.cumsum(send_counts, 0) - send_counts).to(torch.int32)
             N = sum(recv_counts_l)
             x_bytes = x.contiguous().view(torch.uint8).view(T, H * x.element_size())
             sf_bytes = sf.contiguous().view(torch.uint8).view(T, -1) if sf is not None else None
@@ -378,7 +389,6 @@ class ElasticBuffer:
             direct = R == 1
             layout = (RowLayout.make(0, 0, K) if direct else
                       RowLayout.make(x_bytes.shape[1], sf_bytes.shape[1] if sf is not None else 0, K))
-            send_offsets = (torch.cumsum(send_counts, 0) - send_counts).to(torch.int32)
             packed = torch.empty((sum(send_counts_l), layout.row_bytes), dtype=torch.uint8, device=dev)
             kern.dispatch_pack(x_bytes[:, :0] if direct else x_bytes, None if direct else sf_bytes, idx64, w,
                                r * num_max_tokens_per_rank, dst_slot, send_offsets, packed, layout, stream=stream)
@@ -388,30 +398,44 @@ class ElasticBuffer:
                 recv_packed = torch.empty((N, layout.row_bytes), dtype=torch.uint8, device=dev)
                 self._a2a(recv_packed, packed, recv_counts_l, send_counts_l)
             # --- receive side (dispatch_copy_epilogue_impl): metadata, expert layout, copies
-            psum_rank = torch.cumsum(recv_counts_t, 0).to(torch.int32)
-            meta = torch.empty((N, K + 2), dtype=torch.int32, device=dev)
-            out_idx = None if do_expand else torch.empty((N, K), dtype=torch.int64, device=dev)
-            nblocks = (N + 255) // 256
-            block_counts = torch.empty((nblocks, epr), dtype=torch.int32, device=dev)
-            kern.dispatch_count(recv_packed, layout, N, r, epr, psum_rank, meta, out_idx, block_counts, stream=stream)
-            expert_counts = torch.empty((epr,), dtype=torch.int32, device=dev)
-            psum_expert = torch.empty((epr,), dtype=torch.int32, device=dev)
-            kern.dispatch_scan(block_counts, epr, expert_alignment, do_expand, expert_counts, psum_expert,
-                               stream=stream)
-            counts_l = [int(v) for v in expert_counts.tolist()]
-            aligned_l = [align(c, expert_alignment) for c in counts_l]
-            if cumulative_local_expert_recv_stats is not None:
-                cumulative_local_expert_recv_stats += expert_counts.to(cumulative_local_expert_recv_stats.dtype)
+            if cached is not None:
+                psum_rank = cached.psum_num_recv_tokens_per_scaleup_rank
+                psum_expert = cached.psum_num_recv_tokens_per_expert
+                meta = cached.recv_src_metadata[:N]
+                out_idx = None if do_expand else cached._recv_topk_idx.clone()
+                aligned_l = cached.num_recv_tokens_per_expert_list
+                expert_counts = cached.num_unaligned_recv_tokens_per_expert
+                if cumulative_local_expert_recv_stats is not None:
+                    cumulative_local_expert_recv_stats += expert_counts.to(cumulative_local_expert_recv_stats.dtype)
+                self._before_epilogue(previous_event_before_epilogue)
+            else:
+                psum_rank = torch.cumsum(recv_counts_t, 0).to(torch.int32)
+                meta = torch.empty((N, K + 2), dtype=torch.int32, device=dev)
+                out_idx = None if do_expand else torch.empty((N, K), dtype=torch.int64, device=dev)
+                nblocks = (N + 255) // 256
+                block_counts = torch.empty((nblocks, epr), dtype=torch.int32, device=dev)
+                kern.dispatch_count(recv_packed, layout, N, r, epr, psum_rank, meta, out_idx, block_counts,
+                                    stream=stream)
+                expert_counts = torch.empty((epr,), dtype=torch.int32, device=dev)
+                psum_expert = torch.empty((epr,), dtype=torch.int32, device=dev)
+                kern.dispatch_scan(block_counts, epr, expert_alignment, do_expand, expert_counts, psum_expert,
+                                   stream=stream)
+                counts_l = [int(v) for v in expert_counts.tolist()]
+                aligned_l = [align(c, expert_alignment) for c in counts_l]
+                if cumulative_local_expert_recv_stats is not None:
+                    cumulative_local_expert_recv_stats += expert_counts.to(cumulative_local_expert_recv_stats.dtype)
+                self._before_epilogue(previous_event_before_epilogue)
+                if do_expand:
+                    kern.dispatch_slots(recv_packed, layout, N, r, epr, block_counts, meta, stream=stream)
+                else:
+                    meta[:, 2:] = -1
             num_unaligned = expert_counts
-            self._before_epilogue(previous_event_before_epilogue)
             if do_expand:
                 num_expanded = sum(aligned_l)
-                kern.dispatch_slots(recv_packed, layout, N, r, epr, block_counts, meta, stream=stream)
                 alloc = torch.zeros if do_zero_padding else torch.empty
                 n_rows = num_expanded
             else:
                 num_expanded = N
-                meta[:, 2:] = -1
                 alloc = torch.empty
                 n_rows = N
             out_x = alloc((n_rows, H), dtype=x.dtype, device=dev)
@@ -425,6 +449,7 @@ class ElasticBuffer:
                                out_w, x_direct=x_bytes if direct else None,
                                sf_direct=sf_bytes if direct else None, num_max_tokens=num_max_tokens_per_rank,
                                stream=stream)
+            recv_idx64 = out_idx
             if out_idx is not None and topk_idx.dtype != torch.int64:
                 out_idx = out_idx.to(topk_idx.dtype)
             num_recv = N
@@ -451,6 +476,9 @@ class ElasticBuffer:
                               cloned_idx, num_recv, num_expanded, aligned_l, psum_rank, psum_expert,
                               num_unaligned, meta, dst_slot, None, None)
             handle._recv_counts = recv_counts_l
+            handle._send_counts = send_counts_l
+            handle._send_offsets = send_offsets
+            handle._recv_topk_idx = recv_idx64
         out_x = (out_x, out_sf) if out_sf is not None else out_x
         return out_x, out_idx, out_w, handle, EventOverlap(event)
 

@@ -229,6 +229,9 @@ class EPHandle:
         self.cached_recv_src_metadata_before_sort = None
         # Host-side copies captured at dispatch (counts per source rank), and the combine plan cache
         self._recv_counts: Optional[List[int]] = None
+        self._send_counts: Optional[List[int]] = None         # cached dispatch: no host sync needed
+        self._send_offsets: Optional[torch.Tensor] = None
+        self._recv_topk_idx: Optional[torch.Tensor] = None    # non-expanded recv_topk_idx (int64, N rows)
         self._combine_plans = {}
 
     def deterministic_sort(self, *args, **kwargs) -> None:

@@ -410,6 +410,37 @@ def test_hip_graph_capture_replays_combine():
     assert torch.equal(out, ref) and torch.equal(out_w, ref_w)
 
 
+def test_hip_graph_cached_dispatch_and_combine():
+    """With a cached handle the dispatch has no host sync, so a whole EP = 1 layer's token traffic
+    -- cached expanded dispatch + combine -- captures into one HIP graph and replays bitwise."""
+    T, H, K, E = 640, 2048, 8, 64
+    buf, idx, w, g = _ep1_setup(T, H, K, E, seed=5)
+    x = torch.randn((T, H), device='cuda', generator=g).to(torch.bfloat16)
+    _, _, ex_w, handle, _ = buf.dispatch(x, topk_idx=idx, topk_weights=w, num_experts=E, do_expand=True)
+
+    def layer():
+        ex_x, _, ex_w2, _, _ = buf.dispatch(x, topk_weights=w, do_expand=True, handle=handle)
+        return buf.combine(ex_x, handle, topk_weights=ex_w2, apply_topk_weights=True)[:2]
+
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(3):
+            layer()
+    torch.cuda.current_stream().wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        out, out_w = layer()
+    x.copy_(torch.randn(x.shape, device='cuda', generator=g).to(torch.bfloat16))
+    graph.replay()
+    ref, ref_w = layer()
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref) and torch.equal(out_w, ref_w)
+    # the weighted sum of a token's own expanded copies: x scaled by the sum of its valid weights
+    exact = x.double() * (w.double() * (idx >= 0)).sum(dim=1, keepdim=True)
+    assert oracle.calc_diff(oracle.bf16_to_f32(_u16(out)), exact.cpu().numpy()) < 1e-5
+
+
 def test_fp8_dispatch_then_bf16_combine():
     """BASELINE config 4 at EP=1: FP8 (e4m3, per-128 scales) dispatch, BF16 combine."""
     from deepep_amd.utils import per_token_cast_back, per_token_cast_to_fp8

@@ -99,6 +99,17 @@ def _worker(rank, world, port, seed, T, H, K, queue):
                                               apply_topk_weights=True)
         if not torch.equal(outs['xgmi'], outs['rccl']):
             failures.append('weighted: xgmi != rccl')
+        # non-expanded layout (the caller pre-reduces its local experts): both transports agree
+        _, _, recv_w, nh, _ = buf.dispatch(x, topk_idx=torch.from_numpy(idx_all[rank]).to(dev),
+                                            topk_weights=torch.from_numpy(w_all[rank]).to(dev), num_experts=E)
+        g = torch.Generator(device=dev).manual_seed(rank)
+        x_red = torch.randn((nh.num_recv_tokens, H), device=dev, generator=g).to(torch.bfloat16)
+        bias = _bf16(b_all[rank], dev)
+        o = {t: b.combine(x_red, nh, topk_weights=recv_w, bias=bias) for t, b in bufs.items()}
+        if not (torch.equal(o['xgmi'][0], o['rccl'][0]) and torch.equal(o['xgmi'][1], o['rccl'][1])):
+            failures.append('non-expanded: xgmi != rccl')
+        if not torch.equal(o['xgmi'][1].cpu(), torch.from_numpy(w_all[rank])):
+            failures.append('non-expanded: weight pass-through')
         if bufs['xgmi']._sym is None:
             failures.append('xgmi transport did not create its window')
         else:

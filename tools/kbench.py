@@ -51,6 +51,8 @@ def main():
     copy_dst = torch.empty_like(y)
     us = timeit(lambda: copy_dst.copy_(y), s)
     print(json.dumps(dict(variant='d2d_copy_939MB', us=round(us, 1), gbps=round(2 * y.numel() * 2 / us / 1e3, 1))))
+    us = timeit(lambda: copy_dst.fill_(1.0), s)
+    print(json.dumps(dict(variant='fill_939MB (write only)', us=round(us, 1), gbps=round(y.numel() * 2 / us / 1e3, 1))))
     del copy_dst
     lib = buf.kernels.lib
     configs = [  # (vec_per_lane, stage_lds, store_policy); 0/-1 = auto

@@ -1,0 +1,82 @@
+// Dispatch-copy probes (diagnostic, not the product): the expanded copy x[T][H] -> out[N][H]
+// source-major (one wave per (token, 2 KiB chunk), up to K scattered stores) vs destination-major
+// (one wave per (kRows consecutive expanded rows, 2 KiB chunk), gathered loads, in-order stores).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__global__ void __launch_bounds__(256) scatter_copy(const uint8_t* x, const int32_t* dst, int T, int K, int xb,
+                                                    uint8_t* out) {
+    const int lane = threadIdx.x & 63;
+    const int nvec = xb / 16, nch = (nvec + 127) / 128;
+    const int64_t it = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (it >= (int64_t)T * nch) return;
+    const int64_t t = it / nch;
+    const int c = (int)(it - t * nch);
+    int32_t my = lane < K ? dst[t * K + lane] : -1;
+    const uint64_t m0 = __ballot(my >= 0);
+    const int v0 = c * 128 + lane, v1 = v0 + 64;
+    const u32x4 z = {0u, 0u, 0u, 0u};
+    const u32x4 a0 = v0 < nvec ? __builtin_nontemporal_load((const u32x4*)(x + t * xb) + v0) : z;
+    const u32x4 a1 = v1 < nvec ? __builtin_nontemporal_load((const u32x4*)(x + t * xb) + v1) : z;
+    for (uint64_t m = m0; m; m &= m - 1) {
+        const int64_t d = __builtin_amdgcn_readlane(my, __builtin_ctzll(m));
+        auto rs = __builtin_amdgcn_make_buffer_rsrc(out + d * xb, 0, xb, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(a0, rs, v0 * 16, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(a1, rs, v1 * 16, 0, 16);
+    }
+}
+
+template <int kRows, int kAux>
+__global__ void __launch_bounds__(256) gather_copy(const uint8_t* x, const int32_t* inv, int N, int xb,
+                                                   uint8_t* out) {
+    const int lane = threadIdx.x & 63;
+    const int nvec = xb / 16, nch = (nvec + 127) / 128;
+    const int64_t it = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t ngroups = ((int64_t)N + kRows - 1) / kRows;
+    if (it >= ngroups * nch) return;
+    // chunk-major inside a group so the 4 waves of a workgroup write 4 consecutive chunks
+    const int64_t grp = it / nch;
+    const int c = (int)(it - grp * nch);
+    const int v0 = c * 128 + lane, v1 = v0 + 64;
+    const u32x4 z = {0u, 0u, 0u, 0u};
+    u32x4 a[kRows][2];
+    int64_t rows[kRows];
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) {
+        const int64_t j = grp * kRows + r;
+        const int32_t t = j < N ? inv[j] : -1;
+        rows[r] = t;
+        const u32x4* src = (const u32x4*)(x + (int64_t)(t < 0 ? 0 : t) * xb);
+        a[r][0] = (t >= 0 && v0 < nvec) ? src[v0] : z;
+        a[r][1] = (t >= 0 && v1 < nvec) ? src[v1] : z;
+    }
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) {
+        const int64_t j = grp * kRows + r;
+        if (j >= N || rows[r] < 0) continue;
+        auto rs = __builtin_amdgcn_make_buffer_rsrc(out + j * xb, 0, xb, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(a[r][0], rs, v0 * 16, 0, kAux);
+        __builtin_amdgcn_raw_buffer_store_b128(a[r][1], rs, v1 * 16, 0, kAux);
+    }
+}
+
+extern "C" int probe_copy(int variant, const void* x, const int32_t* dst, const int32_t* inv, int T, int K, int N,
+                          int xb, void* out, hipStream_t s) {
+    const int nch = (xb / 16 + 127) / 128;
+    auto grid = [&](int64_t items) { return dim3((unsigned)((items + 3) / 4)); };
+    const uint8_t* xx = (const uint8_t*)x;
+    uint8_t* o = (uint8_t*)out;
+    switch (variant) {
+        case 0: hipLaunchKernelGGL(scatter_copy, grid((int64_t)T * nch), dim3(256), 0, s, xx, dst, T, K, xb, o); break;
+        case 1: hipLaunchKernelGGL((gather_copy<1, 16>), grid((int64_t)N * nch), dim3(256), 0, s, xx, inv, N, xb, o); break;
+        case 2: hipLaunchKernelGGL((gather_copy<2, 16>), grid((int64_t)(N + 1) / 2 * nch), dim3(256), 0, s, xx, inv, N, xb, o); break;
+        case 4: hipLaunchKernelGGL((gather_copy<4, 16>), grid((int64_t)(N + 3) / 4 * nch), dim3(256), 0, s, xx, inv, N, xb, o); break;
+        case 8: hipLaunchKernelGGL((gather_copy<8, 16>), grid((int64_t)(N + 7) / 8 * nch), dim3(256), 0, s, xx, inv, N, xb, o); break;
+        case 40: hipLaunchKernelGGL((gather_copy<4, 0>), grid((int64_t)(N + 3) / 4 * nch), dim3(256), 0, s, xx, inv, N, xb, o); break;
+        case 42: hipLaunchKernelGGL((gather_copy<4, 2>), grid((int64_t)(N + 3) / 4 * nch), dim3(256), 0, s, xx, inv, N, xb, o); break;
+        default: return -1;
+    }
+    return (int)hipGetLastError();
+}

@@ -301,3 +301,74 @@ def test_dispatch_modes_world2(alignment, do_cpu_sync, do_handle_copy):
             if p.is_alive():
                 p.kill()
     assert len(results) == 2 and not any(results.values()), results
+
+
+def _empty_rank_worker(rank, world, port, queue):
+    import sys
+    sys.path.insert(0, ROOT)
+    try:
+        os.environ['MASTER_ADDR'] = '127.0.0.1'
+        os.environ['MASTER_PORT'] = str(port)
+        dist.init_process_group('gloo', rank=rank, world_size=world)
+        import oracle
+        from deepep_amd import ElasticBuffer
+        from tests.oracle_kernels import OracleKernels
+        T_max, H, K, E = 32, 72, 4, 4 * world
+        Ts = [0, T_max, 5][:world]                    # rank 0 sends nothing; the others do
+        rng = np.random.default_rng(3)
+        idx_all, w_all, y_all = [], [], []
+        for r in range(world):
+            idx = np.array([rng.permutation(E)[:K] for _ in range(Ts[r])], dtype=np.int64).reshape(Ts[r], K)
+            w = rng.random((Ts[r], K)).astype(np.float32)
+            y = oracle.f32_to_bf16(rng.standard_normal((Ts[r], K, H)).astype(np.float32))
+            idx_all.append(idx), w_all.append(w), y_all.append(y)
+        disp = oracle.simulate_dispatch(idx_all, E, T_max)
+        x_exp_all, w_exp_all = [], []
+        for r, d in enumerate(disp):
+            xe = np.zeros((d['num_expanded'], H), np.uint16)
+            we = np.zeros((d['num_expanded'],), np.float32)
+            for row, (g, k) in enumerate(d['expanded_src']):
+                s, t = divmod(int(g), T_max)
+                xe[row], we[row] = y_all[s][t, k], w_all[s][t, k]
+            x_exp_all.append(xe), w_exp_all.append(we)
+        expect = oracle.combine_ep(x_exp_all, [d['src_metadata'] for d in disp], idx_all, E, T_max, expanded=True,
+                                   topk_weights_per_rank=w_exp_all, bias_per_rank=[(None, None)] * world)
+        buf = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=T_max, hidden=H, num_topk=K)
+        buf._kernels = OracleKernels()
+        x = torch.zeros((Ts[rank], H), dtype=torch.bfloat16)
+        _, _, ex_w, handle, _ = buf.dispatch(x, topk_idx=torch.from_numpy(idx_all[rank]),
+                                             topk_weights=torch.from_numpy(w_all[rank]), num_experts=E,
+                                             do_expand=True)
+        failures = []
+        out, out_w, _ = buf.combine(_u16_to_bf16(x_exp_all[rank]), handle, topk_weights=ex_w)
+        if tuple(out.shape) != (Ts[rank], H) or not np.array_equal(_bf16_to_u16(out), expect[rank][0]):
+            failures.append('combined_x')
+        if not np.array_equal(out_w.numpy(), expect[rank][1]):
+            failures.append('combined_topk_weights')
+        queue.put((rank, failures))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:
+        queue.put((rank, [traceback.format_exc()]))
+
+
+@pytest.mark.parametrize('world', [2, 3])
+def test_rank_with_no_tokens(world):
+    """A rank that sends no tokens (num_tokens = 0) still takes part in dispatch and combine."""
+    ctx = mp.get_context('spawn')
+    queue = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_empty_rank_worker, args=(r, world, port, queue)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = {}
+    try:
+        for _ in range(world):
+            rank, failures = queue.get(timeout=240)
+            results[rank] = failures
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    assert len(results) == world and not any(results.values()), results

@@ -34,7 +34,7 @@ def _bf16(a: np.ndarray, dev) -> torch.Tensor:
     return torch.from_numpy(np.ascontiguousarray(a).view(np.int16)).view(torch.bfloat16).to(dev)
 
 
-def _worker(rank, world, port, seed, T, H, K, queue):
+def _worker(rank, world, port, seed, T, H, K, queue, empty_rank=-1):
     sys.path.insert(0, ROOT)
     try:
         os.environ['MASTER_ADDR'] = '127.0.0.1'
@@ -48,15 +48,18 @@ def _worker(rank, world, port, seed, T, H, K, queue):
         E = 8 * world
         rng = np.random.default_rng(seed)
         idx_all, w_all, y_all, b_all = [], [], [], []
+        Ts = [0 if r == empty_rank else T for r in range(world)]     # empty_rank sends no tokens
         for r in range(world):
-            idx = np.stack([rng.permutation(E)[:K] for _ in range(T)]).astype(np.int64)
-            idx[rng.random((T, K)) < 0.15] = -1
-            idx[0] = -1                                   # a token routed nowhere
-            w = rng.random((T, K)).astype(np.float32) * (idx >= 0)
-            y = oracle.f32_to_bf16(rng.standard_normal((T, K, H)).astype(np.float32))
+            Tr = Ts[r]
+            idx = np.array([rng.permutation(E)[:K] for _ in range(Tr)], dtype=np.int64).reshape(Tr, K)
+            idx[rng.random((Tr, K)) < 0.15] = -1
+            if Tr:
+                idx[0] = -1                               # a token routed nowhere
+            w = rng.random((Tr, K)).astype(np.float32) * (idx >= 0)
+            y = oracle.f32_to_bf16(rng.standard_normal((Tr, K, H)).astype(np.float32))
             y[idx < 0] = 0
             idx_all.append(idx), w_all.append(w), y_all.append(y)
-            b_all.append(oracle.f32_to_bf16(rng.standard_normal((T, H)).astype(np.float32)))
+            b_all.append(oracle.f32_to_bf16(rng.standard_normal((Tr, H)).astype(np.float32)))
         disp = oracle.simulate_dispatch(idx_all, E, T)
         x_exp_all, w_exp_all = [], []
         for r, d in enumerate(disp):
@@ -72,7 +75,7 @@ def _worker(rank, world, port, seed, T, H, K, queue):
             os.environ['DEEPEP_TRANSPORT'] = transport
             bufs[transport] = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=T, hidden=H, num_topk=K,
                                             explicitly_destroy=True, num_gpu_timeout_secs=20)
-        x = torch.zeros((T, H), dtype=torch.bfloat16, device=dev)
+        x = torch.zeros((Ts[rank], H), dtype=torch.bfloat16, device=dev)
         buf = bufs['xgmi']
         _, _, ex_w, handle, _ = buf.dispatch(x, topk_idx=torch.from_numpy(idx_all[rank]).to(dev),
                                              topk_weights=torch.from_numpy(w_all[rank]).to(dev),
@@ -123,12 +126,13 @@ def _worker(rank, world, port, seed, T, H, K, queue):
         queue.put((rank, [traceback.format_exc()]))
 
 
-@pytest.mark.parametrize('world,T,H,K', [(2, 96, 1024, 8), (4, 64, 7168, 8), (4, 80, 256, 2)])
-def test_xgmi_transport_matches_oracle(world, T, H, K):
+@pytest.mark.parametrize('world,T,H,K,empty_rank', [(2, 96, 1024, 8, -1), (4, 64, 7168, 8, -1), (4, 80, 256, 2, -1),
+                                                   (3, 40, 512, 4, 1)])
+def test_xgmi_transport_matches_oracle(world, T, H, K, empty_rank):
     ctx = mp.get_context('spawn')
     queue = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, 100 + world + K, T, H, K, queue))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, 100 + world + K, T, H, K, queue, empty_rank))
              for r in range(world)]
     for p in procs:
         p.start()

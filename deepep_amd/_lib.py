@@ -55,6 +55,8 @@ SIGNATURES = {
     'deepep_sym_import': (_I, [_P, ctypes.POINTER(ctypes.c_void_p)]),
     'deepep_sym_close': (_I, [_P]),
     'deepep_sym_barrier': (_I, [_P, _I, _I, _I64, _I64, _P, _P]),
+    'deepep_sym_signal': (_I, [_P, _I, _I, _I, _I64, _P]),
+    'deepep_sym_wait': (_I, [_P, _I, _I, _I, _I64, _I64, _P, _P]),
     'deepep_combine_reduce_scatter': (_I, [_I, _P, _I64, _I64, _P, _I64, _I, _P, _P, _I, _I, _P, _I64, _P, _I,
                                            _I64, _P, _P]),
 }

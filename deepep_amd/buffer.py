@@ -25,8 +25,8 @@ import torch
 import torch.distributed as dist
 
 from .event import EventHandle, EventOverlap
-from .handle import (CombinePlan, EPHandle, chunk_plans, epilogue_tables, single_reduction_tables, weight_table,
-                     window_tables)
+from .handle import (ChunkPlan, CombinePlan, EPHandle, chunk_plans, epilogue_tables, single_reduction_tables,
+                     weight_table, window_tables)
 from .kernels import MODE_EPILOGUE, MODE_FUSED, MODE_LOCAL, RowLayout
 from .utils import align, ceil_div, value_or
 
@@ -637,7 +637,10 @@ class ElasticBuffer:
         """EP > 1 combine over the symmetric windows (the reference's NVLink design on xGMI):
         barrier (peers done reading their windows) -> phase A storing every partial and its top-k
         weights straight into the owner's window row slot * T_max + t (combine.cuh:96-106, 215-226)
-        -> barrier (all partials landed, comm.cuh:88-129) -> phase B over the local window."""
+        -> all partials landed (comm.cuh:88-129) -> phase B over the local window.  Split into
+        source-token chunks like the RCCL path: phase A of chunk c is followed by a signal on split
+        barrier c, and phase B of chunk c runs on a second stream behind the wait for every rank's
+        signal c, so it overlaps phase A of the later chunks."""
         R, r = self.num_ranks, self.rank_idx
         T_max = handle.num_max_tokens_per_rank
         T = handle.topk_idx.shape[0]
@@ -645,7 +648,8 @@ class ElasticBuffer:
         self._window_slots = min(R, K)
         row_bytes = align(hidden * 2, 16) + align(K * 4, 16)
         sym = self._window(row_bytes)
-        key = ('xgmi', R, row_bytes)
+        num_chunks = min(self._num_chunks(handle), 63)
+        key = ('xgmi', R, row_bytes, num_chunks)
         plan = handle._combine_plans.get(key)
         if plan is None:
             plan = CombinePlan(num_ranks=R, num_tokens=T, num_topk=K, expanded=expanded)
@@ -658,39 +662,72 @@ class ElasticBuffer:
             plan.recv_counts = recv_counts
             m = meta[:n_recv].to(torch.int64)
             src_rank = torch.div(m[:, 1], K, rounding_mode='floor')
+            src_tok = m[:, 0] % T_max
             slot = torch.full_like(src_rank, r) if rank_layout else m[:, 1] % K
-            row = slot * T_max + m[:, 0] % T_max
-            plan.out_rows = (sym.data_bases_dev[src_rank] + row * row_bytes).contiguous()
-            plan.table_b, plan.row_of_lane = window_tables(handle.topk_idx, handle.num_experts, R, T_max, rank_layout)
-            plan.wtables = {}
+            out_rows = sym.data_bases_dev[src_rank] + (slot * T_max + src_tok) * row_bytes
+            table_b, row_of_lane = window_tables(handle.topk_idx, handle.num_experts, R, T_max, rank_layout)
+            B = (T_max + num_chunks - 1) // num_chunks
+            chunk_of_row = torch.div(src_tok, B, rounding_mode='floor')
+            plan.chunks = []
+            for c in range(num_chunks):
+                rows = (chunk_of_row == c).nonzero().view(-1)
+                if expanded:
+                    table_a = m[rows, 2:].to(torch.int32).contiguous()
+                    wtable_a = table_a
+                elif num_chunks == 1:
+                    table_a = wtable_a = None                 # received row i is unit i
+                else:
+                    table_a = rows.to(torch.int32).view(-1, 1).contiguous()
+                    wtable_a = (rows.view(-1, 1) * K + torch.arange(K, device=rows.device).view(1, K)).to(
+                        torch.int32).contiguous()
+                lo, hi = c * B, min((c + 1) * B, T)
+                plan.chunks.append(ChunkPlan(lo, max(lo, hi), table_a, wtable_a, [], [],
+                                             table_b[lo:hi], row_of_lane[lo:hi]))
+                plan.chunks[-1].out_rows = out_rows[rows].contiguous()
             plan.window_row_bytes = row_bytes
             handle._combine_plans[key] = plan
-        n_recv = sum(plan.recv_counts)
-        meta = handle.recv_src_metadata
-        table_a = meta[:n_recv, 2:] if expanded else None
         kern = self.kernels
-        sym.barrier(stream)
-        self._mark(stream)
-        kern.combine_reduce_scatter(x, n_recv, plan.out_rows, table=table_a, row_weights=row_w,
-                                    wtable=table_a, wsrc=wsrc, num_weights=K if topk_weights is not None else 0,
-                                    weights_offset=align(hidden * 2, 16), stream=stream)
-        self._mark(stream)
-        sym.barrier(stream)
-        self._before_epilogue(previous_event_before_epilogue)
+        w_off = align(hidden * 2, 16)
         n_rows = self._window_slots * T_max
         rows = sym.data[:n_rows * row_bytes].view(torch.bfloat16).view(n_rows, row_bytes // 2)
-        wtable_b, recv_wsrc = None, None
-        if topk_weights is not None:
-            wkey = (row_bytes // 4, align(hidden * 2, 16) // 4)
-            if wkey not in plan.wtables:
-                plan.wtables[wkey] = weight_table(plan.row_of_lane, *wkey)
-            wtable_b = plan.wtables[wkey]
-            recv_wsrc = sym.data[:n_rows * row_bytes].view(torch.float32)
-        self._mark(stream)
-        kern.combine_reduce(MODE_EPILOGUE, rows[:, :hidden], combined_x, T, table=plan.table_b,
-                            bias0=bias_0, bias1=bias_1, wtable=wtable_b, wsrc=recv_wsrc,
-                            out_weights=combined_w, stream=stream)
-        self._mark(stream)
+        recv_wsrc = sym.data[:n_rows * row_bytes].view(torch.float32) if topk_weights is not None else None
+        pipelined = len(plan.chunks) > 1
+        sym.barrier(stream)                               # peers finished reading their windows
+        if pipelined:
+            if getattr(self, '_stream_b', None) is None:
+                self._stream_b = torch.cuda.Stream(device=self.device)
+            stream_b = self._stream_b
+            stream_b.wait_stream(stream)
+        for c, ch in enumerate(plan.chunks):
+            self._mark(stream)
+            kern.combine_reduce_scatter(x, ch.out_rows.shape[0], ch.out_rows, table=ch.table_a, row_weights=row_w,
+                                        wtable=ch.wtable_a, wsrc=wsrc,
+                                        num_weights=K if topk_weights is not None else 0,
+                                        weights_offset=w_off, stream=stream)
+            self._mark(stream)
+            sym.signal(1 + c, stream)
+        self._before_epilogue(previous_event_before_epilogue)
+        sb = stream_b if pipelined else stream
+        if pipelined and previous_event_before_epilogue is not None:
+            previous_event_before_epilogue.stream_wait(stream_b)
+        for c, ch in enumerate(plan.chunks):
+            sym.wait(1 + c, sb)
+            wtable_b = None
+            if topk_weights is not None:
+                wkey = (row_bytes // 4, w_off // 4)
+                if wkey not in ch.wtables:
+                    ch.wtables[wkey] = weight_table(ch.row_of_lane, *wkey)
+                wtable_b = ch.wtables[wkey]
+            lo, hi = ch.lo, ch.hi
+            self._mark(sb)
+            kern.combine_reduce(MODE_EPILOGUE, rows[:, :hidden], combined_x[lo:hi], hi - lo, table=ch.table_b,
+                                bias0=bias_0[lo:hi] if bias_0 is not None else None,
+                                bias1=bias_1[lo:hi] if bias_1 is not None else None,
+                                wtable=wtable_b, wsrc=recv_wsrc,
+                                out_weights=combined_w[lo:hi] if combined_w is not None else None, stream=sb)
+            self._mark(sb)
+        if pipelined:
+            stream.wait_stream(stream_b)
 
     def combine(self,
                 x: torch.Tensor,

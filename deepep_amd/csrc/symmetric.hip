@@ -52,6 +52,51 @@ sym_barrier_kernel(const uint64_t* peer_flags, int rank, int num_ranks, int64_t 
     __threadfence_system();
 }
 
+// Split barrier for pipelining: `signal` publishes `value` into slot `slot` of every rank's flag
+// table (after this stream's earlier work), `wait` waits for every rank's signal in this rank's
+// table.  Flag table of a window: int64 [kMaxSlots][64], slot 0 is the full barrier above.
+__global__ void __launch_bounds__(64)
+sym_signal_kernel(const uint64_t* peer_flags, int rank, int num_ranks, int slot, int64_t value) {
+    const int s = static_cast<int>(threadIdx.x);
+    if (s >= num_ranks) return;
+    __threadfence_system();
+    int64_t* theirs = reinterpret_cast<int64_t*>(peer_flags[s]) + static_cast<int64_t>(slot) * 64;
+    __hip_atomic_store(theirs + rank, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void __launch_bounds__(64)
+sym_wait_kernel(const uint64_t* peer_flags, int rank, int num_ranks, int slot, int64_t value, int64_t timeout_ticks,
+                int32_t* error_flag) {
+    const int s = static_cast<int>(threadIdx.x);
+    if (s >= num_ranks) return;
+    const int64_t* mine = reinterpret_cast<const int64_t*>(peer_flags[rank]) + static_cast<int64_t>(slot) * 64;
+    const uint64_t t0 = wall_clock64();
+    while (__hip_atomic_load(mine + s, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < value) {
+        if (static_cast<int64_t>(wall_clock64() - t0) > timeout_ticks) {
+            if (error_flag != nullptr) atomicOr(error_flag, 2);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+    __threadfence_system();
+}
+
+int64_t timeout_ticks(int64_t timeout_us, int* rc) {
+    static thread_local int64_t ticks_per_us = 0;
+    *rc = DEEPEP_OK;
+    if (ticks_per_us == 0) {
+        int dev = 0, khz = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e == hipSuccess) e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
+        if (e != hipSuccess) {
+            *rc = hip_fail(e, "wall clock rate");
+            return 0;
+        }
+        ticks_per_us = khz > 1000 ? khz / 1000 : 1;
+    }
+    return (timeout_us > 0 ? timeout_us : 100000000LL) * ticks_per_us;
+}
+
 }  // namespace
 
 extern "C" {
@@ -109,19 +154,38 @@ int deepep_sym_barrier(const uint64_t* peer_flags, int rank, int num_ranks, int6
                        int32_t* error_flag, deepep_stream_t stream) {
     if (peer_flags == nullptr || num_ranks < 1 || num_ranks > 64 || rank < 0 || rank >= num_ranks || epoch < 1)
         return deepep_amd_set_error(DEEPEP_ERR_INVALID_ARG, "sym_barrier: bad arguments");
-    static thread_local int64_t ticks_per_us = 0;
-    if (ticks_per_us == 0) {
-        int dev = 0, khz = 0;
-        hipError_t e = hipGetDevice(&dev);
-        if (e == hipSuccess) e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
-        if (e != hipSuccess) return hip_fail(e, "wall clock rate");
-        ticks_per_us = khz > 1000 ? khz / 1000 : 1;
-    }
-    const int64_t ticks = (timeout_us > 0 ? timeout_us : 100000000LL) * ticks_per_us;
+    int rc = DEEPEP_OK;
+    const int64_t ticks = timeout_ticks(timeout_us, &rc);
+    if (rc != DEEPEP_OK) return rc;
     hipLaunchKernelGGL(sym_barrier_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream),
                        peer_flags, rank, num_ranks, epoch, ticks, error_flag);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? DEEPEP_OK : hip_fail(e, "barrier launch");
+}
+
+int deepep_sym_signal(const uint64_t* peer_flags, int rank, int num_ranks, int slot, int64_t value,
+                      deepep_stream_t stream) {
+    if (peer_flags == nullptr || num_ranks < 1 || num_ranks > 64 || rank < 0 || rank >= num_ranks || slot < 1 ||
+        slot >= DEEPEP_SYM_FLAG_SLOTS || value < 1)
+        return deepep_amd_set_error(DEEPEP_ERR_INVALID_ARG, "sym_signal: bad arguments");
+    hipLaunchKernelGGL(sym_signal_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream),
+                       peer_flags, rank, num_ranks, slot, value);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? DEEPEP_OK : hip_fail(e, "signal launch");
+}
+
+int deepep_sym_wait(const uint64_t* peer_flags, int rank, int num_ranks, int slot, int64_t value, int64_t timeout_us,
+                    int32_t* error_flag, deepep_stream_t stream) {
+    if (peer_flags == nullptr || num_ranks < 1 || num_ranks > 64 || rank < 0 || rank >= num_ranks || slot < 1 ||
+        slot >= DEEPEP_SYM_FLAG_SLOTS || value < 1)
+        return deepep_amd_set_error(DEEPEP_ERR_INVALID_ARG, "sym_wait: bad arguments");
+    int rc = DEEPEP_OK;
+    const int64_t ticks = timeout_ticks(timeout_us, &rc);
+    if (rc != DEEPEP_OK) return rc;
+    hipLaunchKernelGGL(sym_wait_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream),
+                       peer_flags, rank, num_ranks, slot, value, ticks, error_flag);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? DEEPEP_OK : hip_fail(e, "wait launch");
 }
 
 }  // extern "C"

@@ -33,6 +33,7 @@ class ChunkPlan:
     table_b: torch.Tensor                    # source side: [hi - lo, min(R, K)] rows of the chunk's receive buffer
     row_of_lane: torch.Tensor                # source side: [hi - lo, K]
     wtables: dict = field(default_factory=dict)
+    out_rows: Optional[torch.Tensor] = None  # xGMI transport, expert side: [n] window row address per unit
 
 
 @dataclass

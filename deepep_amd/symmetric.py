@@ -8,7 +8,8 @@ Every rank allocates one uncached device window (deepep_sym_alloc), exports it w
 HIP IPC, and opens every peer's window (deepep_sym_import); kernels then store into a
 peer's HBM over xGMI.  Layout of a window:
 
-    [0, HEADER_BYTES)        int64 flags[num_ranks]: barrier epochs written by the peers
+    [0, HEADER_BYTES)        int64 flags[64 slots][64 ranks]: barrier epochs written by the peers
+                             (slot 0: the full barrier; slots 1..63: split barriers of pipelined phases)
     [HEADER_BYTES, ...)      data: the combine receive rows (see ElasticBuffer._combine_xgmi)
 """
 import ctypes
@@ -59,6 +60,7 @@ class SymmetricBuffer:
         self.data = torch.as_tensor(_DeviceArray(self.base + HEADER_BYTES, self.data_bytes), device=device)
         self.error_flag = torch.zeros((1,), dtype=torch.int32, device=device)
         self.epoch = 0
+        self._slot_epoch = [0] * 64                 # split-barrier counters (slot 0 = the full barrier)
 
     def _ipc_exchange(self, group) -> List[int]:
         handle = ctypes.create_string_buffer(64)
@@ -82,6 +84,20 @@ class SymmetricBuffer:
         handle = stream.cuda_stream if stream is not None else torch.cuda.current_stream().cuda_stream
         _lib.check(self.lib.deepep_sym_barrier(self.bases_dev.data_ptr(), self.rank, self.num_ranks, self.epoch,
                                                self.timeout_us, self.error_flag.data_ptr(), handle), 'sym_barrier')
+
+    def signal(self, slot: int, stream) -> None:
+        """Publish this rank's arrival at split barrier `slot` (1..63) after `stream`'s earlier work."""
+        self._slot_epoch[slot] += 1
+        handle = stream.cuda_stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        _lib.check(self.lib.deepep_sym_signal(self.bases_dev.data_ptr(), self.rank, self.num_ranks, slot,
+                                              self._slot_epoch[slot], handle), 'sym_signal')
+
+    def wait(self, slot: int, stream) -> None:
+        """Make `stream` wait until every rank has signalled `slot` as often as this rank has."""
+        handle = stream.cuda_stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        _lib.check(self.lib.deepep_sym_wait(self.bases_dev.data_ptr(), self.rank, self.num_ranks, slot,
+                                            self._slot_epoch[slot], self.timeout_us, self.error_flag.data_ptr(),
+                                            handle), 'sym_wait')
 
     def check(self) -> None:
         """Raise if a barrier timed out (host sync)."""

@@ -196,6 +196,17 @@ int deepep_sym_close(void* ptr);
 int deepep_sym_barrier(const uint64_t* peer_flags, int rank, int num_ranks, int64_t epoch, int64_t timeout_us,
                        int32_t* error_flag, deepep_stream_t stream);
 
+/* Split barrier for pipelined phases, on flag slot 1 <= slot < DEEPEP_SYM_FLAG_SLOTS of the same
+ * tables (int64 [DEEPEP_SYM_FLAG_SLOTS][64] per window; slot 0 is deepep_sym_barrier's):
+ * deepep_sym_signal stores `value` into slot `slot`, entry [rank], of every rank's table after the
+ * stream's earlier work (system-scope release); deepep_sym_wait waits until every entry of slot
+ * `slot` of this rank's table reaches `value` (timeout as deepep_sym_barrier). */
+#define DEEPEP_SYM_FLAG_SLOTS 64
+int deepep_sym_signal(const uint64_t* peer_flags, int rank, int num_ranks, int slot, int64_t value,
+                      deepep_stream_t stream);
+int deepep_sym_wait(const uint64_t* peer_flags, int rank, int num_ranks, int slot, int64_t value, int64_t timeout_us,
+                    int32_t* error_flag, deepep_stream_t stream);
+
 /* Phase A writing straight into the owners' receive rows (combine_impl's NVLink push,
  * combine.cuh:96-106, 125-176, 215-226): the reduce of deepep_combine_reduce(DEEPEP_MODE_LOCAL, ...)
  * with unit u's bf16 row stored at byte address out_rows[u] (any rank's window, 16-byte aligned)

@@ -34,9 +34,11 @@ def _bf16(a: np.ndarray, dev) -> torch.Tensor:
     return torch.from_numpy(np.ascontiguousarray(a).view(np.int16)).view(torch.bfloat16).to(dev)
 
 
-def _worker(rank, world, port, seed, T, H, K, queue, empty_rank=-1):
+def _worker(rank, world, port, seed, T, H, K, queue, empty_rank=-1, chunks=0):
     sys.path.insert(0, ROOT)
     try:
+        if chunks:
+            os.environ['DEEPEP_COMBINE_CHUNKS'] = str(chunks)
         os.environ['MASTER_ADDR'] = '127.0.0.1'
         os.environ['MASTER_PORT'] = str(port)
         import torch.distributed as dist
@@ -126,13 +128,16 @@ def _worker(rank, world, port, seed, T, H, K, queue, empty_rank=-1):
         queue.put((rank, [traceback.format_exc()]))
 
 
-@pytest.mark.parametrize('world,T,H,K,empty_rank', [(2, 96, 1024, 8, -1), (4, 64, 7168, 8, -1), (4, 80, 256, 2, -1),
-                                                   (3, 40, 512, 4, 1)])
-def test_xgmi_transport_matches_oracle(world, T, H, K, empty_rank):
+@pytest.mark.parametrize('world,T,H,K,empty_rank,chunks', [
+    (2, 96, 1024, 8, -1, 0), (4, 64, 7168, 8, -1, 0), (4, 80, 256, 2, -1, 0), (3, 40, 512, 4, 1, 0),
+    (2, 96, 1024, 8, -1, 3), (4, 80, 256, 2, -1, 5), (3, 40, 512, 4, 1, 4)])
+def test_xgmi_transport_matches_oracle(world, T, H, K, empty_rank, chunks):
+    """chunks > 0: the pipelined schedule (phase A per source-token chunk + split barrier, phase B
+    of each chunk on a second stream)."""
     ctx = mp.get_context('spawn')
     queue = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, 100 + world + K, T, H, K, queue, empty_rank))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, 100 + world + K, T, H, K, queue, empty_rank, chunks))
              for r in range(world)]
     for p in procs:
         p.start()

@@ -401,12 +401,12 @@ def main():
             'metric': 'combine GB/s (device-resident BF16 top-k weighted reduce) at 1/2/4/8 MI355X',
             'value': round(value, 2), 'unit': 'GB/s', 'n_gpus': world, 'steps': args.steps,
             'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 4), 'higher_is_better': True,
-            'scaling': 'weak', 'vs_baseline': None, 'dtype': 'bf16 (fp32 accumulate)', 'data': 'synthetic',
+            'scaling': 'weak', 'vs_baseline': None, 'dtype': 'bf16', 'data': 'synthetic',
             'config': {'workload': f'EP={world} combine, {T} tokens/rank x hidden {H} x top-{K}, '
                                    f'{E} experts, {"skewed x%g" % args.skew if args.skew != 1.0 else "uniform"} routing, '
                                    f'{"FP8 dispatch, " if args.fp8_dispatch else ""}expanded layout, '
                                    f'{"gating-weighted" if weighted else "plain (reference semantics)"}',
-                       'tokens_per_rank': T, 'hidden': H, 'topk': K, 'experts': E,
+                       'tokens_per_rank': T, 'hidden': H, 'topk': K, 'experts': E, 'accumulate': 'fp32',
                        'parallelism': f'ep{world}', 'transport': transport},
             'roofline': roofline, 'cpu_baseline': cpu_baseline, 'cpu_torch': cpu_torch, 'loopback': loopback,
             'phases': phases, 'rccl': rccl, 'xgmi': xgmi,

@@ -79,7 +79,8 @@ const char* deepep_amd_last_error(void);
  *                  out_weights[u*out_weights_stride + k] = (i = wtable ? wtable[u*wtable_stride + k]
  *                                                             : u*num_weights + k) >= 0 ? wsrc[i] : 0
  *                  (a stride lets the weights ride in the tail of packed exchange rows)
- *   units_per_block  reserved (0); the launch tiles (row, column-chunk) items, 4 per workgroup
+ *   units_per_block  workgroup shape: 4 = 4 (row, column-chunk) items per 256-thread workgroup,
+ *                  anything else = the default 8 items per 512-thread workgroup
  *   error_flag     device int or NULL; set to 1 when a slot is >= num_src_rows
  *                  (such slots are skipped, never dereferenced)
  */

@@ -9,9 +9,9 @@ semantics (csrc/elastic/buffer.hpp:526-584) and the same error behaviour
   EP = 1   one fused launch (local reduce + epilogue, no receive buffer);
   EP > 1   phase A (local reduce per received token) -> one RCCL all_to_all_single
            of the bf16 partials over xGMI -> phase B (epilogue reduce + bias).
-* dispatch (the handle producer, not the optimisation target of this build) is
-  written with torch ops and one RCCL all_to_all_single of packed token rows; it
-  produces the reference's handle layout (recv_src_metadata etc.) with the
+* dispatch (the handle producer) is seven HIP kernels (csrc/dispatch.hip) around one
+  exchange of counts (one host sync) and one RCCL all_to_all_single of packed token
+  rows; it produces the reference's handle layout (recv_src_metadata etc.) with the
   deterministic receive order the combine plan relies on (handle.py).
 
 Single node only: num_scaleout_ranks == 1 (hybrid RDMA mode, Engram, PP and AGRS
@@ -373,13 +373,22 @@ class ElasticBuffer:
                 dst_slot = torch.empty((T, R), dtype=torch.int32, device=dev)
                 send_counts = torch.empty((R,), dtype=torch.int32, device=dev)
                 kern.dispatch_route(idx64, num_experts, R, dst_slot, send_counts, stream=stream)
+                expert_hist = torch.empty((num_experts,), dtype=torch.int32, device=dev)
+                kern.dispatch_expert_counts(idx64, num_experts, expert_hist, stream=stream)
+                # notify (dispatch.cuh:79-258): every destination gets [tokens | tokens per local expert]
+                # from this rank; one exchange and ONE host sync size every receive-side allocation
+                notify = torch.cat([send_counts.view(R, 1), expert_hist.view(R, epr)], dim=1)
                 if R == 1:
-                    recv_counts_t = send_counts
+                    recv_notify = notify
                 else:
-                    recv_counts_t = torch.empty_like(send_counts)
-                    self._a2a(recv_counts_t, send_counts)
-                counts_l = [int(v) for v in torch.cat([send_counts, recv_counts_t]).tolist()]   # host sync
-                send_counts_l, recv_counts_l = counts_l[:R], counts_l[R:]
+                    recv_notify = torch.empty_like(notify)
+                    self._a2a(recv_notify, notify)
+                host = [int(v) for v in torch.cat([send_counts, recv_notify.view(-1)]).tolist()]   # host sync
+                send_counts_l = host[:R]
+                rows = [host[R + i * (1 + epr): R + (i + 1) * (1 + epr)] for i in range(R)]
+                recv_counts_l = [row[0] for row in rows]
+                expert_counts_l = [sum(row[1 + e] for row in rows) for e in range(epr)]
+                recv_counts_t = recv_notify[:, 0].contiguous()
                 send_offsets = (torch.cumsum(send_counts, 0) - send_counts).to(torch.int32)
             N = sum(recv_counts_l)
             x_bytes = x.contiguous().view(torch.uint8).view(T, H * x.element_size())
@@ -420,8 +429,7 @@ class ElasticBuffer:
                 psum_expert = torch.empty((epr,), dtype=torch.int32, device=dev)
                 kern.dispatch_scan(block_counts, epr, expert_alignment, do_expand, expert_counts, psum_expert,
                                    stream=stream)
-                counts_l = [int(v) for v in expert_counts.tolist()]
-                aligned_l = [align(c, expert_alignment) for c in counts_l]
+                aligned_l = [align(c, expert_alignment) for c in expert_counts_l]      # known since notify
                 if cumulative_local_expert_recv_stats is not None:
                     cumulative_local_expert_recv_stats += expert_counts.to(cumulative_local_expert_recv_stats.dtype)
                 self._before_epilogue(previous_event_before_epilogue)

@@ -96,6 +96,31 @@ route_assign_kernel(const int64_t* __restrict__ topk_idx, int T, int K, int epr,
     }
 }
 
+// ---------------------------------------------------------------- expert histogram (notify)
+// counts[e] += #{(t, k) : topk_idx[t][k] == e}: the per-expert half of dispatch_impl's notify
+// (dispatch.cuh:79-258), exchanged together with the per-rank counts so the receiver learns its
+// expert sizes -- and the host both vectors -- in one sync.  LDS histogram per workgroup, then one
+// global atomic per non-empty bin (integer adds: the result does not depend on their order).
+constexpr int kHistEntries = 2048;                   // (t, k) entries per workgroup
+
+__global__ void __launch_bounds__(256)
+expert_hist_kernel(const int64_t* __restrict__ topk_idx, int64_t n, int E, int32_t* __restrict__ counts) {
+    extern __shared__ int32_t s_hist[];              // [E]
+    for (int e = threadIdx.x; e < E; e += 256) s_hist[e] = 0;
+    __syncthreads();
+    const int64_t base = static_cast<int64_t>(blockIdx.x) * kHistEntries;
+    for (int j = threadIdx.x; j < kHistEntries; j += 256) {
+        const int64_t i = base + j;
+        if (i < n) {
+            const int64_t e = topk_idx[i];
+            if (e >= 0 && e < E) atomicAdd(&s_hist[e], 1);
+        }
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < E; e += 256)
+        if (s_hist[e] != 0) atomicAdd(&counts[e], s_hist[e]);
+}
+
 // ---------------------------------------------------------------- pack: one wave per token
 // packed row layout (bytes): [x | sf @sf_off | topk_idx (int64) @idx_off | weights @w_off | src @src_off]
 __global__ void __launch_bounds__(64)
@@ -364,6 +389,21 @@ int deepep_dispatch_route(const int64_t* topk_idx, int num_tokens, int num_topk,
     hipLaunchKernelGGL(route_assign_kernel, dim3(nb), dim3(256), 0, s, topk_idx, num_tokens, num_topk, epr, num_ranks,
                        block_counts, dst_slot, send_counts);
     return launch_status("dispatch_route");
+}
+
+int deepep_dispatch_expert_counts(const int64_t* topk_idx, int num_tokens, int num_topk, int num_experts,
+                                  int32_t* counts, deepep_stream_t stream) {
+    if (num_tokens < 0 || num_topk < 1 || num_topk > 32 || num_experts < 1 || num_experts > 32768 ||
+        counts == nullptr || (num_tokens > 0 && topk_idx == nullptr))
+        return deepep_amd_set_error(DEEPEP_ERR_INVALID_ARG, "dispatch_expert_counts: invalid arguments");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const hipError_t e = hipMemsetAsync(counts, 0, sizeof(int32_t) * num_experts, s);
+    if (e != hipSuccess) return launch_status("dispatch_expert_counts memset");
+    const int64_t n = static_cast<int64_t>(num_tokens) * num_topk;
+    if (n > 0)
+        hipLaunchKernelGGL(expert_hist_kernel, dim3(static_cast<unsigned>((n + kHistEntries - 1) / kHistEntries)),
+                           dim3(256), num_experts * 4, s, topk_idx, n, num_experts, counts);
+    return launch_status("dispatch_expert_counts");
 }
 
 int deepep_dispatch_pack(const void* x, int64_t x_row_stride_bytes, int x_bytes,

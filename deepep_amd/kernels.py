@@ -159,6 +159,16 @@ class HipKernels:
                                             ptr(send_counts), ptr(block_counts), _stream_handle(stream))
         _lib.check(rc, 'dispatch_route')
 
+    def dispatch_expert_counts(self, topk_idx, num_experts, counts, stream=None):
+        """counts[e] = (t, k) entries routed to expert e (int32 [num_experts])."""
+        _require(topk_idx.is_cuda and topk_idx.dtype == torch.int64 and topk_idx.is_contiguous(), 'topk_idx int64')
+        _require(counts.dtype == torch.int32 and counts.is_contiguous() and counts.numel() == num_experts,
+                 'expert counts must be contiguous int32 [num_experts]')
+        T, K = topk_idx.shape
+        rc = self.lib.deepep_dispatch_expert_counts(ptr(topk_idx), T, K, num_experts, ptr(counts),
+                                                    _stream_handle(stream))
+        _lib.check(rc, 'dispatch_expert_counts')
+
     def dispatch_pack(self, x_bytes, sf_bytes, topk_idx, topk_weights, src_base, dst_slot, send_offsets,
                       packed, layout: RowLayout, stream=None):
         """x_bytes / sf_bytes: [T, bytes] uint8 views (rows may be strided)."""

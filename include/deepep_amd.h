@@ -26,7 +26,7 @@
  *       materialised once per handle
  *   deepep_combine_buffer_size
  *       ElasticBuffer::get_combine_buffer_size (csrc/elastic/buffer.hpp:616-650)
- *   deepep_dispatch_route / _pack                    (the handle producer, send side)
+ *   deepep_dispatch_route / _expert_counts / _pack   (the handle producer, send side)
  *       dispatch_impl's notify, slot assignment and token push
  *       (deep_ep/include/deep_ep/impls/dispatch.cuh:79-258, 336-392)
  *   deepep_dispatch_count / _scan / _slots / _copy   (receive side)
@@ -45,7 +45,7 @@ extern "C" {
 
 typedef struct ihipStream_t* deepep_stream_t;   /* == hipStream_t */
 
-#define DEEPEP_AMD_ABI_VERSION 3
+#define DEEPEP_AMD_ABI_VERSION 4
 
 #define DEEPEP_OK               0
 #define DEEPEP_ERR_INVALID_ARG  (-1)
@@ -136,6 +136,14 @@ int deepep_set_launch_config(int vec_per_lane, int stage_lds, int store_policy);
  * ceil(num_tokens / 256) * num_ranks entries. */
 int deepep_dispatch_route(const int64_t* topk_idx, int num_tokens, int num_topk, int num_experts, int num_ranks,
                           int32_t* dst_slot, int32_t* send_counts, int32_t* block_counts, deepep_stream_t stream);
+
+/* counts[e] = #{(t, k) : topk_idx[t][k] == e} (int32 [num_experts], zeroed first; entries < 0 are
+ * masked slots).  The per-expert half of dispatch_impl's notify (dispatch.cuh:79-258): each sender
+ * sends slice [r * experts_per_rank, (r + 1) * experts_per_rank) to rank r with its per-rank count, so
+ * one exchange and one host sync give the receiver both its row count per source rank and its
+ * rows per local expert. */
+int deepep_dispatch_expert_counts(const int64_t* topk_idx, int num_tokens, int num_topk, int num_experts,
+                                  int32_t* counts, deepep_stream_t stream);
 
 /* Write packed row send_offsets[r] + dst_slot[t][r] for every (token t, destination r);
  * src_global_idx = src_base + t.  topk_weights may be NULL (zeros are sent). */

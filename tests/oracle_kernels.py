@@ -63,6 +63,10 @@ class OracleKernels:
                                    torch.full(is_to.shape, -1, dtype=torch.int64)).to(torch.int32))
         send_counts.copy_(is_to.sum(dim=0).to(torch.int32))
 
+    def dispatch_expert_counts(self, topk_idx, num_experts, counts, stream=None):
+        valid = topk_idx[topk_idx >= 0].view(-1)
+        counts.copy_(torch.bincount(valid, minlength=num_experts)[:num_experts].to(torch.int32))
+
     def dispatch_pack(self, x_bytes, sf_bytes, topk_idx, topk_weights, src_base, dst_slot, send_offsets,
                       packed, layout, stream=None):
         t_idx, r_idx = (dst_slot >= 0).nonzero(as_tuple=True)

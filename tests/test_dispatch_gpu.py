@@ -56,7 +56,9 @@ def _run_dispatch(kern, dev, ranks, E, K, H, T_max, expanded, alignment, fp8, di
         packed = torch.zeros((sum(cl), layout.row_bytes), dtype=torch.uint8, device=dev)
         kern.dispatch_pack(xb[:, :0] if direct else xb, None if direct else sb, idx, w, r * T_max, dst, offs,
                            packed, layout)
-        sends.append((dst.cpu(), cl, packed, layout, xb, sb))
+        hist = torch.empty((E,), dtype=torch.int32, device=dev)
+        kern.dispatch_expert_counts(idx, E, hist)
+        sends.append((dst.cpu(), cl, packed, layout, xb, sb, hist.cpu()))
     outs = []
     for r in range(R):
         parts = [sends[s][2][sum(sends[s][1][:r]):sum(sends[s][1][:r + 1])] for s in range(R)]
@@ -90,7 +92,8 @@ def _run_dispatch(kern, dev, ranks, E, K, H, T_max, expanded, alignment, fp8, di
                            num_max_tokens=T_max)
         outs.append(dict(meta=meta.cpu(), ridx=None if ridx is None else ridx.cpu(), ec=ec.cpu(), pe=pe.cpu(),
                          rx=rx.cpu(), rsf=None if rsf is None else rsf.cpu(), rw=rw.cpu(), dst=sends[r][0],
-                         cnt=sends[r][1]))
+                         cnt=sends[r][1],
+                         notify_ec=sum(sends[s][6][r * epr:(r + 1) * epr] for s in range(R))))
     return outs
 
 
@@ -122,6 +125,8 @@ def test_dispatch_primitives_match_cpu(hip, R, K, E, T, H, expanded, alignment, 
         if not expanded:
             assert torch.equal(g['ridx'], e['ridx']), f'rank {r} recv_topk_idx'
         assert torch.equal(g['ec'], e['ec']) and torch.equal(g['pe'], e['pe']), f'rank {r} expert counts'
+        # the notify histogram (senders' slices for rank r) predicts the receive side's counts
+        assert torch.equal(g['notify_ec'], g['ec']) and torch.equal(e['notify_ec'], e['ec']), f'rank {r} notify'
         assert torch.equal(g['rx'].view(torch.uint8), e['rx'].view(torch.uint8)), f'rank {r} recv_x'
         assert torch.equal(g['rw'], e['rw']), f'rank {r} weights'
         if fp8:

@@ -62,6 +62,79 @@ __global__ void __launch_bounds__(256) gather_copy(const uint8_t* x, const int32
     }
 }
 
+
+// Generalised source-major scatter: kWaves waves per workgroup, item = (token, 64*kVPT-vector chunk).
+template <int kWaves, int kVPT, int kAux>
+__global__ void __launch_bounds__(64 * kWaves) scatter_copy_t(const uint8_t* x, const int32_t* dst, int T, int K,
+                                                              int xb, uint8_t* out) {
+    const int lane = threadIdx.x & 63;
+    constexpr int kCh = 64 * kVPT;
+    const int nvec = xb / 16, nch = (nvec + kCh - 1) / kCh;
+    const int64_t it = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+    if (it >= (int64_t)T * nch) return;
+    const int64_t t = it / nch;
+    const int c = (int)(it - t * nch);
+    int32_t my = lane < K ? dst[t * K + lane] : -1;
+    const uint64_t m0 = __ballot(my >= 0);
+    const u32x4 z = {0u, 0u, 0u, 0u};
+    u32x4 a[kVPT];
+#pragma unroll
+    for (int v = 0; v < kVPT; ++v) {
+        const int vi = c * kCh + v * 64 + lane;
+        a[v] = vi < nvec ? __builtin_nontemporal_load((const u32x4*)(x + t * xb) + vi) : z;
+    }
+    for (uint64_t m = m0; m; m &= m - 1) {
+        const int64_t d = __builtin_amdgcn_readlane(my, __builtin_ctzll(m));
+        auto rs = __builtin_amdgcn_make_buffer_rsrc(out + d * xb, 0, xb, 0x00020000);
+#pragma unroll
+        for (int v = 0; v < kVPT; ++v)
+            __builtin_amdgcn_raw_buffer_store_b128(a[v], rs, (c * kCh + v * 64 + lane) * 16, 0, kAux);
+    }
+}
+
+template <int kWaves, int kVPT, int kAux>
+static void launch_t(const uint8_t* x, const int32_t* dst, int T, int K, int xb, uint8_t* o, hipStream_t s) {
+    const int nch = (xb / 16 + 64 * kVPT - 1) / (64 * kVPT);
+    const int64_t items = (int64_t)T * nch;
+    hipLaunchKernelGGL((scatter_copy_t<kWaves, kVPT, kAux>), dim3((unsigned)((items + kWaves - 1) / kWaves)),
+                       dim3(64 * kWaves), 0, s, x, dst, T, K, xb, o);
+}
+
+
+// Write-only scatter (no loads): the destination pattern of the copy with constant data.
+__global__ void __launch_bounds__(256) scatter_write_only(const int32_t* dst, int T, int K, int xb, uint8_t* out) {
+    const int lane = threadIdx.x & 63;
+    const int nvec = xb / 16, nch = (nvec + 127) / 128;
+    const int64_t it = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (it >= (int64_t)T * nch) return;
+    const int64_t t = it / nch;
+    const int c = (int)(it - t * nch);
+    int32_t my = lane < K ? dst[t * K + lane] : -1;
+    const uint64_t m0 = __ballot(my >= 0);
+    const int v0 = c * 128 + lane, v1 = v0 + 64;
+    const u32x4 a = {(uint32_t)t, 1u, 2u, 3u};
+    for (uint64_t m = m0; m; m &= m - 1) {
+        const int64_t d = __builtin_amdgcn_readlane(my, __builtin_ctzll(m));
+        auto rs = __builtin_amdgcn_make_buffer_rsrc(out + d * xb, 0, xb, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(a, rs, v0 * 16, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(a, rs, v1 * 16, 0, 16);
+    }
+}
+// Write-only in address order: one wave per (row, 2 KiB chunk) of out.
+__global__ void __launch_bounds__(256) seq_write_only(int N, int xb, uint8_t* out) {
+    const int lane = threadIdx.x & 63;
+    const int nvec = xb / 16, nch = (nvec + 127) / 128;
+    const int64_t it = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (it >= (int64_t)N * nch) return;
+    const int64_t j = it / nch;
+    const int c = (int)(it - j * nch);
+    const int v0 = c * 128 + lane, v1 = v0 + 64;
+    const u32x4 a = {(uint32_t)j, 1u, 2u, 3u};
+    auto rs = __builtin_amdgcn_make_buffer_rsrc(out + j * xb, 0, xb, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(a, rs, v0 * 16, 0, 16);
+    __builtin_amdgcn_raw_buffer_store_b128(a, rs, v1 * 16, 0, 16);
+}
+
 extern "C" int probe_copy(int variant, const void* x, const int32_t* dst, const int32_t* inv, int T, int K, int N,
                           int xb, void* out, hipStream_t s) {
     const int nch = (xb / 16 + 127) / 128;
@@ -76,6 +149,20 @@ extern "C" int probe_copy(int variant, const void* x, const int32_t* dst, const 
         case 8: hipLaunchKernelGGL((gather_copy<8, 16>), grid((int64_t)(N + 7) / 8 * nch), dim3(256), 0, s, xx, inv, N, xb, o); break;
         case 40: hipLaunchKernelGGL((gather_copy<4, 0>), grid((int64_t)(N + 3) / 4 * nch), dim3(256), 0, s, xx, inv, N, xb, o); break;
         case 42: hipLaunchKernelGGL((gather_copy<4, 2>), grid((int64_t)(N + 3) / 4 * nch), dim3(256), 0, s, xx, inv, N, xb, o); break;
+        case 100: launch_t<4, 2, 16>(xx, dst, T, K, xb, o, s); break;
+        case 101: launch_t<8, 2, 16>(xx, dst, T, K, xb, o, s); break;
+        case 102: launch_t<4, 4, 16>(xx, dst, T, K, xb, o, s); break;
+        case 103: launch_t<8, 4, 16>(xx, dst, T, K, xb, o, s); break;
+        case 104: launch_t<4, 7, 16>(xx, dst, T, K, xb, o, s); break;
+        case 105: launch_t<4, 14, 16>(xx, dst, T, K, xb, o, s); break;
+        case 106: launch_t<4, 2, 0>(xx, dst, T, K, xb, o, s); break;
+        case 107: launch_t<4, 2, 2>(xx, dst, T, K, xb, o, s); break;
+        case 108: launch_t<2, 2, 16>(xx, dst, T, K, xb, o, s); break;
+        case 109: launch_t<4, 1, 16>(xx, dst, T, K, xb, o, s); break;
+        case 110: launch_t<16, 2, 16>(xx, dst, T, K, xb, o, s); break;
+        case 111: launch_t<8, 7, 16>(xx, dst, T, K, xb, o, s); break;
+        case 200: hipLaunchKernelGGL(scatter_write_only, grid((int64_t)T * nch), dim3(256), 0, s, dst, T, K, xb, o); break;
+        case 201: hipLaunchKernelGGL(seq_write_only, grid((int64_t)N * nch), dim3(256), 0, s, N, xb, o); break;
         default: return -1;
     }
     return (int)hipGetLastError();

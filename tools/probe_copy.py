@@ -41,13 +41,13 @@ def main():
     s = torch.cuda.current_stream()
     xb = H * 2
     nbytes = T * xb + N * xb
-    for v in (0, 1, 2, 4, 8, 40, 42, 0):
+    for v in (0, 200, 201, 1, 0, 200, 201):
         out.zero_()
         fn = lambda: lib.probe_copy(v, x.data_ptr(), dst.data_ptr(), inv.data_ptr(), T, K, N, xb, out.data_ptr(),
                                     s.cuda_stream)
         assert fn() == 0
         torch.cuda.synchronize()
-        ok = bool(torch.equal(out, ref))
+        ok = bool(torch.equal(out, ref)) if v < 200 else None
         us = timeit(fn, s, iters=20)
         print(json.dumps(dict(variant=v, us=round(us, 1), gbps=round(nbytes / us / 1e3, 1), equal=ok)), flush=True)
     dist.destroy_process_group()

@@ -798,10 +798,13 @@ class ElasticBuffer:
                         'bias must be contiguous bf16 [num_combined_tokens, hidden]')
         single_reduction = expanded and not self.allow_multiple_reduction
         if single_reduction:
-            _assert(topk_weights is None, 'expanded combine without multiple reduction cannot carry top-k weights')
+            # the reference's expanded send carries no weights (combine.cuh:67-69) -- unless they are
+            # the gating weights this build applies (the legacy low-latency semantics)
+            _assert(topk_weights is None or apply_topk_weights,
+                    'expanded combine without multiple reduction cannot carry top-k weights')
         if apply_topk_weights:
-            _assert(expanded and topk_weights is not None and not single_reduction,
-                    'apply_topk_weights needs the expanded layout, topk_weights and multiple reduction')
+            _assert(expanded and topk_weights is not None,
+                    'apply_topk_weights needs the expanded layout and topk_weights')
 
         kern = self.kernels
         R = self.num_ranks
@@ -824,22 +827,32 @@ class ElasticBuffer:
             if R == 1:
                 self._before_epilogue(previous_event_before_epilogue)
                 if single_reduction:
-                    kern.combine_reduce(MODE_EPILOGUE, x, combined_x, T, table=plan.local_table,
-                                        bias0=bias_0, bias1=bias_1, stream=stream)
+                    kern.combine_reduce(MODE_EPILOGUE, x, combined_x, T, table=plan.local_table, row_weights=row_w,
+                                        bias0=bias_0, bias1=bias_1, wtable=plan.local_table, wsrc=wsrc,
+                                        out_weights=combined_w, stream=stream)
                 else:
                     wtable = plan.local_table if expanded else plan.local_wtable
                     kern.combine_reduce(MODE_FUSED, x, combined_x, T, table=plan.local_table, row_weights=row_w,
                                         bias0=bias_0, bias1=bias_1, wtable=wtable, wsrc=wsrc,
                                         out_weights=combined_w, stream=stream)
             elif single_reduction:
+                # every valid expanded row travels unreduced (kDoExpandedSend, combine.cuh:177-213);
+                # weighted: with its gating weight in a 16-byte row tail, applied by the one reduction
                 n_send = sum(plan.send_counts1)
-                send = torch.empty((n_send, hidden), dtype=x.dtype, device=x.device)
-                kern.combine_reduce(MODE_LOCAL, x, send, n_send, table=plan.send_slots1, stream=stream)
-                recv = torch.empty((sum(plan.back_counts1), hidden), dtype=x.dtype, device=x.device)
+                w_elems = 8 if row_w is not None else 0
+                send = torch.empty((n_send, hidden + w_elems), dtype=x.dtype, device=x.device)
+                send_w = send[:, hidden:].view(torch.float32)[:, :1] if w_elems else None
+                kern.combine_reduce(MODE_LOCAL, x, send[:, :hidden], n_send, table=plan.send_slots1,
+                                    wtable=plan.send_slots1 if w_elems else None, wsrc=wsrc if w_elems else None,
+                                    out_weights=send_w, stream=stream)
+                recv = torch.empty((sum(plan.back_counts1), hidden + w_elems), dtype=x.dtype, device=x.device)
                 self._all_to_all(recv, send, plan.back_counts1, plan.send_counts1)
                 self._before_epilogue(previous_event_before_epilogue)
-                kern.combine_reduce(MODE_EPILOGUE, recv, combined_x, T, table=plan.table_b1,
-                                    bias0=bias_0, bias1=bias_1, stream=stream)
+                recv_w = recv[:, hidden:].view(torch.float32)[:, 0].contiguous() if w_elems else None
+                kern.combine_reduce(MODE_EPILOGUE, recv[:, :hidden], combined_x, T, table=plan.table_b1,
+                                    row_weights=recv_w, bias0=bias_0, bias1=bias_1,
+                                    wtable=plan.table_b1 if w_elems else None, wsrc=recv_w, out_weights=combined_w,
+                                    stream=stream)
             elif use_xgmi:
                 self._combine_xgmi(handle, x, expanded, row_w, wsrc, K, hidden, bias_0, bias_1, topk_weights,
                                    combined_x, combined_w, previous_event_before_epilogue, stream)

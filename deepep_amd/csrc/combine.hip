@@ -224,7 +224,8 @@ combine_rows_kernel(const Params p) {
         copy_row = !kWeighted && n == 1;                      // no_local_reduce (combine.cuh:134-156)
         init = (!kWeighted && n == 2) ? -0.0f : 0.0f;
     } else {
-        init = (!has_bias && n == 2) ? -0.0f : 0.0f;          // epilogue: bypass only without bias
+        // epilogue: bypass only without bias; weighted (single reduction, legacy semantics): from +0
+        init = (!kWeighted && !has_bias && n == 2) ? -0.0f : 0.0f;
     }
     float acc[kVPT][8];
 #pragma unroll
@@ -420,8 +421,8 @@ int deepep_combine_reduce(int mode, int weighted,
         return set_error(DEEPEP_ERR_INVALID_ARG, "row strides must be >= hidden and multiples of 8 elements");
     if (table != nullptr && (table_width < 1 || table_width > kMaxWidth || table_stride < table_width))
         return set_error(DEEPEP_ERR_INVALID_ARG, "table width %d outside [1, %d] or stride too small", table_width, kMaxWidth);
-    if (weighted && (mode == DEEPEP_MODE_EPILOGUE || row_weights == nullptr))
-        return set_error(DEEPEP_ERR_INVALID_ARG, "weighted reduction needs row weights and mode LOCAL or FUSED");
+    if (weighted && row_weights == nullptr)
+        return set_error(DEEPEP_ERR_INVALID_ARG, "weighted reduction needs row weights");
     if (mode == DEEPEP_MODE_LOCAL && (bias0 != nullptr || bias1 != nullptr))
         return set_error(DEEPEP_ERR_INVALID_ARG, "bias is applied by the epilogue, not the local reduce");
     if (out_weights != nullptr && (wsrc == nullptr || num_weights < 1 || num_weights > kMaxWidth))
@@ -526,7 +527,8 @@ int launch_combine(int mode, int weighted, const Params& p, deepep_stream_t stre
         if (weighted) launch_vpt<DEEPEP_MODE_LOCAL, true>(p, vpt, lds, policy, s);
         else launch_vpt<DEEPEP_MODE_LOCAL, false>(p, vpt, lds, policy, s);
     } else if (mode == DEEPEP_MODE_EPILOGUE) {
-        launch_vpt<DEEPEP_MODE_EPILOGUE, false>(p, vpt, lds, policy, s);
+        if (weighted) launch_vpt<DEEPEP_MODE_EPILOGUE, true>(p, vpt, lds, policy, s);
+        else launch_vpt<DEEPEP_MODE_EPILOGUE, false>(p, vpt, lds, policy, s);
     } else {
         if (weighted) launch_vpt<DEEPEP_MODE_FUSED, true>(p, vpt, lds, policy, s);
         else launch_vpt<DEEPEP_MODE_FUSED, false>(p, vpt, lds, policy, s);

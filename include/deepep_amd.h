@@ -72,7 +72,8 @@ const char* deepep_amd_last_error(void);
  *   weighted       0: plain sum (ElasticBuffer semantics);
  *                  1: row j scaled by row_weights[slot_j] with an fp32 fma chain
  *                     (legacy low_latency_combine semantics, csrc/kernels/legacy/
- *                     internode_ll.cu:1072-1135); modes LOCAL and FUSED only
+ *                     internode_ll.cu:1072-1135); in mode EPILOGUE (the single-reduction
+ *                     combine) the chain starts from +0 + bias0 + bias1
  *   bias0, bias1   bf16 [num_units][hidden] or NULL (modes EPILOGUE and FUSED)
  *   out_weights    fp32 rows of out_weights_stride floats (0 = num_weights) or NULL: top-k
  *                  weight pass-through, written once per unit:

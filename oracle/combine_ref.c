@@ -97,14 +97,22 @@ static void combine_reduce_row(const uint16_t* const* src, int n, int width,
  * 1080-1125): combined_values start at 0.0f and accumulate
  * float(y) * weight; nvcc contracts that into one FMA (default
  * -fmad=true), restated here with fmaf(). */
-static void weighted_reduce_row(const uint16_t* const* src, const float* w, int n,
-                                int hidden, uint16_t* dst) {
+static void weighted_reduce_row_bias(const uint16_t* const* src, const float* w, int n,
+                                     const uint16_t* bias0, const uint16_t* bias1,
+                                     int hidden, uint16_t* dst) {
     for (int h = 0; h < hidden; ++h) {
         float acc = 0.0f;
+        if (bias0) acc += bf16_to_f32(bias0[h]);
+        if (bias1) acc += bf16_to_f32(bias1[h]);
         for (int j = 0; j < n; ++j)
             acc = fmaf(bf16_to_f32(src[j][h]), w[j], acc);
         dst[h] = f32_to_bf16(acc);
     }
+}
+
+static void weighted_reduce_row(const uint16_t* const* src, const float* w, int n,
+                                int hidden, uint16_t* dst) {
+    weighted_reduce_row_bias(src, w, n, NULL, NULL, hidden, dst);
 }
 
 /* ------------------------------------------------------------- phase A
@@ -254,7 +262,12 @@ int oracle_combine_weighted_ll(const uint16_t* y, const int64_t* topk_idx, const
  * reference's receive buffer.  Used by the CPU orchestration tests as a
  * stand-in kernel provider; its semantics are the phase-A/phase-B rules above
  * (mode 0 = phase A, 1 = phase B with width = table width, 2 = phase A then
- * phase B over one slot).  Pointers are host pointers. */
+ * phase B over one slot).  Pointers are host pointers.
+ * Weighted mode 1 (the single-reduction weighted combine: every expanded row
+ * sent unreduced, one reduction at the source rank) is the legacy low-latency
+ * sum with the bias in front: acc = 0 + bias0 + bias1, then acc = fma(y_j, w_j,
+ * acc) over the valid rows, one rounding -- without bias exactly
+ * internode_ll.cu:1072-1135. */
 int oracle_combine_rows(int mode, int weighted,
                         const uint16_t* src, int64_t num_src_rows, int64_t src_stride,
                         const int32_t* table, int64_t table_stride, int table_width,
@@ -283,7 +296,8 @@ int oracle_combine_rows(int mode, int weighted,
         const uint16_t* b0 = bias0 ? bias0 + (int64_t)u * hidden : NULL;
         const uint16_t* b1 = bias1 ? bias1 + (int64_t)u * hidden : NULL;
         if (mode == 1) {
-            combine_reduce_row(rows, n, width, b0, b1, hidden, dst);
+            if (weighted) weighted_reduce_row_bias(rows, w, n, b0, b1, hidden, dst);
+            else combine_reduce_row(rows, n, width, b0, b1, hidden, dst);
         } else {
             uint16_t* a = mode == 2 ? partial : dst;
             if (weighted) weighted_reduce_row(rows, w, n, hidden, a);

@@ -37,6 +37,20 @@ def _bf16_to_u16(t: torch.Tensor) -> np.ndarray:
     return t.contiguous().view(torch.int16).numpy().view(np.uint16)
 
 
+def _weighted_single(y_u16: np.ndarray, idx: torch.Tensor, w: torch.Tensor, bias) -> torch.Tensor:
+    """Expected single-reduction weighted combine of one source rank: acc = 0 + bias0 + bias1, then
+    the legacy low-latency fma chain over the valid top-k rows (oracle_combine_rows, mode 1 weighted)."""
+    from tests.oracle_kernels import OracleKernels
+    T, K, H = y_u16.shape
+    src = _u16_to_bf16(y_u16.reshape(T * K, H))
+    table = torch.where(idx >= 0, torch.arange(T * K).view(T, K), torch.full((T, K), -1)).to(torch.int32)
+    b0, b1 = (None, None) if bias is None else ((bias, None) if isinstance(bias, torch.Tensor) else bias)
+    out = torch.empty((T, H), dtype=torch.bfloat16)
+    OracleKernels().combine_reduce(1, src, out, T, table=table, row_weights=w.reshape(-1).contiguous(),
+                                   bias0=b0, bias1=b1)
+    return out
+
+
 def _worker(rank, world, port, fixture, queue, env=None):
     import sys
     sys.path.insert(0, ROOT)
@@ -46,6 +60,7 @@ def _worker(rank, world, port, fixture, queue, env=None):
         os.environ.update(env or {})
         dist.init_process_group('gloo', rank=rank, world_size=world)
         from deepep_amd import ElasticBuffer
+        import oracle
         from tests.oracle_kernels import OracleKernels
         fx = load(fixture)
         T, H, K, E, R = (int(v) for v in fx['meta'])
@@ -116,6 +131,16 @@ def _worker(rank, world, port, fixture, queue, env=None):
                     out, _, _ = buf.combine(x_red, handle, topk_weights=recv_w, bias=bias)
                     if not np.array_equal(_bf16_to_u16(out), me[f'combined_multi_b{nb}']):
                         failures.append(f'single-reduction non-expanded combine b{nb}')
+                    # gating-weighted: every row unreduced to its source rank, one fma chain there
+                    out, out_w, _ = buf.combine(x_exp, ex_handle, topk_weights=ex_w, bias=bias,
+                                                apply_topk_weights=True)
+                    if not torch.equal(out, _weighted_single(me['y'], topk_idx, topk_w, bias)):
+                        failures.append(f'single-reduction weighted combine b{nb}')
+                    if nb == 0 and not np.array_equal(_bf16_to_u16(out),
+                                                      oracle.weighted_ll(me['y'], me['topk_idx'], me['topk_weights'])):
+                        failures.append('single-reduction weighted != legacy low-latency restatement')
+                    if not torch.equal(out_w, topk_w):
+                        failures.append(f'single-reduction weighted pass-through b{nb}')
             buf.destroy()
         queue.put((rank, failures))
         dist.barrier()

@@ -1,6 +1,7 @@
 """GPU parity tests: the HIP kernels (through the C-ABI) against the oracle, bitwise.
 
-* kernel level: every reduction mode, weighted/unweighted, bias 0/1/2, slot-table widths
+* kernel level: every reduction mode, weighted/unweighted (weighted EPILOGUE = the single-reduction
+  gating-weighted combine), bias 0/1/2, slot-table widths
   1..32, ragged hidden sizes (tail lanes), empty tables, -0/inf edge values;
 * ElasticBuffer level on one GPU: the golden fixtures of the reference oracle at EP = 1
   (BASELINE config 1) and, with 4 or 8 ranks simulated by threads on the one device
@@ -106,8 +107,7 @@ def test_kernel_modes_widths(kern, mode, width, hidden):
     nbs = [0] if mode == MODE_LOCAL else [0, 1, 2]
     for nb in nbs:
         _run(kern, mode, False, 37, width, hidden, nb, seed=width * 100 + nb)
-        if mode != MODE_EPILOGUE:
-            _run(kern, mode, True, 37, width, hidden, nb, seed=width * 100 + nb + 7)
+        _run(kern, mode, True, 37, width, hidden, nb, seed=width * 100 + nb + 7)
 
 
 @pytest.mark.parametrize('mode', [MODE_LOCAL, MODE_EPILOGUE, MODE_FUSED])
@@ -131,8 +131,7 @@ def test_kernel_launch_configs_identical(kern, cfg):
     try:
         for mode in (MODE_LOCAL, MODE_EPILOGUE, MODE_FUSED):
             _run(kern, mode, False, 29, 8, 2056, 0 if mode == MODE_LOCAL else 2, seed=sum(cfg) + 2 + mode)
-            if mode != MODE_EPILOGUE:
-                _run(kern, mode, True, 29, 8, 7168, 0 if mode == MODE_LOCAL else 1, seed=sum(cfg) + 2 + 3 * mode)
+            _run(kern, mode, True, 29, 8, 7168, 0 if mode == MODE_LOCAL else 1, seed=sum(cfg) + 2 + 3 * mode)
     finally:
         kern.lib.deepep_set_launch_config(0, -1, -1)
 
@@ -295,6 +294,28 @@ def _buffer_case(rank, world, fixture, comm, results):
                     failures.append(f'{tag} b{nb}')
                 if not torch.equal(out_w.cpu(), torch.from_numpy(me['topk_weights'])):
                     failures.append(f'{tag} weights b{nb}')
+        # allow_multiple_reduction=False: every expanded row travels unreduced, one reduction at the
+        # source rank -- plain (refs.combine single-level fixtures) and gating-weighted (legacy
+        # low-latency fma chain, bias in front)
+        from tests.test_buffer_cpu import _weighted_single
+        sbuf = ElasticBuffer(grp, num_max_tokens_per_rank=T, hidden=H, num_topk=K, allow_multiple_reduction=False)
+        if world > 1:
+            sbuf._a2a = buf._a2a
+        for nb in (0, 1, 2):
+            bias = None if nb == 0 else (biases[0] if nb == 1 else tuple(biases))
+            out, out_w, _ = sbuf.combine(x_exp, ex_handle, bias=bias)
+            torch.cuda.synchronize()
+            if not np.array_equal(_u16(out), me[f'combined_single_b{nb}']) or out_w is not None:
+                failures.append(f'single-reduction b{nb}')
+            out, out_w, _ = sbuf.combine(x_exp, ex_handle, topk_weights=ex_w, bias=bias, apply_topk_weights=True)
+            torch.cuda.synchronize()
+            cpu_bias = None if bias is None else (bias.cpu() if nb == 1 else tuple(b.cpu() for b in bias))
+            exp = _weighted_single(me['y'], torch.from_numpy(me['topk_idx']), torch.from_numpy(me['topk_weights']),
+                                   cpu_bias)
+            if not torch.equal(out.cpu(), exp):
+                failures.append(f'single-reduction weighted b{nb}')
+            if not torch.equal(out_w.cpu(), torch.from_numpy(me['topk_weights'])):
+                failures.append(f'single-reduction weighted pass-through b{nb}')
         results[rank] = failures
     except Exception:
         import traceback

@@ -52,8 +52,18 @@ def main():
         torch.cuda.synchronize()
         return [a.elapsed_time(b) * 1e3 for a, b in evs]
 
+    # same kernel, same bytes, token-major rows (table[t][k] = t*K + k): no scatter
+    ident = (torch.arange(T, device='cuda').view(T, 1) * K + torch.arange(K, device='cuda').view(1, K)).to(torch.int32)
+    ident = ident.contiguous()
+
+    def launch_ident():
+        buf.kernels.combine_reduce(MODE_FUSED, y, out, T, table=ident, row_weights=ex_w,
+                                   wtable=ident, wsrc=ex_w, out_weights=out_w, stream=s)
+    ti = series(launch_ident, 200)
+    print(json.dumps(dict(what='fused_weighted_token_major_rows', p50=pct(ti, .5),
+                          frac_p50=round(nbytes / pct(ti, .5) / 1e3 / 8000, 4))), flush=True)
     dst = torch.empty_like(y)
-    for phase in range(3):
+    for phase in range(2):
         ts = series(launch, 500)
         print(json.dumps(dict(phase=phase, what='fused_weighted', first10=[round(t, 1) for t in ts[:10]],
                               p10=pct(ts, .1), p50=pct(ts, .5), p90=pct(ts, .9), mean=round(sum(ts) / len(ts), 1),

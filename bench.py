@@ -171,6 +171,92 @@ def _bench_xgmi(buf, y, handle, ex_w, weighted, total_bytes, steps, warmup, dev)
                      'symmetric windows over xGMI, device barriers, phase B from the local window')
 
 
+def _calc_diff(a: torch.Tensor, b: torch.Tensor) -> float:
+    """deep_ep/utils/math.py:5-9."""
+    a, b = a.double() + 1, b.double() + 1
+    return float(1 - 2 * (a * b).sum() / (a * a + b * b).sum())
+
+
+def _bench_single(y, handle, ex_w, weighted, total_bytes, steps, warmup, dev, ref_multi):
+    """EP > 1 combine with allow_multiple_reduction=False on the same batch: every expanded row
+    travels unreduced (weighted: with its gating weight) and the source rank reduces once -- the
+    legacy low-latency semantics, and the north star's "all-to-all feeding each rank's local reduce".
+    Timed like the main loop on both transports; per-phase times on RCCL (phase A = pack copy, B =
+    the one reduce).  Failures are reported, never raised."""
+    from deepep_amd import ElasticBuffer
+    T_max, H, K = handle.num_max_tokens_per_rank, y.shape[1], handle.topk_idx.shape[1]
+
+    def agree(ok: bool) -> bool:
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return bool(t.item())
+
+    def vmax(v: float) -> float:
+        t = torch.tensor([v], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    res, outs = {}, {}
+    transports = ['rccl'] + (['xgmi'] if os.environ.get('DEEPEP_BENCH_XGMI', '1') != '0' else [])
+    for transport in transports:
+        sb, err = None, None
+        try:
+            sb = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=T_max, hidden=H, num_topk=K,
+                               allow_multiple_reduction=False, explicitly_destroy=True, num_gpu_timeout_secs=10)
+            sb.transport = transport
+
+            def step():
+                return sb.combine(y, handle, topk_weights=ex_w if weighted else None, apply_topk_weights=weighted)
+            outs[transport] = step()[0]
+            torch.cuda.synchronize()
+            if sb._sym is not None:
+                sb._sym.check()
+        except Exception as e:      # noqa: BLE001 -- reported in the JSON line
+            err = f'{type(e).__name__}: {e}'[:300]
+        if not agree(err is None):
+            res[transport] = dict(error=err or 'failed on another rank')
+            outs.pop(transport, None)
+            continue
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        el = vmax(time.perf_counter() - t0)
+        entry = dict(value=round(total_bytes * steps / el / 1e9, 2), ms_per_step=round(el * 1e3 / steps, 4))
+        if transport == 'rccl':
+            sb._phase_events = []
+            n_ph = max(5, steps // 2)
+            for _ in range(n_ph):
+                step()
+            torch.cuda.synchronize()
+            ev, sb._phase_events = sb._phase_events, None
+            t_a = vmax(sum(ev[4 * i].elapsed_time(ev[4 * i + 1]) for i in range(n_ph)) / n_ph)
+            t_x = vmax(sum(ev[4 * i + 1].elapsed_time(ev[4 * i + 2]) for i in range(n_ph)) / n_ph)
+            t_b = vmax(sum(ev[4 * i + 2].elapsed_time(ev[4 * i + 3]) for i in range(n_ph)) / n_ph)
+            entry.update(phase_a_ms=round(t_a, 4), exchange_ms=round(t_x, 4), phase_b_ms=round(t_b, 4),
+                         reduce_only_gbps=round(total_bytes / (t_b * 1e-3) / 1e9, 1))
+        else:
+            entry['barrier_timeout'] = not agree(int(sb._sym.error_flag.item()) == 0)
+        res[transport] = entry
+        sb.destroy()
+    if 'rccl' in outs and 'xgmi' in outs and 'value' in res.get('xgmi', {}):
+        res['xgmi']['bitwise_equal_to_rccl'] = agree(bool(torch.equal(outs['rccl'], outs['xgmi'])))
+    if 'rccl' in outs:
+        d = vmax(_calc_diff(outs['rccl'], ref_multi))
+        res['calc_diff_vs_multi_reduction'] = d
+    res['note'] = ('allow_multiple_reduction=False, same batch and bytes: rows unreduced to the source rank '
+                   '(weighted: legacy low-latency fma chain), one reduce there; reduce_only = algorithmic bytes '
+                   'of all ranks / phase B (max over ranks)')
+    return res
+
+
 def _pmc_traffic(workload: str):
     """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_traffic.py), if any."""
     path = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
@@ -328,6 +414,11 @@ def main():
     xgmi = None
     if world > 1 and os.environ.get('DEEPEP_BENCH_XGMI', '1') != '0':
         xgmi = _bench_xgmi(buf, y, handle, ex_w, weighted, total_bytes, args.steps, args.warmup, dev)
+    single = None
+    if world > 1 and os.environ.get('DEEPEP_BENCH_SINGLE', '1') != '0':
+        ref_multi, _, _ = buf.combine(y, handle, topk_weights=ex_w, apply_topk_weights=weighted)
+        single = _bench_single(y, handle, ex_w, weighted, total_bytes, args.steps, args.warmup, dev, ref_multi)
+        del ref_multi
 
     # Handle producer: dispatch of the same batch, expanded layout.  Includes its
     # host syncs (received-token counts), as the reference's dispatch with do_cpu_sync=True.
@@ -409,7 +500,7 @@ def main():
                        'tokens_per_rank': T, 'hidden': H, 'topk': K, 'experts': E, 'accumulate': 'fp32',
                        'parallelism': f'ep{world}', 'transport': transport},
             'roofline': roofline, 'cpu_baseline': cpu_baseline, 'cpu_torch': cpu_torch, 'loopback': loopback,
-            'phases': phases, 'rccl': rccl, 'xgmi': xgmi,
+            'phases': phases, 'rccl': rccl, 'xgmi': xgmi, 'single_reduction': single,
             'dispatch': dispatch,
         }
         print(json.dumps(line), flush=True)

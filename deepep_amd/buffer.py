@@ -17,6 +17,7 @@ semantics (csrc/elastic/buffer.hpp:526-584) and the same error behaviour
 Single node only: num_scaleout_ranks == 1 (hybrid RDMA mode, Engram, PP and AGRS
 are out of scope for this build).
 """
+import itertools
 import math
 import os
 from typing import List, Optional, Sequence, Tuple, Union
@@ -33,6 +34,7 @@ from .utils import align, ceil_div, value_or
 topk_idx_t = torch.int32 if int(os.environ.get('EP_NUM_TOPK_IDX_BITS', 64)) == 32 else torch.int64
 
 BUFFER_ALIGNMENT = 2 * 1024 * 1024          # symmetric::kNumAlignmentBytes (symmetric.hpp:16)
+_WINDOW_IDS = itertools.count(1)            # symmetric windows created by this process
 _TOKEN_ALIGN = 32                           # ptx::kNumTMAAlignBytes (ptx.cuh:16)
 
 
@@ -626,19 +628,40 @@ class ElasticBuffer:
 
     # ------------------------------------------------------------------ EP > 1 over xGMI windows
     def _window(self, row_bytes: int):
-        """The symmetric window, sized for min(R, K) receive slots x T_max rows (buffer.hpp:616-633);
-        allocated on first use (collective: every rank reaches the same combine)."""
+        """The symmetric window: `num_bytes` (the reference's symmetric buffer size, buffer.hpp:589-686,
+        which holds every combine layout of the declared shape: min(R, K) or K receive slots x T_max
+        rows) or more if a call needs it; allocated on first use (collective: every rank reaches the
+        same combine)."""
         slots = self._window_slots
         need = slots * self.num_max_tokens_per_rank * row_bytes
         if self._sym is not None and self._sym.data_bytes >= need:
             return self._sym
         from .symmetric import SymmetricBuffer
-        if self._sym is not None:
-            self._group_barrier()
-            self._sym.destroy()
-        self._sym = SymmetricBuffer(self.group, self.rank_idx, self.num_ranks, need, self.device,
-                                    exchange=self._sym_exchange, timeout_s=self.num_gpu_timeout_secs)
+        old = self._sym
+        if old is not None:
+            self._group_barrier()                 # no rank still uses the old window
+        # the new window is allocated (and exported) before the old one is freed: exporting an
+        # allocation that reuses a freed, previously exported address fails (hipIpcGetMemHandle)
+        self._sym = SymmetricBuffer(self.group, self.rank_idx, self.num_ranks, max(need, self.num_bytes),
+                                    self.device, exchange=self._sym_exchange, timeout_s=self.num_gpu_timeout_secs)
+        if old is not None:
+            old.destroy()
+        # plans cache peer row addresses: they are valid for this window only (a process-unique id,
+        # since one handle may serve several buffers)
+        if getattr(self, '_sym_gen', None) is not None:
+            self._old_sym_gens.add(self._sym_gen)
+        else:
+            self._old_sym_gens = set()
+        self._sym_gen = next(_WINDOW_IDS)
         return self._sym
+
+    def _window_plan(self, handle: EPHandle, key: tuple):
+        """The handle's cached xGMI plan for `key` under the current window, dropping plans that
+        address an earlier (freed) window."""
+        stale = [k for k in handle._combine_plans if k[0] in ('xgmi', 'xgmi-single') and k[-1] in self._old_sym_gens]
+        for k in stale:
+            del handle._combine_plans[k]
+        return handle._combine_plans.get(key + (self._sym_gen,))
 
     def _combine_xgmi(self, handle, x, expanded, row_w, wsrc, K, hidden, bias_0, bias_1, topk_weights,
                       combined_x, combined_w, previous_event_before_epilogue, stream) -> None:
@@ -658,7 +681,7 @@ class ElasticBuffer:
         sym = self._window(row_bytes)
         num_chunks = min(self._num_chunks(handle), 63)
         key = ('xgmi', R, row_bytes, num_chunks)
-        plan = handle._combine_plans.get(key)
+        plan = self._window_plan(handle, key)
         if plan is None:
             plan = CombinePlan(num_ranks=R, num_tokens=T, num_topk=K, expanded=expanded)
             meta = handle.recv_src_metadata
@@ -693,7 +716,7 @@ class ElasticBuffer:
                                              table_b[lo:hi], row_of_lane[lo:hi]))
                 plan.chunks[-1].out_rows = out_rows[rows].contiguous()
             plan.window_row_bytes = row_bytes
-            handle._combine_plans[key] = plan
+            handle._combine_plans[key + (self._sym_gen,)] = plan
         kern = self.kernels
         w_off = align(hidden * 2, 16)
         n_rows = self._window_slots * T_max
@@ -736,6 +759,100 @@ class ElasticBuffer:
             self._mark(sb)
         if pipelined:
             stream.wait_stream(stream_b)
+
+    def _combine_xgmi_single(self, handle, x, row_w, wsrc, K, hidden, bias_0, bias_1, topk_weights,
+                             combined_x, combined_w, previous_event_before_epilogue, stream) -> None:
+        """Single-reduction combine over the symmetric windows (kDoExpandedSend, combine.cuh:177-213):
+        every valid expanded row of (token t, lane k) is copied unreduced -- with its gating weight in
+        a 16-byte tail when weights are given -- straight into the source rank's window row
+        k * T_max + t (per-top-k slot layout, buffer.hpp:616-633), then one EPILOGUE reduce per token
+        over its K rows (weighted: the legacy low-latency fma chain).  Chunked by source token like
+        _combine_xgmi, phase B of chunk c behind the split barrier of chunk c."""
+        R, r = self.num_ranks, self.rank_idx
+        T_max = handle.num_max_tokens_per_rank
+        T = handle.topk_idx.shape[0]
+        with_w = topk_weights is not None
+        self._window_slots = K
+        w_off = align(hidden * 2, 16)
+        row_bytes = w_off + 16                # the weight tail is always reserved: one window size per buffer
+        sym = self._window(row_bytes)
+        num_chunks = min(self._num_chunks(handle), 63)
+        key = ('xgmi-single', R, row_bytes, num_chunks)
+        plan = self._window_plan(handle, key)
+        if plan is None:
+            plan = CombinePlan(num_ranks=R, num_tokens=T, num_topk=K, expanded=True)
+            meta = handle.recv_src_metadata
+            recv_counts = handle._recv_counts
+            if recv_counts is None:
+                psum = [0] + [int(v) for v in handle.psum_num_recv_tokens_per_scaleup_rank.tolist()]
+                recv_counts = [psum[i + 1] - psum[i] for i in range(R)]
+            m = meta[:sum(recv_counts)].to(torch.int64)
+            slots = m[:, 2:]
+            i_idx, k_idx = (slots >= 0).nonzero(as_tuple=True)           # every valid (received token, lane)
+            rows_exp = slots[i_idx, k_idx]
+            src_rank = torch.div(m[i_idx, 1], K, rounding_mode='floor')
+            src_tok = m[i_idx, 0] % T_max
+            out_rows = sym.data_bases_dev[src_rank] + (k_idx * T_max + src_tok) * row_bytes
+            k_all = torch.arange(K, device=handle.topk_idx.device).view(1, K)
+            t_all = torch.arange(T, device=handle.topk_idx.device).view(T, 1)
+            table_b = torch.where(handle.topk_idx >= 0, k_all * T_max + t_all, torch.full_like(handle.topk_idx, -1))
+            table_b = table_b.to(torch.int32).contiguous()
+            B = (T_max + num_chunks - 1) // num_chunks
+            chunk_of = torch.div(src_tok, B, rounding_mode='floor')
+            plan.chunks = []
+            for c in range(num_chunks):
+                sel = (chunk_of == c).nonzero().view(-1)
+                lo, hi = c * B, min((c + 1) * B, T)
+                ch = ChunkPlan(lo, max(lo, hi), rows_exp[sel].to(torch.int32).view(-1, 1).contiguous(), None, [], [],
+                               table_b[lo:hi], table_b[lo:hi])
+                ch.out_rows = out_rows[sel].contiguous()
+                plan.chunks.append(ch)
+            plan.window_row_bytes = row_bytes
+            handle._combine_plans[key + (self._sym_gen,)] = plan
+        kern = self.kernels
+        n_rows = K * T_max
+        win = sym.data[:n_rows * row_bytes]
+        rows = win.view(torch.bfloat16).view(n_rows, row_bytes // 2)
+        win_w = win.view(torch.float32).view(K, T_max, row_bytes // 4)[:, :, w_off // 4] if with_w else None
+        recv_w = torch.empty((K, T_max), dtype=torch.float32, device=x.device) if with_w else None
+        pipelined = len(plan.chunks) > 1
+        sym.barrier(stream)                               # peers finished reading their windows
+        if pipelined:
+            if getattr(self, '_stream_b', None) is None:
+                self._stream_b = torch.cuda.Stream(device=self.device)
+            stream_b = self._stream_b
+            stream_b.wait_stream(stream)
+        for c, ch in enumerate(plan.chunks):
+            self._mark(stream)
+            kern.combine_reduce_scatter(x, ch.out_rows.shape[0], ch.out_rows, table=ch.table_a,
+                                        wtable=ch.table_a if with_w else None, wsrc=wsrc if with_w else None,
+                                        num_weights=1 if with_w else 0, weights_offset=w_off, stream=stream)
+            self._mark(stream)
+            sym.signal(1 + c, stream)
+        self._before_epilogue(previous_event_before_epilogue)
+        sb = stream_b if pipelined else stream
+        if pipelined and previous_event_before_epilogue is not None:
+            previous_event_before_epilogue.stream_wait(stream_b)
+        for c, ch in enumerate(plan.chunks):
+            sym.wait(1 + c, sb)
+            lo, hi = ch.lo, ch.hi
+            rw = None
+            if with_w:
+                with torch.cuda.stream(sb):
+                    recv_w[:, lo:hi].copy_(win_w[:, lo:hi])      # the chunk's weights out of the row tails
+                rw = recv_w.view(-1)
+            self._mark(sb)
+            kern.combine_reduce(MODE_EPILOGUE, rows[:, :hidden], combined_x[lo:hi], hi - lo, table=ch.table_b,
+                                row_weights=rw if row_w is not None else None,
+                                bias0=bias_0[lo:hi] if bias_0 is not None else None,
+                                bias1=bias_1[lo:hi] if bias_1 is not None else None,
+                                wtable=ch.table_b if with_w else None, wsrc=rw,
+                                out_weights=combined_w[lo:hi] if combined_w is not None else None, stream=sb)
+            self._mark(sb)
+        if pipelined:
+            stream.wait_stream(stream_b)
+            if recv_w is not None:
+                recv_w.record_stream(stream_b)
 
     def combine(self,
                 x: torch.Tensor,
@@ -817,7 +934,7 @@ class ElasticBuffer:
             compute_stream = self._prologue(previous_event, allocate_on_comm_stream)
             stream = self.comm_stream
         with (self._null_ctx() if sync_mode else self._stream_ctx()):
-            use_xgmi = R > 1 and not single_reduction and self.transport == 'xgmi' and self.use_cuda
+            use_xgmi = R > 1 and self.transport == 'xgmi' and self.use_cuda
             num_chunks = self._num_chunks(handle) if not single_reduction else 1
             plan = None if use_xgmi else self._plan(handle, single_reduction, num_chunks)
             combined_x = torch.empty((T, hidden), dtype=x.dtype, device=x.device)
@@ -835,6 +952,9 @@ class ElasticBuffer:
                     kern.combine_reduce(MODE_FUSED, x, combined_x, T, table=plan.local_table, row_weights=row_w,
                                         bias0=bias_0, bias1=bias_1, wtable=wtable, wsrc=wsrc,
                                         out_weights=combined_w, stream=stream)
+            elif single_reduction and use_xgmi:
+                self._combine_xgmi_single(handle, x, row_w, wsrc, K, hidden, bias_0, bias_1, topk_weights,
+                                          combined_x, combined_w, previous_event_before_epilogue, stream)
             elif single_reduction:
                 # every valid expanded row travels unreduced (kDoExpandedSend, combine.cuh:177-213);
                 # weighted: with its gating weight in a 16-byte row tail, applied by the one reduction
@@ -842,17 +962,21 @@ class ElasticBuffer:
                 w_elems = 8 if row_w is not None else 0
                 send = torch.empty((n_send, hidden + w_elems), dtype=x.dtype, device=x.device)
                 send_w = send[:, hidden:].view(torch.float32)[:, :1] if w_elems else None
+                self._mark(stream)
                 kern.combine_reduce(MODE_LOCAL, x, send[:, :hidden], n_send, table=plan.send_slots1,
                                     wtable=plan.send_slots1 if w_elems else None, wsrc=wsrc if w_elems else None,
                                     out_weights=send_w, stream=stream)
+                self._mark(stream)
                 recv = torch.empty((sum(plan.back_counts1), hidden + w_elems), dtype=x.dtype, device=x.device)
                 self._all_to_all(recv, send, plan.back_counts1, plan.send_counts1)
                 self._before_epilogue(previous_event_before_epilogue)
                 recv_w = recv[:, hidden:].view(torch.float32)[:, 0].contiguous() if w_elems else None
+                self._mark(stream)
                 kern.combine_reduce(MODE_EPILOGUE, recv[:, :hidden], combined_x, T, table=plan.table_b1,
                                     row_weights=recv_w, bias0=bias_0, bias1=bias_1,
                                     wtable=plan.table_b1 if w_elems else None, wsrc=recv_w, out_weights=combined_w,
                                     stream=stream)
+                self._mark(stream)
             elif use_xgmi:
                 self._combine_xgmi(handle, x, expanded, row_w, wsrc, K, hidden, bias_0, bias_1, topk_weights,
                                    combined_x, combined_w, previous_event_before_epilogue, stream)

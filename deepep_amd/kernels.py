@@ -95,8 +95,8 @@ class HipKernels:
             _require(out_weights.shape[0] >= num_units, 'weight output has fewer rows than units')
             num_weights = out_weights.shape[1]
             ow_stride = out_weights.stride(0)
-            _require(wsrc is not None and wsrc.dtype == torch.float32 and wsrc.dim() == 1 and wsrc.stride(0) == 1,
-                     'weight source must be a 1-D float32 view')
+            _require(wsrc is not None and wsrc.dtype == torch.float32 and wsrc.dim() == 1 and
+                     (wsrc.stride(0) == 1 or wsrc.numel() == 0), 'weight source must be a 1-D float32 view')
         weighted = row_weights is not None
         if weighted:
             _require(row_weights.dtype == torch.float32 and row_weights.is_contiguous(),

@@ -42,6 +42,8 @@ def _weighted_single(y_u16: np.ndarray, idx: torch.Tensor, w: torch.Tensor, bias
     the legacy low-latency fma chain over the valid top-k rows (oracle_combine_rows, mode 1 weighted)."""
     from tests.oracle_kernels import OracleKernels
     T, K, H = y_u16.shape
+    if T == 0:
+        return torch.empty((0, H), dtype=torch.bfloat16)
     src = _u16_to_bf16(y_u16.reshape(T * K, H))
     table = torch.where(idx >= 0, torch.arange(T * K).view(T, K), torch.full((T, K), -1)).to(torch.int32)
     b0, b1 = (None, None) if bias is None else ((bias, None) if isinstance(bias, torch.Tensor) else bias)

@@ -115,6 +115,63 @@ def _worker(rank, world, port, seed, T, H, K, queue, empty_rank=-1, chunks=0):
             failures.append('non-expanded: xgmi != rccl')
         if not torch.equal(o['xgmi'][1].cpu(), torch.from_numpy(w_all[rank])):
             failures.append('non-expanded: weight pass-through')
+        # allow_multiple_reduction=False: every expanded row pushed unreduced into the source rank's
+        # window (per-top-k slots), one reduction there -- plain vs the reference oracle, gating-weighted
+        # vs the legacy low-latency fma chain (bias in front); both transports
+        from tests.test_buffer_cpu import _weighted_single
+        sbufs = {}
+        # num_bytes just fits the multiple-reduction layout, so the single reduction's K-slot window
+        # forces a re-allocation (where K > min(R, K))
+        mb = 2 << 20
+        multi_bytes = min(world, K) * T * ((2 * H + 15) // 16 * 16 + (4 * K + 15) // 16 * 16)
+        for transport in ('xgmi', 'rccl'):
+            os.environ['DEEPEP_TRANSPORT'] = transport
+            sbufs[transport] = ElasticBuffer(dist.group.WORLD, num_bytes=(multi_bytes + mb - 1) // mb * mb,
+                                             num_max_tokens_per_rank=T, hidden=H, num_topk=K,
+                                             allow_multiple_reduction=False, explicitly_destroy=True,
+                                             num_gpu_timeout_secs=5)
+        # the non-expanded handle takes the multiple-reduction path on this buffer too: its window
+        # (min(R, K) slots) is outgrown by the expanded single reduction's (K slots) below, so the
+        # buffer re-allocates and plans addressing the old window must not be reused
+        nb_bias = _bf16(b_all[rank], dev)
+
+        def non_expanded_check(tag):
+            r = sbufs['xgmi'].combine(x_red, nh, topk_weights=recv_w, bias=nb_bias)
+            if not (torch.equal(r[0], o['rccl'][0]) and torch.equal(r[1], o['rccl'][1])):
+                failures.append(f'non-expanded on the single-reduction buffer ({tag})')
+        non_expanded_check('before')
+        for nb in (0, 1):
+            expect = oracle.combine_ep(x_exp_all, [d['src_metadata'] for d in disp], idx_all, E, T, expanded=True,
+                                       allow_multiple_reduction=False,
+                                       bias_per_rank=[(b if nb else None, None) for b in b_all])
+            bias = _bf16(b_all[rank], dev) if nb else None
+            bias_cpu = torch.from_numpy(b_all[rank].view(np.int16)).view(torch.bfloat16) if nb else None
+            exp_w = _weighted_single(y_all[rank], torch.from_numpy(idx_all[rank]), torch.from_numpy(w_all[rank]),
+                                     bias_cpu)
+            for it in range(2):
+                for transport, b in sbufs.items():
+                    out, out_w, _ = b.combine(_bf16(x_exp_all[rank], dev), handle, bias=bias)
+                    torch.cuda.current_stream().synchronize()
+                    if not np.array_equal(_u16(out), expect[rank][0]) or out_w is not None:
+                        failures.append(f'{transport} single-reduction (bias {nb}, call {it})')
+                    out, out_w, _ = b.combine(_bf16(x_exp_all[rank], dev), handle, topk_weights=ex_w, bias=bias,
+                                              apply_topk_weights=True)
+                    torch.cuda.current_stream().synchronize()
+                    if os.environ.get('DEEPEP_TEST_TRACE'):
+                        flag = int(b._sym.error_flag.item()) if b._sym is not None else -1
+                        print(f'rank {rank} {transport} nb={nb} it={it} flag={flag} epoch='
+                              f'{b._sym.epoch if b._sym is not None else -1}', file=sys.stderr, flush=True)
+                    if not torch.equal(out.cpu(), exp_w):
+                        failures.append(f'{transport} single-reduction weighted (bias {nb}, call {it})')
+                    if not np.array_equal(out_w.cpu().numpy(), w_all[rank]):
+                        failures.append(f'{transport} single-reduction weighted pass-through (bias {nb}, call {it})')
+        non_expanded_check('after re-allocation')
+        if sbufs['xgmi']._sym is None:
+            failures.append('xgmi single-reduction transport did not create its window')
+        else:
+            sbufs['xgmi']._sym.check()
+        for b in sbufs.values():
+            b.destroy()
         if bufs['xgmi']._sym is None:
             failures.append('xgmi transport did not create its window')
         else:
@@ -144,11 +201,14 @@ def test_xgmi_transport_matches_oracle(world, T, H, K, empty_rank, chunks):
     results = {}
     try:
         for _ in range(world):
-            rank, failures = queue.get(timeout=300)
+            rank, failures = queue.get(timeout=150)
             results[rank] = failures
     finally:
         for p in procs:
             p.join(timeout=60)
             if p.is_alive():
                 p.kill()
-    assert len(results) == world and not any(results.values()), results
+    if len(results) != world or any(results.values()):
+        # the root cause is usually one rank's exception; its peers then fail with a closed connection
+        tails = {r: [f[-1500:] for f in fl] for r, fl in results.items()}
+        pytest.fail(f'{len(results)}/{world} ranks reported; failures: {tails}', pytrace=False)

@@ -18,7 +18,7 @@ run() {   # run <name> <timeout> <cmd...>
 }
 for step in "$@"; do
     case $step in
-        tests)  run pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
+        tests)  run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 170 --timeout-method thread ;;
         smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench)  run bench 600 python bench.py ;;
         benchplain) run bench_plain 600 python bench.py --plain --no-cpu-baseline --no-loopback ;;

@@ -288,7 +288,7 @@ def main():
 
     rank, world = _init_dist(args.gpus)
     from deepep_amd import ElasticBuffer
-    from deepep_amd.kernels import MODE_FUSED
+    from deepep_amd.kernels import MODE_EPILOGUE, MODE_FUSED
     T, H, K, E = args.tokens, args.hidden, args.topk, args.experts
     weighted = not args.plain
     dev = torch.device('cuda', torch.cuda.current_device())
@@ -377,12 +377,39 @@ def main():
         torch.cuda.synchronize()
         copy_gbps = 2 * y.numel() * 2 * 5 / (c0.elapsed_time(c1) * 1e-3) / 1e9
         del dst
+        # The reduce phase of the EP > 1 single-reduction combine (allow_multiple_reduction=False): after
+        # the exchange a rank's receive window holds its tokens' K unreduced rows at k * T_max + t (rows
+        # of 2H + 16 bytes, weight in the tail); one weighted EPILOGUE launch reduces them.  Same
+        # algorithmic bytes per token; what every rank runs at N GPUs once the rows have landed.
+        row_e = H + 8
+        win = torch.randn((K * T, row_e), device=dev).to(torch.bfloat16)
+        win_w = torch.rand((K * T,), device=dev)
+        kk = torch.arange(K, device=dev).view(1, K)
+        tt = torch.arange(T, device=dev).view(T, 1)
+        tab_b = torch.where(topk_idx >= 0, kk * T + tt, torch.full_like(topk_idx, -1)).to(torch.int32).contiguous()
+
+        def launch_b():
+            kern.combine_reduce(MODE_EPILOGUE, win[:, :H], out, T, table=tab_b, row_weights=win_w if weighted else None,
+                                wtable=tab_b, wsrc=win_w, out_weights=out_w, stream=stream)
+        for _ in range(5):
+            launch_b()
+        k0.record(stream)
+        for _ in range(args.steps):
+            launch_b()
+        k1.record(stream)
+        torch.cuda.synchronize()
+        b_us = k0.elapsed_time(k1) * 1e3 / args.steps
+        single_b = dict(kernel_us=round(b_us, 2), gbps=round(bytes_rank / (b_us * 1e-6) / 1e9, 1),
+                        frac=round(bytes_rank / (b_us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4),
+                        note='reduce phase of the EP > 1 single-reduction combine (one weighted EPILOGUE launch over '
+                             'the K unreduced rows per token in a [K, T] receive window), same algorithmic bytes')
+        del win, win_w
         workload = f'combine_fused_{"weighted" if weighted else "plain"}_t{T}_h{H}_k{K}'
         roofline = dict(bound='hbm', achieved=round(achieved, 1), peak=HBM_PEAK_GBPS, unit='GB/s',
                         frac=round(achieved / HBM_PEAK_GBPS, 4), traffic=_pmc_traffic(workload),
                         kernel='combine_rows_kernel<FUSED>', kernel_us=round(kern_us, 2),
                         bytes_per_launch=bytes_rank, in_region_us_per_step=round(comm_ms * 1e3, 2),
-                        same_run_d2d_copy_gbps=round(copy_gbps, 1))
+                        same_run_d2d_copy_gbps=round(copy_gbps, 1), single_reduction_phase_b=single_b)
 
     phases = None
     if world > 1:
@@ -424,7 +451,7 @@ def main():
     # host syncs (received-token counts), as the reference's dispatch with do_cpu_sync=True.
     torch.cuda.synchronize()
     dist.barrier()
-    n_disp = 10
+    n_disp = 50
     x_disp = torch.randn((T, H), device=dev).to(torch.bfloat16)
     if args.fp8_dispatch:
         from deepep_amd.utils import per_token_cast_to_fp8

@@ -35,7 +35,6 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kMaxWidth = 32;          // top-k <= 32, as the reference (combine_reduce_epilogue.cuh:64)
-constexpr int kGroup = 8;              // source rows in flight per lane per group
 
 thread_local char g_last_error[512] = "";
 
@@ -139,7 +138,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void* row, int 
 // (and its gating weights) is staged once per workgroup in LDS (kLDS) or per wave in registers,
 // one entry per lane; the valid slots are then visited in ascending order through the ballot mask,
 // which is exactly the compacted order of compute_topk_slots (combine_utils.cuh:41-53).
-template <int kMode, bool kWeighted, int kVPT, bool kFull, int kStoreAux, bool kLDS, int kWaves = 4>
+template <int kMode, bool kWeighted, int kVPT, bool kFull, int kStoreAux, bool kLDS, int kWaves = 4, int kGroup = 8>
 __global__ void __launch_bounds__(64 * kWaves)
 combine_rows_kernel(const Params p) {
     constexpr int kChunkVecs = 64 * kVPT;
@@ -241,15 +240,23 @@ combine_rows_kernel(const Params p) {
         }
     }
 
+    // The valid lanes, lowest first, kGroup at a time: every row of a group is loaded before any is
+    // accumulated (kGroup rows x kVPT x 16 B in flight per lane), and the accumulation order is the
+    // ascending lane order of compute_topk_slots whatever the group size.  `rem` is wave-uniform.
     u32x4 result[kVPT];
-    for (int g = 0; g < width; g += kGroup) {
-        const uint32_t gmask = static_cast<uint32_t>(valid >> g) & 0xffu;
-        if (gmask == 0u) continue;
+    uint64_t rem = valid;
+    while (rem != 0ull) {
+        int lane_of[kGroup];
+#pragma unroll
+        for (int j = 0; j < kGroup; ++j) {
+            lane_of[j] = rem != 0ull ? static_cast<int>(__builtin_ctzll(rem)) : -1;
+            rem &= rem - 1ull;                              // (no-op once empty)
+        }
         u32x4 vals[kGroup][kVPT];
 #pragma unroll
         for (int j = 0; j < kGroup; ++j) {
-            if (gmask & (1u << j)) {
-                const int32_t sj = __builtin_amdgcn_readlane(my_slot, g + j);
+            if (lane_of[j] >= 0) {
+                const int32_t sj = __builtin_amdgcn_readlane(my_slot, lane_of[j]);
                 const u32x4* row = reinterpret_cast<const u32x4*>(p.src + static_cast<int64_t>(sj) * p.src_stride);
 #pragma unroll
                 for (int v = 0; v < kVPT; ++v)
@@ -258,16 +265,13 @@ combine_rows_kernel(const Params p) {
         }
         if (copy_row) {
 #pragma unroll
-            for (int j = 0; j < kGroup; ++j)
-                if (gmask & (1u << j))
-#pragma unroll
-                    for (int v = 0; v < kVPT; ++v) result[v] = vals[j][v];
+            for (int v = 0; v < kVPT; ++v) result[v] = vals[0][v];        // n == 1: lane_of[0] is it
         } else {
 #pragma unroll
             for (int j = 0; j < kGroup; ++j) {
-                if (gmask & (1u << j)) {
+                if (lane_of[j] >= 0) {
                     if constexpr (kWeighted) {
-                        const float w = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_w), g + j));
+                        const float w = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_w), lane_of[j]));
 #pragma unroll
                         for (int v = 0; v < kVPT; ++v) acc_fma(acc[v], vals[j][v], w);
                     } else {
@@ -310,43 +314,64 @@ struct LaunchConfig {
     int vec_per_lane = 0;        // 0: auto (16-byte vectors per lane per source row and item)
     int stage_lds = -1;          // -1: auto (1 = LDS staging per workgroup, 0 = per-wave registers)
     int store_policy = -1;       // -1: auto (0 plain, 1 nt, 2 sc1)
+    int rows_in_flight = 0;      // 0: auto (source rows loaded per lane before accumulating: 2, 4 or 8)
 };
 LaunchConfig g_config;
 
+template <int kMode, bool kWeighted, int kVPT, bool kFull, int kAux, bool kLDS, int kWaves, int kGroup>
+void launch_shape(const Params& p, int64_t items, hipStream_t stream) {
+    const dim3 grid(static_cast<unsigned>((items + kWaves - 1) / kWaves)), block(64 * kWaves);
+    hipLaunchKernelGGL((combine_rows_kernel<kMode, kWeighted, kVPT, kFull, kAux, kLDS, kWaves, kGroup>), grid, block,
+                       0, stream, p);
+}
+
+// Workgroup shape and rows in flight.  The fused / epilogue reduces (8 rows per token at EP = 1):
+// 8 waves x 8 rows in flight (measured on two boxes: 157.5-159.7 us vs 159.6-161.1 us with 4 waves,
+// 169 us with 16, 180 us with 12).  Phase A of EP > 1 (1.5 local rows per received token at EP = 8)
+// gains from occupancy instead: see launch_combine for the automatic choice.
 template <int kMode, bool kWeighted, int kVPT, bool kFull, int kAux>
-void launch_lds(const Params& p, bool lds, hipStream_t stream) {
+void launch_lds(const Params& p, bool lds, int waves, int group, hipStream_t stream) {
     const int nvec = p.hidden / 8;
     const int64_t items = static_cast<int64_t>(p.num_units) * ((nvec + 64 * kVPT - 1) / (64 * kVPT));
     if constexpr (kAux == kAuxSC1) {
-        // Default shape: 8 waves (512 threads) per workgroup, 8 consecutive items.  Measured on two
-        // boxes: 157.5-159.7 us vs 159.6-161.1 us with 4 waves, 169 us with 16, 180 us with 12.
-        if (lds && p.units_per_block != 4) {
-            const dim3 grid(static_cast<unsigned>((items + 7) / 8)), block(512);
-            hipLaunchKernelGGL((combine_rows_kernel<kMode, kWeighted, kVPT, kFull, kAux, true, 8>), grid, block, 0, stream, p);
+        if (lds) {
+            if (waves == 8) {
+                if (group == 2) launch_shape<kMode, kWeighted, kVPT, kFull, kAux, true, 8, 2>(p, items, stream);
+                else if (group == 4) launch_shape<kMode, kWeighted, kVPT, kFull, kAux, true, 8, 4>(p, items, stream);
+                else launch_shape<kMode, kWeighted, kVPT, kFull, kAux, true, 8, 8>(p, items, stream);
+            } else {
+                if (group == 2) launch_shape<kMode, kWeighted, kVPT, kFull, kAux, true, 4, 2>(p, items, stream);
+                else if (group == 4) launch_shape<kMode, kWeighted, kVPT, kFull, kAux, true, 4, 4>(p, items, stream);
+                else launch_shape<kMode, kWeighted, kVPT, kFull, kAux, true, 4, 8>(p, items, stream);
+            }
             return;
         }
     }
-    const dim3 grid(static_cast<unsigned>((items + 3) / 4)), block(256);
-    if (lds) hipLaunchKernelGGL((combine_rows_kernel<kMode, kWeighted, kVPT, kFull, kAux, true>), grid, block, 0, stream, p);
-    else hipLaunchKernelGGL((combine_rows_kernel<kMode, kWeighted, kVPT, kFull, kAux, false>), grid, block, 0, stream, p);
+    if (lds) launch_shape<kMode, kWeighted, kVPT, kFull, kAux, true, 4, 8>(p, items, stream);
+    else launch_shape<kMode, kWeighted, kVPT, kFull, kAux, false, 4, 8>(p, items, stream);
 }
 
+struct Shape {
+    int vpt, policy, waves, group;
+    bool lds;
+};
+
 template <int kMode, bool kWeighted, int kVPT, bool kFull>
-void launch_aux(const Params& p, bool lds, int policy, hipStream_t stream) {
-    if (policy == 0) launch_lds<kMode, kWeighted, kVPT, kFull, 0>(p, lds, stream);
-    else if (policy == 1) launch_lds<kMode, kWeighted, kVPT, kFull, kAuxNT>(p, lds, stream);
-    else launch_lds<kMode, kWeighted, kVPT, kFull, kAuxSC1>(p, lds, stream);
+void launch_aux(const Params& p, const Shape& sh, hipStream_t stream) {
+    if (sh.policy == 0) launch_lds<kMode, kWeighted, kVPT, kFull, 0>(p, sh.lds, sh.waves, sh.group, stream);
+    else if (sh.policy == 1) launch_lds<kMode, kWeighted, kVPT, kFull, kAuxNT>(p, sh.lds, sh.waves, sh.group, stream);
+    else launch_lds<kMode, kWeighted, kVPT, kFull, kAuxSC1>(p, sh.lds, sh.waves, sh.group, stream);
 }
 
 template <int kMode, bool kWeighted>
-void launch_vpt(const Params& p, int vpt, bool lds, int policy, hipStream_t stream) {
+void launch_vpt(const Params& p, const Shape& sh, hipStream_t stream) {
     const int nvec = p.hidden / 8;
-    if (vpt == 1) {
-        if (nvec % 64 == 0) launch_aux<kMode, kWeighted, 1, true>(p, lds, policy, stream);
-        else launch_aux<kMode, kWeighted, 1, false>(p, lds, policy, stream);
+    if (sh.vpt == 1) {
+        if (nvec % 64 == 0) launch_aux<kMode, kWeighted, 1, true>(p, sh, stream);
+        else launch_aux<kMode, kWeighted, 1, false>(p, sh, stream);
     } else {
-        if (nvec % 128 == 0) launch_aux<kMode, kWeighted, 2, true>(p, lds, policy, stream);
-        else launch_aux<kMode, kWeighted, 2, false>(p, lds, policy, stream);
+        if (nvec % 128 == 0) launch_aux<kMode, kWeighted, 2, true>(p, sh, stream);
+        else launch_aux<kMode, kWeighted, 2, false>(p, sh, stream);
     }
 }
 
@@ -515,23 +540,27 @@ int deepep_combine_reduce_scatter(int weighted,
 namespace {
 
 int launch_combine(int mode, int weighted, const Params& p, deepep_stream_t stream) {
-    // Launch shape: one wave per (unit, 64 x vpt x 16-byte column chunk) item, 4 items per
-    // workgroup; at hidden 7168 a token is 7 items of 2 KiB per source row.
+    // Launch shape: one wave per (unit, 64 x vpt x 16-byte column chunk) item; at hidden 7168 a
+    // token is 7 items of 2 KiB per source row.
     const int nvec = p.hidden / 8;
-    int vpt = g_config.vec_per_lane > 0 ? g_config.vec_per_lane : (nvec >= 128 ? 2 : 1);
-    if (vpt != 1 && vpt != 2) vpt = 2;
-    const bool lds = g_config.stage_lds >= 0 ? g_config.stage_lds != 0 : true;
-    const int policy = g_config.store_policy >= 0 ? g_config.store_policy : 2;
+    Shape sh;
+    sh.vpt = g_config.vec_per_lane > 0 ? g_config.vec_per_lane : (nvec >= 128 ? 2 : 1);
+    if (sh.vpt != 1 && sh.vpt != 2) sh.vpt = 2;
+    sh.lds = g_config.stage_lds >= 0 ? g_config.stage_lds != 0 : true;
+    sh.policy = g_config.store_policy >= 0 ? g_config.store_policy : 2;
+    // units_per_block 4 / 8 forces the workgroup shape; 0 = automatic
+    sh.waves = p.units_per_block == 4 ? 4 : (p.units_per_block == 8 ? 8 : (mode == DEEPEP_MODE_LOCAL ? 4 : 8));
+    sh.group = g_config.rows_in_flight > 0 ? g_config.rows_in_flight : 8;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (mode == DEEPEP_MODE_LOCAL) {
-        if (weighted) launch_vpt<DEEPEP_MODE_LOCAL, true>(p, vpt, lds, policy, s);
-        else launch_vpt<DEEPEP_MODE_LOCAL, false>(p, vpt, lds, policy, s);
+        if (weighted) launch_vpt<DEEPEP_MODE_LOCAL, true>(p, sh, s);
+        else launch_vpt<DEEPEP_MODE_LOCAL, false>(p, sh, s);
     } else if (mode == DEEPEP_MODE_EPILOGUE) {
-        if (weighted) launch_vpt<DEEPEP_MODE_EPILOGUE, true>(p, vpt, lds, policy, s);
-        else launch_vpt<DEEPEP_MODE_EPILOGUE, false>(p, vpt, lds, policy, s);
+        if (weighted) launch_vpt<DEEPEP_MODE_EPILOGUE, true>(p, sh, s);
+        else launch_vpt<DEEPEP_MODE_EPILOGUE, false>(p, sh, s);
     } else {
-        if (weighted) launch_vpt<DEEPEP_MODE_FUSED, true>(p, vpt, lds, policy, s);
-        else launch_vpt<DEEPEP_MODE_FUSED, false>(p, vpt, lds, policy, s);
+        if (weighted) launch_vpt<DEEPEP_MODE_FUSED, true>(p, sh, s);
+        else launch_vpt<DEEPEP_MODE_FUSED, false>(p, sh, s);
     }
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess)
@@ -576,12 +605,14 @@ int deepep_build_local_plan(const int32_t* src_metadata, int num_recv_tokens, in
     return DEEPEP_OK;
 }
 
-int deepep_set_launch_config(int vec_per_lane, int stage_lds, int store_policy) {
-    if (vec_per_lane < 0 || vec_per_lane > 2 || stage_lds < -1 || stage_lds > 1 || store_policy < -1 || store_policy > 2)
+int deepep_set_launch_config(int vec_per_lane, int stage_lds, int store_policy, int rows_in_flight) {
+    if (vec_per_lane < 0 || vec_per_lane > 2 || stage_lds < -1 || stage_lds > 1 || store_policy < -1 ||
+        store_policy > 2 || (rows_in_flight != 0 && rows_in_flight != 2 && rows_in_flight != 4 && rows_in_flight != 8))
         return set_error(DEEPEP_ERR_INVALID_ARG, "invalid launch configuration");
     g_config.vec_per_lane = vec_per_lane;
     g_config.stage_lds = stage_lds;
     g_config.store_policy = store_policy;
+    g_config.rows_in_flight = rows_in_flight;
     return DEEPEP_OK;
 }
 

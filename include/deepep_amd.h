@@ -45,7 +45,7 @@ extern "C" {
 
 typedef struct ihipStream_t* deepep_stream_t;   /* == hipStream_t */
 
-#define DEEPEP_AMD_ABI_VERSION 4
+#define DEEPEP_AMD_ABI_VERSION 5
 
 #define DEEPEP_OK               0
 #define DEEPEP_ERR_INVALID_ARG  (-1)
@@ -81,7 +81,7 @@ const char* deepep_amd_last_error(void);
  *                                                             : u*num_weights + k) >= 0 ? wsrc[i] : 0
  *                  (a stride lets the weights ride in the tail of packed exchange rows)
  *   units_per_block  workgroup shape: 4 = 4 (row, column-chunk) items per 256-thread workgroup,
- *                  anything else = the default 8 items per 512-thread workgroup
+ *                  8 = 8 items per 512-thread workgroup, 0 = automatic (4 for LOCAL, else 8)
  *   error_flag     device int or NULL; set to 1 when a slot is >= num_src_rows
  *                  (such slots are skipped, never dereferenced)
  */
@@ -120,9 +120,10 @@ int deepep_build_local_plan(const int32_t* src_metadata, int num_recv_tokens, in
  *   vec_per_lane   16-byte vectors each lane loads per source row and item (1 or 2)
  *   stage_lds      1: stage the slot table / weights per workgroup in LDS; 0: per wave in registers
  *   store_policy   output store cache policy: 0 plain, 1 nt, 2 sc1 (write-through)
+ *   rows_in_flight source rows each lane loads before accumulating them (2, 4 or 8; sc1 + LDS only)
  * The results are identical for every configuration; only the speed changes.
  */
-int deepep_set_launch_config(int vec_per_lane, int stage_lds, int store_policy);
+int deepep_set_launch_config(int vec_per_lane, int stage_lds, int store_policy, int rows_in_flight);
 
 /* ------------------------------------------------------------------ dispatch
  * Packed token row exchanged between ranks (byte offsets, all 16-byte aligned except as noted):

@@ -123,17 +123,22 @@ def test_kernel_units_per_block(kern, upb):
     _run(kern, MODE_LOCAL, True, 53, 8, 7168, 0, seed=upb + 1, upb=upb, wt=False)
 
 
-@pytest.mark.parametrize('cfg', [(1, 0, 0), (1, 1, 1), (2, 0, 1), (2, 1, 0), (2, 0, 2), (0, -1, -1)])
-def test_kernel_launch_configs_identical(kern, cfg):
-    """Every deepep_set_launch_config variant (vector width, LDS staging, store policy) gives the
-    same bits (the tuning knobs of tools/kbench.py)."""
+@pytest.mark.parametrize('cfg', [(1, 0, 0, 0), (1, 1, 1, 0), (2, 0, 1, 0), (2, 1, 0, 0), (2, 0, 2, 0), (0, -1, -1, 0),
+                                 (0, -1, -1, 2), (0, -1, -1, 4), (1, 1, 2, 2)])
+@pytest.mark.parametrize('upb', [0, 4, 8])
+def test_kernel_launch_configs_identical(kern, cfg, upb):
+    """Every deepep_set_launch_config variant (vector width, LDS staging, store policy, rows in
+    flight) and workgroup shape gives the same bits (the tuning knobs of tools/kbench.py)."""
     assert kern.lib.deepep_set_launch_config(*cfg) == 0
     try:
         for mode in (MODE_LOCAL, MODE_EPILOGUE, MODE_FUSED):
-            _run(kern, mode, False, 29, 8, 2056, 0 if mode == MODE_LOCAL else 2, seed=sum(cfg) + 2 + mode)
-            _run(kern, mode, True, 29, 8, 7168, 0 if mode == MODE_LOCAL else 1, seed=sum(cfg) + 2 + 3 * mode)
+            _run(kern, mode, False, 29, 8, 2056, 0 if mode == MODE_LOCAL else 2, seed=sum(cfg) + 2 + mode, upb=upb)
+            _run(kern, mode, True, 29, 8, 7168, 0 if mode == MODE_LOCAL else 1, seed=sum(cfg) + 2 + 3 * mode,
+                 upb=upb)
+            _run(kern, mode, True, 29, 17, 520, 0 if mode == MODE_LOCAL else 2, seed=sum(cfg) + 10 + 5 * mode,
+                 upb=upb)                                                       # > 8 valid rows
     finally:
-        kern.lib.deepep_set_launch_config(0, -1, -1)
+        kern.lib.deepep_set_launch_config(0, -1, -1, 0)
 
 
 @pytest.mark.parametrize('weighted,hidden', [(False, 7168), (True, 520), (False, 64)])

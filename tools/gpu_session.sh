@@ -30,6 +30,7 @@ for step in "$@"; do
         pcopy)  run pcopy 600 python tools/probe_copy.py ;;
         kwaves) run kwaves 600 python tools/kbench_waves.py ;;
         kvar)   run kvar 300 python tools/kvar.py ;;
+        kphase) run kphase 300 python tools/kphase.py ;;
         pmclist) run pmclist 120 rocprofv3 --list-avail ;;
         smi)    run smi 60 rocm-smi --showclocks --showpower --showtemp ;;
         bench2gloo) export DEEPEP_BENCH_BACKEND=gloo; run bench2gloo 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29655 bench.py --gpus 2 --steps 10 --warmup 3; unset DEEPEP_BENCH_BACKEND ;;

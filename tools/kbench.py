@@ -59,7 +59,7 @@ def main():
         (0, -1, -1), (2, 1, 2), (2, 0, 2), (1, 1, 2), (1, 0, 2), (2, 1, 0), (2, 1, 1), (2, 0, 0)]
     for weighted in (True, False):
         for cfg in configs:
-            assert lib.deepep_set_launch_config(*cfg) == 0
+            assert lib.deepep_set_launch_config(*cfg, 0) == 0
             fn = lambda: buf.kernels.combine_reduce(MODE_FUSED, y, out, T, table=plan.local_table,
                                                     row_weights=ex_w if weighted else None,
                                                     wtable=plan.local_table, wsrc=ex_w, out_weights=out_w, stream=s)
@@ -67,7 +67,7 @@ def main():
             print(json.dumps(dict(variant=f'fused_{"w" if weighted else "p"}_cfg{cfg}', us=round(us, 1),
                                   gbps=round(nbytes / us / 1e3, 1), frac=round(nbytes / us / 1e3 / 8000, 4))),
                   flush=True)
-    lib.deepep_set_launch_config(0, -1, -1)
+    lib.deepep_set_launch_config(0, -1, -1, 0)
     # read-only ceiling: sum of all expanded rows (torch reduction kernel)
     us = timeit(lambda: y.sum(dtype=torch.float32), s, iters=10)
     print(json.dumps(dict(variant='torch_sum_939MB', us=round(us, 1), gbps=round(y.numel() * 2 / us / 1e3, 1))))

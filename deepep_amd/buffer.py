@@ -63,6 +63,20 @@ def calculate_buffer_size(num_ranks: int, num_max_tokens_per_rank: int, hidden: 
     return align(max(dispatch_bytes, combine_bytes), BUFFER_ALIGNMENT)
 
 
+def _interleave_by_rank(units: torch.Tensor, dest_rank: torch.Tensor, num_ranks: int) -> torch.Tensor:
+    """Reorder a phase-A launch's units (ascending, hence grouped by destination rank) round-robin
+    over the destinations: the waves in flight at any moment then store to every peer at once, so
+    all of xGMI's point-to-point links carry traffic instead of one link at a time.  Units are
+    independent, so the order changes no result."""
+    if units.numel() == 0 or num_ranks == 1:
+        return units
+    d = dest_rank[units]
+    counts = torch.bincount(d, minlength=num_ranks)
+    start = torch.cumsum(counts, 0) - counts
+    pos = torch.arange(units.numel(), device=units.device) - start[d]        # units are sorted by d
+    return units[torch.argsort(pos * num_ranks + d)]
+
+
 class ElasticBuffer:
     """The elastic EP buffer (single node): dispatch produces an EPHandle, combine reduces."""
 
@@ -701,13 +715,11 @@ class ElasticBuffer:
             chunk_of_row = torch.div(src_tok, B, rounding_mode='floor')
             plan.chunks = []
             for c in range(num_chunks):
-                rows = (chunk_of_row == c).nonzero().view(-1)
+                rows = _interleave_by_rank((chunk_of_row == c).nonzero().view(-1), src_rank, R)
                 if expanded:
                     table_a = m[rows, 2:].to(torch.int32).contiguous()
                     wtable_a = table_a
-                elif num_chunks == 1:
-                    table_a = wtable_a = None                 # received row i is unit i
-                else:
+                else:                                         # units are interleaved: explicit rows
                     table_a = rows.to(torch.int32).view(-1, 1).contiguous()
                     wtable_a = (rows.view(-1, 1) * K + torch.arange(K, device=rows.device).view(1, K)).to(
                         torch.int32).contiguous()
@@ -801,7 +813,7 @@ class ElasticBuffer:
             chunk_of = torch.div(src_tok, B, rounding_mode='floor')
             plan.chunks = []
             for c in range(num_chunks):
-                sel = (chunk_of == c).nonzero().view(-1)
+                sel = _interleave_by_rank((chunk_of == c).nonzero().view(-1), src_rank, R)
                 lo, hi = c * B, min((c + 1) * B, T)
                 ch = ChunkPlan(lo, max(lo, hi), rows_exp[sel].to(torch.int32).view(-1, 1).contiguous(), None, [], [],
                                table_b[lo:hi], table_b[lo:hi])

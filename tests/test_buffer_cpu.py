@@ -399,3 +399,15 @@ def test_rank_with_no_tokens(world):
             if p.is_alive():
                 p.kill()
     assert len(results) == world and not any(results.values()), results
+
+
+def test_interleave_by_rank_is_a_round_robin_permutation():
+    """xGMI phase-A units are reordered round-robin over destination ranks (every link busy at once)."""
+    from deepep_amd.buffer import _interleave_by_rank
+    dest = torch.tensor([0] * 5 + [1] * 2 + [3] * 4)           # per received row, grouped by rank
+    units = torch.tensor([0, 1, 2, 4, 5, 6, 7, 9, 10])          # a chunk's rows (ascending)
+    out = _interleave_by_rank(units, dest, 4)
+    assert sorted(out.tolist()) == units.tolist()
+    assert out.tolist() == [0, 5, 7, 1, 6, 9, 2, 10, 4]
+    assert _interleave_by_rank(units, dest, 1).tolist() == units.tolist()
+    assert _interleave_by_rank(units[:0], dest, 4).numel() == 0

@@ -579,7 +579,7 @@ int deepep_build_local_plan(const int32_t* src_metadata, int num_recv_tokens, in
                             deepep_stream_t stream) {
     if (num_recv_tokens < 0 || num_tokens < 0 || num_topk < 1 || num_topk > kMaxWidth || num_max_tokens_per_rank < 1)
         return set_error(DEEPEP_ERR_INVALID_ARG, "invalid plan sizes");
-    if (plan == nullptr || (num_recv_tokens > 0 && src_metadata == nullptr))
+    if ((num_tokens > 0 && plan == nullptr) || (num_recv_tokens > 0 && src_metadata == nullptr))
         return set_error(DEEPEP_ERR_INVALID_ARG, "null plan/metadata");
     if (plan_width != (expanded ? num_topk : 1))
         return set_error(DEEPEP_ERR_INVALID_ARG, "plan width must be num_topk (expanded) or 1");

@@ -74,8 +74,8 @@ class HipKernels:
                        stream=None) -> None:
         _require(src.is_cuda and out.is_cuda, 'combine tensors must be on the GPU')
         _require(src.dtype == torch.bfloat16 and out.dtype == torch.bfloat16, 'combine rows must be bfloat16')
-        _require(src.dim() == 2 and out.dim() == 2 and src.stride(1) == 1 and out.stride(1) == 1,
-                 'combine rows must be 2-D with unit column stride')
+        _require(src.dim() == 2 and out.dim() == 2 and (src.numel() == 0 or src.stride(1) == 1) and
+                 (out.numel() == 0 or out.stride(1) == 1), 'combine rows must be 2-D with unit column stride')
         hidden = out.shape[1]
         _require(src.shape[1] == hidden or src.shape[0] == 0, 'source and output hidden sizes differ')
         _require(out.shape[0] >= num_units, 'output has fewer rows than units')
@@ -121,8 +121,8 @@ class HipKernels:
                                num_weights: int = 0, weights_offset: int = 0,
                                error_flag: Optional[torch.Tensor] = None, stream=None) -> None:
         """Phase A storing unit u's row at byte address out_rows[u] (a peer window over xGMI)."""
-        _require(src.is_cuda and src.dtype == torch.bfloat16 and src.dim() == 2 and src.stride(1) == 1,
-                 'combine rows must be 2-D bf16 on the GPU with unit column stride')
+        _require(src.is_cuda and src.dtype == torch.bfloat16 and src.dim() == 2 and
+                 (src.numel() == 0 or src.stride(1) == 1), 'combine rows must be 2-D bf16 on the GPU with unit column stride')
         _require(out_rows.is_cuda and out_rows.dtype == torch.int64 and out_rows.is_contiguous() and
                  out_rows.shape[0] >= num_units, 'out_rows must be int64 [num_units] on the GPU')
         t, t_stride, t_width = _table_view(table)

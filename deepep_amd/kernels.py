@@ -96,7 +96,7 @@ class HipKernels:
             num_weights = out_weights.shape[1]
             ow_stride = out_weights.stride(0)
             _require(wsrc is not None and wsrc.dtype == torch.float32 and wsrc.dim() == 1 and
-                     (wsrc.stride(0) == 1 or wsrc.numel() == 0), 'weight source must be a 1-D float32 view')
+                     (wsrc.stride(0) == 1 or wsrc.numel() <= 1), 'weight source must be a 1-D float32 view')
         weighted = row_weights is not None
         if weighted:
             _require(row_weights.dtype == torch.float32 and row_weights.is_contiguous(),

@@ -211,8 +211,11 @@ def combine_ep(recv_x_per_rank: Sequence[np.ndarray], src_metadata_per_rank: Seq
                expanded: bool, allow_multiple_reduction: bool = True,
                topk_weights_per_rank: Optional[Sequence[np.ndarray]] = None,
                bias_per_rank: Optional[Sequence[Tuple[Optional[np.ndarray], Optional[np.ndarray]]]] = None,
+               weighted: bool = False,
                ) -> List[Tuple[np.ndarray, Optional[np.ndarray]]]:
-    """The reference combine across R ranks: phase A -> receive-slot scatter -> phase B."""
+    """The reference combine across R ranks: phase A -> receive-slot scatter -> phase B.
+    weighted: phase A scales each row by its top-k weight (legacy fma chain, this build's
+    apply_topk_weights with multiple reduction)."""
     R = len(recv_x_per_rank)
     K = topk_idx_per_rank[0].shape[1]
     hidden = recv_x_per_rank[0].shape[1]
@@ -236,7 +239,7 @@ def combine_ep(recv_x_per_rank: Sequence[np.ndarray], src_metadata_per_rank: Seq
                         recv[src_rank[i]][k, src_tok[i]] = x[slot]
             continue
         w = topk_weights_per_rank[r] if topk_weights_per_rank is not None else None
-        partial, pw = phase_a(x, meta, K, expanded, w)
+        partial, pw = phase_a(x, meta, K, expanded, w, weighted=weighted)
         for i in range(meta.shape[0]):
             slot = r if rank_layout else src_topk[i]
             recv[src_rank[i]][slot, src_tok[i]] = partial[i]

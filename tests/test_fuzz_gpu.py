@@ -111,3 +111,103 @@ def test_random_shapes_ep1(group, seed):
             if not np.array_equal(out_w.cpu().numpy(), w):
                 failures.append('non-expanded weights')
     assert not failures, (seed, T, H, K, E, masked, failures)
+
+
+def _ep_thread(rank, world, seed, comm, results):
+    """One simulated rank of a random EP = `world` case (threads on the one GPU, all-to-all by copies)."""
+    try:
+        from deepep_amd import ElasticBuffer
+        from tests.test_combine_gpu import _Done, _FakeGroup
+        torch.cuda.set_device(0)
+        rng = np.random.default_rng(seed)            # same stream in every thread: same global case
+        K = int(rng.choice([1, 2, 4, 6, 8]))
+        E = int(world * rng.integers(max(1, (K + world - 1) // world), 5))
+        H = int(rng.choice([64, 520, 2056]))
+        T = int(rng.choice([33, 96]))
+        Ts = [int(rng.integers(0, T + 1)) for _ in range(world)]
+        idx_all, w_all, y_all, b_all = [], [], [], []
+        for r in range(world):
+            idx = np.array([rng.permutation(E)[:K] for _ in range(Ts[r])], dtype=np.int64).reshape(Ts[r], K)
+            idx[rng.random((Ts[r], K)) < 0.15] = -1
+            idx_all.append(idx)
+            w_all.append((rng.random((Ts[r], K)).astype(np.float32) * (idx >= 0)).astype(np.float32))
+            y = oracle.f32_to_bf16(rng.standard_normal((Ts[r], K, H)).astype(np.float32))
+            y[idx < 0] = 0
+            y_all.append(y)
+            b_all.append(oracle.f32_to_bf16(rng.standard_normal((Ts[r], H)).astype(np.float32)))
+        disp = oracle.simulate_dispatch(idx_all, E, T)
+        x_exp_all, w_exp_all = [], []
+        for d in disp:
+            xe = np.zeros((d['num_expanded'], H), np.uint16)
+            we = np.zeros((d['num_expanded'],), np.float32)
+            for row, (g, k) in enumerate(d['expanded_src']):
+                s, t = divmod(int(g), T)
+                xe[row], we[row] = y_all[s][t, k], w_all[s][t, k]
+            x_exp_all.append(xe), w_exp_all.append(we)
+        metas = [d['src_metadata'] for d in disp]
+        grp = _FakeGroup(rank, world, comm)
+        failures = []
+        bias = _bf16(b_all[rank])
+        x = torch.zeros((Ts[rank], H), dtype=torch.bfloat16, device='cuda')
+        g_idx, g_w = torch.from_numpy(idx_all[rank]).cuda(), torch.from_numpy(w_all[rank]).cuda()
+        for amr in (True, False):
+            buf = ElasticBuffer(grp, num_max_tokens_per_rank=T, hidden=H, num_topk=K, allow_multiple_reduction=amr)
+            buf._a2a = lambda out, inp, os_=None, is_=None: comm.a2a(rank, out, inp, os_, is_)
+            buf._a2a_async = lambda out, inp, os_, is_: (comm.a2a(rank, out, inp, os_, is_), _Done())[1]
+            _, _, ex_w, handle, _ = buf.dispatch(x, topk_idx=g_idx, topk_weights=g_w, num_experts=E, do_expand=True)
+            if not np.array_equal(handle.recv_src_metadata.cpu().numpy(), metas[rank]):
+                failures.append(f'amr={amr}: recv_src_metadata')
+                continue
+            xin = _bf16(x_exp_all[rank])
+            for weighted in (False, True):
+                if amr:
+                    exp = oracle.combine_ep(x_exp_all, metas, idx_all, E, T, expanded=True,
+                                            topk_weights_per_rank=w_exp_all,
+                                            bias_per_rank=[(b, None) for b in b_all], weighted=weighted)[rank]
+                    out, out_w, _ = buf.combine(xin, handle, topk_weights=ex_w, bias=bias, apply_topk_weights=weighted)
+                    ok_w = np.array_equal(out_w.cpu().numpy(), exp[1])
+                    exp = exp[0]
+                elif weighted:
+                    cb = torch.from_numpy(b_all[rank].view(np.int16)).view(torch.bfloat16)
+                    exp = _u16(_weighted_single(y_all[rank], torch.from_numpy(idx_all[rank]),
+                                                torch.from_numpy(w_all[rank]), cb))
+                    out, out_w, _ = buf.combine(xin, handle, topk_weights=ex_w, bias=bias, apply_topk_weights=True)
+                    ok_w = np.array_equal(out_w.cpu().numpy(), w_all[rank])
+                else:
+                    exp = oracle.combine_ep(x_exp_all, metas, idx_all, E, T, expanded=True,
+                                            allow_multiple_reduction=False,
+                                            bias_per_rank=[(b, None) for b in b_all])[rank][0]
+                    out, out_w, _ = buf.combine(xin, handle, bias=bias)
+                    ok_w = out_w is None
+                torch.cuda.synchronize()
+                if not np.array_equal(_u16(out), exp):
+                    failures.append(f'amr={amr} weighted={weighted}: combined_x')
+                if not ok_w:
+                    failures.append(f'amr={amr} weighted={weighted}: weights')
+        results[rank] = failures
+    except Exception:
+        import traceback
+        results[rank] = [traceback.format_exc()]
+        comm.bar.abort()
+
+
+@pytest.mark.parametrize('case', range(16))
+def test_random_shapes_ep_sim(case, monkeypatch):
+    """Random EP = 2..8 cases (ragged per-rank batches incl. empty ranks, top-k 1..8, R > K and
+    R <= K layouts, chunked and one-shot exchange), all ranks simulated by threads on the GPU."""
+    import threading
+    from tests.test_combine_gpu import _ThreadComm
+    rng = np.random.default_rng(1000 + case)
+    world = int(rng.choice([2, 3, 4, 5, 8]))
+    if rng.random() < 0.5:
+        monkeypatch.setenv('DEEPEP_COMBINE_CHUNKS', str(int(rng.choice([2, 3]))))
+    comm = _ThreadComm(world)
+    results = {}
+    threads = [threading.Thread(target=_ep_thread, args=(r, world, 2000 + case, comm, results)) for r in range(world)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=150)
+    assert len(results) == world, results
+    bad = {r: f for r, f in results.items() if f}
+    assert not bad, (case, world, bad)

@@ -284,6 +284,8 @@ def main():
     ap.add_argument('--cpu-seconds', type=float, default=10.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-loopback', action='store_true')
+    ap.add_argument('--no-flushed', action='store_true',
+                    help='skip the per-launch flushed timing (keeps a rocprof kernel average to back-to-back launches)')
     args = ap.parse_args()
 
     rank, world = _init_dist(args.gpus)
@@ -368,7 +370,7 @@ def main():
         # before every launch, each launch timed alone (here: 512 MB written, HIP events around the kernel)
         flush = torch.empty((512 << 20) // 4, dtype=torch.int32, device=dev)
         fl_us = []
-        for _ in range(min(args.steps, 50)):
+        for _ in range(0 if args.no_flushed else min(args.steps, 50)):
             flush.zero_()
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(stream)
@@ -377,7 +379,7 @@ def main():
             fl_us.append((a, b))
         torch.cuda.synchronize()
         fl_us = sorted(a.elapsed_time(b) * 1e3 for a, b in fl_us)
-        kern_us_flushed = fl_us[len(fl_us) // 2]
+        kern_us_flushed = fl_us[len(fl_us) // 2] if fl_us else None
         del flush
         achieved = bytes_rank / (kern_us * 1e-6) / 1e9
         # same-run memory reference: a device-to-device copy of the expanded rows (boxes differ by up
@@ -423,7 +425,7 @@ def main():
         roofline = dict(bound='hbm', achieved=round(achieved, 1), peak=HBM_PEAK_GBPS, unit='GB/s',
                         frac=round(achieved / HBM_PEAK_GBPS, 4), traffic=_pmc_traffic(workload),
                         kernel='combine_rows_kernel<FUSED>', kernel_us=round(kern_us, 2),
-                        kernel_us_flushed_median=round(kern_us_flushed, 2),
+                        kernel_us_flushed_median=None if kern_us_flushed is None else round(kern_us_flushed, 2),
                         bytes_per_launch=bytes_rank, in_region_us_per_step=round(comm_ms * 1e3, 2),
                         same_run_d2d_copy_gbps=round(copy_gbps, 1), single_reduction_phase_b=single_b)
 

@@ -22,7 +22,7 @@ for step in "$@"; do
         smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench)  run bench 600 python bench.py ;;
         benchplain) run bench_plain 600 python bench.py --plain --no-cpu-baseline --no-loopback ;;
-        prof)   run rocprof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o prof --output-format csv -- python3 bench.py --no-cpu-baseline --no-loopback --steps 20 --warmup 5 ;;
+        prof)   run rocprof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o prof --output-format csv -- python3 bench.py --no-cpu-baseline --no-loopback --no-flushed --steps 20 --warmup 5 ;;
         kbench) run kbench 600 python tools/kbench.py ;;
         kalign) run kalign 600 python tools/kbench_align.py ;;
         kab)    run kab 600 python tools/kbench_ab.py ;;

@@ -26,8 +26,8 @@ import torch
 import torch.distributed as dist
 
 from .event import EventHandle, EventOverlap
-from .handle import (ChunkPlan, CombinePlan, EPHandle, chunk_plans, epilogue_tables, single_reduction_tables,
-                     weight_table, window_tables)
+from .handle import (ChunkPlan, CombinePlan, EPHandle, chunk_plans, epilogue_tables, single_chunk_plans,
+                     single_reduction_tables, weight_table, window_tables)
 from .kernels import MODE_EPILOGUE, MODE_FUSED, MODE_LOCAL, RowLayout
 from .utils import align, ceil_div, value_or
 
@@ -550,6 +550,9 @@ class ElasticBuffer:
             self.kernels.build_local_plan(meta, n_recv, K, handle.num_max_tokens_per_rank, handle.do_expand,
                                           plan.local_table, T, handle.topk_idx, plan.local_wtable,
                                           stream=torch.cuda.current_stream() if self.use_cuda else None)
+        elif single_reduction and num_chunks > 1:
+            plan.chunks = single_chunk_plans(meta, recv_counts, handle.topk_idx, handle.num_experts, R,
+                                             handle.num_max_tokens_per_rank, num_chunks)
         elif single_reduction:
             plan.table_b1, plan.back_counts1 = single_reduction_tables(handle.topk_idx, handle.num_experts, R)
             slots = meta[:n_recv, 2:]
@@ -639,6 +642,60 @@ class ElasticBuffer:
             for _, recv, packed, _ in in_flight:          # used on stream_b / the RCCL stream
                 recv.record_stream(stream_b)
                 packed.record_stream(stream_b)
+
+    def _combine_single_chunks(self, plan, x, row_w, wsrc, hidden, bias_0, bias_1, combined_x, combined_w,
+                               previous_event_before_epilogue, stream) -> None:
+        """Single-reduction combine over RCCL, chunked like _combine_chunks: the pack of chunk c+1
+        runs while RCCL moves chunk c, and the one reduction of chunk c (weighted: the legacy fma
+        chain) runs on a second stream while RCCL moves chunk c+1."""
+        kern = self.kernels
+        w_elems = 8 if row_w is not None else 0
+        row_elems = hidden + w_elems
+        pipelined = self.use_cuda
+        if pipelined:
+            if getattr(self, '_stream_b', None) is None:
+                self._stream_b = torch.cuda.Stream(device=self.device)
+            stream_b = self._stream_b
+            stream_b.wait_stream(stream)
+        in_flight = []
+        for ch in plan.chunks:
+            n_send = sum(ch.send_counts)
+            send = torch.empty((n_send, row_elems), dtype=x.dtype, device=x.device)
+            send_w = send[:, hidden:].view(torch.float32)[:, :1] if w_elems else None
+            self._mark(stream)
+            kern.combine_reduce(MODE_LOCAL, x, send[:, :hidden], n_send, table=ch.table_a,
+                                wtable=ch.table_a if w_elems else None, wsrc=wsrc if w_elems else None,
+                                out_weights=send_w, stream=stream)
+            self._mark(stream)
+            recv = torch.empty((sum(ch.back_counts), row_elems), dtype=x.dtype, device=x.device)
+            if pipelined:
+                work = self._a2a_async(recv, send, ch.back_counts, ch.send_counts)
+            else:
+                self._all_to_all(recv, send, ch.back_counts, ch.send_counts)
+                work = None
+            in_flight.append((ch, recv, send, work))
+        self._before_epilogue(previous_event_before_epilogue)
+        if pipelined and previous_event_before_epilogue is not None:
+            previous_event_before_epilogue.stream_wait(stream_b)
+        for ch, recv, send, work in in_flight:
+            with (torch.cuda.stream(stream_b) if pipelined else self._null_ctx()):
+                sb = stream_b if pipelined else stream
+                if work is not None:
+                    work.wait()
+                recv_w = recv[:, hidden:].view(torch.float32)[:, 0].contiguous() if w_elems else None
+                lo, hi = ch.lo, ch.hi
+                self._mark(sb)
+                kern.combine_reduce(MODE_EPILOGUE, recv[:, :hidden], combined_x[lo:hi], hi - lo, table=ch.table_b,
+                                    row_weights=recv_w, bias0=bias_0[lo:hi] if bias_0 is not None else None,
+                                    bias1=bias_1[lo:hi] if bias_1 is not None else None,
+                                    wtable=ch.table_b if w_elems else None, wsrc=recv_w,
+                                    out_weights=combined_w[lo:hi] if combined_w is not None else None, stream=sb)
+                self._mark(sb)
+        if pipelined:
+            stream.wait_stream(stream_b)
+            for _, recv, send, _ in in_flight:
+                recv.record_stream(stream_b)
+                send.record_stream(stream_b)
 
     # ------------------------------------------------------------------ EP > 1 over xGMI windows
     def _window(self, row_bytes: int):
@@ -947,7 +1004,7 @@ class ElasticBuffer:
             stream = self.comm_stream
         with (self._null_ctx() if sync_mode else self._stream_ctx()):
             use_xgmi = R > 1 and self.transport == 'xgmi' and self.use_cuda
-            num_chunks = self._num_chunks(handle) if not single_reduction else 1
+            num_chunks = self._num_chunks(handle)
             plan = None if use_xgmi else self._plan(handle, single_reduction, num_chunks)
             combined_x = torch.empty((T, hidden), dtype=x.dtype, device=x.device)
             combined_w = torch.empty((T, K), dtype=torch.float32, device=x.device) if topk_weights is not None else None
@@ -967,6 +1024,9 @@ class ElasticBuffer:
             elif single_reduction and use_xgmi:
                 self._combine_xgmi_single(handle, x, row_w, wsrc, K, hidden, bias_0, bias_1, topk_weights,
                                           combined_x, combined_w, previous_event_before_epilogue, stream)
+            elif single_reduction and plan.chunks is not None:
+                self._combine_single_chunks(plan, x, row_w, wsrc, hidden, bias_0, bias_1, combined_x, combined_w,
+                                            previous_event_before_epilogue, stream)
             elif single_reduction:
                 # every valid expanded row travels unreduced (kDoExpandedSend, combine.cuh:177-213);
                 # weighted: with its gating weight in a 16-byte row tail, applied by the one reduction

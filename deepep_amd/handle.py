@@ -240,3 +240,36 @@ class EPHandle:
         source global index, expanded rows by (expert, source index)), which is the order the
         reference's deterministic_sort produces (elastic.py:100-192); nothing to do."""
         return None
+
+
+def single_chunk_plans(meta: torch.Tensor, recv_counts: List[int], topk_idx: torch.Tensor, num_experts: int,
+                       num_ranks: int, num_max_tokens: int, num_chunks: int) -> List[ChunkPlan]:
+    """The single-reduction exchange (every valid expanded row unreduced) split into the same source-
+    token chunks as chunk_plans.  Expert side: chunk c's rows are, per source rank, a contiguous run
+    of received rows, and their valid lanes in (row, lane) order are the chunk's send buffer, grouped
+    by source rank (`table_a` = [n, 1] expanded rows).  Source side: `table_b` [hi - lo, K] is
+    single_reduction_tables over the chunk's tokens."""
+    T, K = topk_idx.shape
+    R = num_ranks
+    dev = meta.device
+    n_recv = sum(recv_counts)
+    B = (num_max_tokens + num_chunks - 1) // num_chunks
+    m = meta[:n_recv]
+    chunk_of_row = torch.div(m[:, 0] % num_max_tokens, B, rounding_mode='floor')
+    src_rank = torch.div(m[:, 1], K, rounding_mode='floor')
+    plans = []
+    for c in range(num_chunks):
+        lo, hi = c * B, min((c + 1) * B, T)
+        rows = (chunk_of_row == c).nonzero().view(-1)
+        slots = m[rows, 2:]
+        valid = slots >= 0
+        send_slots = slots[valid].view(-1, 1).to(torch.int32).contiguous()
+        lanes_per_row = valid.sum(dim=1)
+        send_counts = [int(v) for v in torch.bincount(src_rank[rows], weights=lanes_per_row.to(torch.float64),
+                                                      minlength=R).round().to(torch.int64).tolist()]
+        if hi > lo:
+            table_b, back_counts = single_reduction_tables(topk_idx[lo:hi], num_experts, R)
+        else:
+            table_b, back_counts = torch.empty((0, K), dtype=torch.int32, device=dev), [0] * R
+        plans.append(ChunkPlan(lo, max(lo, hi), send_slots, None, send_counts, back_counts, table_b, table_b))
+    return plans

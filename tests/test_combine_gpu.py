@@ -305,7 +305,7 @@ def _buffer_case(rank, world, fixture, comm, results):
         from tests.test_buffer_cpu import _weighted_single
         sbuf = ElasticBuffer(grp, num_max_tokens_per_rank=T, hidden=H, num_topk=K, allow_multiple_reduction=False)
         if world > 1:
-            sbuf._a2a = buf._a2a
+            sbuf._a2a, sbuf._a2a_async = buf._a2a, buf._a2a_async
         for nb in (0, 1, 2):
             bias = None if nb == 0 else (biases[0] if nb == 1 else tuple(biases))
             out, out_w, _ = sbuf.combine(x_exp, ex_handle, bias=bias)

@@ -1,0 +1,149 @@
+"""The stream modes of the reference test (tests/elastic/test_ep.py:22-41): with / without
+previous_event, async_with_compute_stream, allocate_on_comm_stream (and
+previous_event_before_epilogue), for dispatch and combine, on the GPU.  Every mode must give the
+sync-mode bits.  The inputs are produced on the compute stream right before each call, so a
+missing stream dependency would read stale data, and the outputs are overwritten on the compute
+stream right after the (awaited) call.  EP = 1 on the real device and EP = 4 with ranks simulated by
+threads (the pipelined multi-chunk path, whose phase B runs on a second stream)."""
+import os
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _modes():
+    """enumerate_ep_modes' stream axes (test_ep.py:22-31) plus a previous_event_before_epilogue."""
+    for with_previous_event in (0, 1):
+        for async_with_compute_stream in (0, 1):
+            for allocate_on_comm_stream in ((1,) if with_previous_event else (0, 1)):
+                yield with_previous_event, async_with_compute_stream, allocate_on_comm_stream, 0
+    yield 0, 1, 0, 1
+    yield 1, 1, 1, 1
+
+
+def _launch(buf, name, with_previous_event, async_with_compute_stream, before_epilogue, params):
+    """test_ep.py:34-41: capture the previous event, call, wait on the returned event if async."""
+    if with_previous_event:
+        params['previous_event'] = buf.capture()
+    if before_epilogue:
+        params['previous_event_before_epilogue'] = buf.capture()
+    values = getattr(buf, name)(**params)
+    hooked = []
+    if async_with_compute_stream:
+        values[-1].register_hook_after_wait(lambda: hooked.append(1))
+        values[-1].current_stream_wait()
+        assert hooked == [1]
+    return values
+
+
+def _run_modes(buf, x_src, idx, w, E, T, H, tag):
+    """All modes for one buffer; returns the list of mismatches."""
+    fails = []
+    biases = [torch.randn((T, H), device='cuda').to(torch.bfloat16) for _ in range(2)]
+
+    def fresh(t):
+        # produced on the compute stream right before the call (a slow multiply chain, so a
+        # comm-stream kernel that does not wait reads unfinished data)
+        out = t
+        for _ in range(3):
+            out = out * 1
+        return out
+
+    ref = {}
+    for mode in [(0, 0, 0, 0)] + list(_modes()):
+        prev, asyn, alloc, before = mode
+        common = dict(async_with_compute_stream=bool(asyn), allocate_on_comm_stream=bool(alloc))
+        recv_x, recv_idx, recv_w, handle, _ = _launch(
+            buf, 'dispatch', prev, asyn, 0, dict(x=fresh(x_src), topk_idx=idx, topk_weights=w, num_experts=E,
+                                                 **common))
+        ex_x, _, ex_w, ex_handle, _ = _launch(
+            buf, 'dispatch', prev, asyn, 0, dict(x=fresh(x_src), topk_idx=idx, topk_weights=w, num_experts=E,
+                                                 do_expand=True, **common))
+        got = {'recv_x': recv_x.clone(), 'ex_x': ex_x.clone(), 'recv_w': recv_w.clone(), 'ex_w': ex_w.clone()}
+        g = torch.Generator(device='cuda').manual_seed(7)
+        y_red = torch.randn((handle.num_recv_tokens, H), device='cuda', generator=g).to(torch.bfloat16)
+        y_exp = torch.randn(ex_x.shape, device='cuda', generator=g).to(torch.bfloat16)
+        for nb in (0, 1, 2):
+            bias = None if nb == 0 else (fresh(biases[0]) if nb == 1 else (fresh(biases[0]), fresh(biases[1])))
+            out, out_w, _ = _launch(buf, 'combine', prev, asyn, before,
+                                    dict(x=fresh(y_red), handle=handle, topk_weights=recv_w, bias=bias, **common))
+            got[f'combine_b{nb}'], got[f'combine_w_b{nb}'] = out.clone(), out_w.clone()
+            out.fill_(0)                                   # the caller reuses the memory right away
+            out, out_w, _ = _launch(buf, 'combine', prev, asyn, before,
+                                    dict(x=fresh(y_exp), handle=ex_handle, topk_weights=ex_w, bias=bias, **common))
+            got[f'expanded_b{nb}'], got[f'expanded_w_b{nb}'] = out.clone(), out_w.clone()
+            out.fill_(0)
+        out, _, _ = _launch(buf, 'combine', prev, asyn, before,
+                            dict(x=fresh(y_exp), handle=ex_handle, topk_weights=ex_w, apply_topk_weights=True,
+                                 **common))
+        got['weighted'] = out.clone()
+        torch.cuda.synchronize()
+        if mode == (0, 0, 0, 0):
+            ref = got
+            continue
+        for k, v in got.items():
+            if not torch.equal(v, ref[k]):
+                fails.append(f'{tag} mode {mode}: {k}')
+    return fails
+
+
+def _inputs(T, H, K, E, seed):
+    g = torch.Generator(device='cuda').manual_seed(seed)
+    w, idx = torch.topk(torch.rand((T, E), device='cuda', generator=g), K, dim=-1, sorted=False)
+    idx = idx.to(torch.int64)
+    idx[torch.rand(idx.shape, device='cuda', generator=g) < 0.1] = -1
+    w = w.masked_fill(idx < 0, 0)
+    x = torch.randn((T, H), device='cuda', generator=g).to(torch.bfloat16)
+    return x, idx, w
+
+
+def test_stream_modes_ep1():
+    import torch.distributed as dist
+    from deepep_amd import ElasticBuffer
+    if not dist.is_initialized():
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        os.environ.setdefault('MASTER_PORT', '29551')
+        dist.init_process_group('gloo', rank=0, world_size=1)
+    T, H, K, E = 777, 2048, 8, 64
+    x, idx, w = _inputs(T, H, K, E, 1)
+    buf = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=T, hidden=H, num_topk=K)
+    fails = _run_modes(buf, x, idx, w, E, T, H, 'ep1')
+    assert not fails, fails
+
+
+def _sim_rank(rank, world, comm, results):
+    try:
+        from deepep_amd import ElasticBuffer
+        from tests.test_combine_gpu import _Done, _FakeGroup
+        torch.cuda.set_device(0)
+        T, H, K, E = 1100, 1024, 8, 32
+        x, idx, w = _inputs(T, H, K, E, 100 + rank)
+        buf = ElasticBuffer(_FakeGroup(rank, world, comm), num_max_tokens_per_rank=T, hidden=H, num_topk=K)
+        buf._a2a = lambda out, inp, os_=None, is_=None: comm.a2a(rank, out, inp, os_, is_)
+        buf._a2a_async = lambda out, inp, os_, is_: (comm.a2a(rank, out, inp, os_, is_), _Done())[1]
+        results[rank] = _run_modes(buf, x, idx, w, E, T, H, f'ep{world} rank {rank}')
+    except Exception:
+        import traceback
+        results[rank] = [traceback.format_exc()]
+        comm.bar.abort()
+
+
+def test_stream_modes_ep4_pipelined(monkeypatch):
+    """EP = 4, 1100 tokens per rank -> the 4-chunk pipelined exchange (phase B on a second stream)."""
+    from tests.test_combine_gpu import _ThreadComm
+    monkeypatch.setenv('DEEPEP_COMBINE_CHUNKS', '4')
+    world = 4
+    comm = _ThreadComm(world)
+    results = {}
+    threads = [threading.Thread(target=_sim_rank, args=(r, world, comm, results)) for r in range(world)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=160)
+    assert len(results) == world, results
+    bad = {r: f for r, f in results.items() if f}
+    assert not bad, bad

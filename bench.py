@@ -135,7 +135,7 @@ def _bench_xgmi(buf, y, handle, ex_w, weighted, total_bytes, steps, warmup, dev)
     try:
         xb = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=buf.num_max_tokens_per_rank,
                            hidden=y.shape[1], num_topk=handle.topk_idx.shape[1], explicitly_destroy=True,
-                           num_gpu_timeout_secs=10)
+                           num_gpu_timeout_secs=5)
         xb.transport = 'xgmi'
         out, _, _ = xb.combine(y, handle, topk_weights=ex_w, apply_topk_weights=weighted)
         torch.cuda.synchronize()
@@ -152,6 +152,10 @@ def _bench_xgmi(buf, y, handle, ex_w, weighted, total_bytes, steps, warmup, dev)
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
+    # a device barrier that timed out in warm-up would make every timed step wait the timeout
+    if not agree(int(xb._sym.error_flag.item()) == 0):
+        xb.destroy()
+        return dict(error='device barrier timeout during warm-up', bitwise_equal_to_rccl=equal_all)
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -202,7 +206,7 @@ def _bench_single(y, handle, ex_w, weighted, total_bytes, steps, warmup, dev, re
         sb, err = None, None
         try:
             sb = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=T_max, hidden=H, num_topk=K,
-                               allow_multiple_reduction=False, explicitly_destroy=True, num_gpu_timeout_secs=10)
+                               allow_multiple_reduction=False, explicitly_destroy=True, num_gpu_timeout_secs=5)
             sb.transport = transport
 
             def step():
@@ -220,6 +224,11 @@ def _bench_single(y, handle, ex_w, weighted, total_bytes, steps, warmup, dev, re
         for _ in range(warmup):
             step()
         torch.cuda.synchronize()
+        if sb._sym is not None and not agree(int(sb._sym.error_flag.item()) == 0):
+            res[transport] = dict(error='device barrier timeout during warm-up')
+            outs.pop(transport, None)
+            sb.destroy()
+            continue
         dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()

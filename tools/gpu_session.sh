@@ -21,6 +21,8 @@ for step in "$@"; do
         tests)  run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 170 --timeout-method thread ;;
         smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench)  run bench 600 python bench.py ;;
+        benchc4) run bench_c4 600 python bench.py --fp8-dispatch --no-cpu-baseline --no-loopback ;;
+        benchc5) run bench_c5 600 python bench.py --tokens 16384 --skew 4 --no-cpu-baseline --no-loopback ;;
         benchplain) run bench_plain 600 python bench.py --plain --no-cpu-baseline --no-loopback ;;
         prof)   run rocprof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o prof --output-format csv -- python3 bench.py --no-cpu-baseline --no-loopback --no-flushed --steps 20 --warmup 5 ;;
         kbench) run kbench 600 python tools/kbench.py ;;
@@ -33,6 +35,7 @@ for step in "$@"; do
         kphase) run kphase 300 python tools/kphase.py ;;
         pmclist) run pmclist 120 rocprofv3 --list-avail ;;
         smi)    run smi 60 rocm-smi --showclocks --showpower --showtemp ;;
+        bench4gloo) export DEEPEP_BENCH_BACKEND=gloo; run bench4gloo 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29657 bench.py --gpus 4 --steps 4 --warmup 2; unset DEEPEP_BENCH_BACKEND ;;
         bench2gloo) export DEEPEP_BENCH_BACKEND=gloo; run bench2gloo 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29655 bench.py --gpus 2 --steps 10 --warmup 3; unset DEEPEP_BENCH_BACKEND ;;
         pmc)    for c in FETCH_SIZE WRITE_SIZE TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum; do
                     run pmc_$c 600 rocprofv3 --pmc $c -d $OUT/pmc_$c -o pmc --output-format csv -- python3 tools/pmc_run.py

@@ -11,7 +11,7 @@ from typing import Optional
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('DEEPEP_AMD_LIB', os.path.join(_HERE, 'libdeepep_amd.so'))
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 MODE_LOCAL, MODE_EPILOGUE, MODE_FUSED = 0, 1, 2
 
@@ -58,6 +58,8 @@ SIGNATURES = {
     'deepep_sym_barrier': (_I, [_P, _I, _I, _I64, _I64, _P, _P]),
     'deepep_sym_signal': (_I, [_P, _I, _I, _I, _I64, _P]),
     'deepep_sym_wait': (_I, [_P, _I, _I, _I, _I64, _I64, _P, _P]),
+    'deepep_stream_create_cu_budget': (_I, [_I, ctypes.POINTER(ctypes.c_void_p)]),
+    'deepep_stream_destroy': (_I, [_P]),
     'deepep_combine_reduce_scatter': (_I, [_I, _P, _I64, _I64, _P, _I64, _I, _P, _P, _I, _I, _P, _I64, _P, _I,
                                            _I64, _P, _P]),
 }

@@ -164,6 +164,8 @@ class ElasticBuffer:
                 self._group_barrier()             # no peer still stores into this rank's window
                 self._sym.destroy()
                 self._sym = None
+            for raw, _ in self.__dict__.pop('_budget_streams', {}).values():
+                self.kernels.lib.deepep_stream_destroy(raw)
             self.runtime = None
 
     @staticmethod
@@ -942,17 +944,48 @@ class ElasticBuffer:
         expanded row by its top-k weight inside the reduction (the gating-weighted sum of the
         legacy low_latency_combine, csrc/kernels/legacy/internode_ll.cu:1072-1135).  Requires
         the expanded layout and `topk_weights`.  The weights are still passed through."""
+        explicit_sms = num_sms
         num_sms = handle.num_sms if num_sms == 0 else num_sms
         num_qps = self.get_theoretical_num_qps(num_sms) if num_qps == 0 else num_qps
         _assert(num_qps <= self.num_allocated_qps, 'Allocated QPs are not enough')
         bias_0, bias_1 = self._unpack_bias(bias)
-        return self._combine(x, topk_weights, bias_0, bias_1, handle, num_sms, previous_event,
-                             previous_event_before_epilogue, async_with_compute_stream,
-                             allocate_on_comm_stream, apply_topk_weights)
+        budget = self._cu_budget_stream(explicit_sms)
+        if budget is None:
+            return self._combine(x, topk_weights, bias_0, bias_1, handle, num_sms, previous_event,
+                                 previous_event_before_epilogue, async_with_compute_stream,
+                                 allocate_on_comm_stream, apply_topk_weights)
+        # An explicit num_sms below the CU count: the combine's kernels run on a stream restricted to
+        # that many CUs (the reference's combine_impl grid, combine.hpp:135), the rest stay free for
+        # compute.  That stream plays the comm stream, so the call takes the async-capable path.
+        saved, self.comm_stream = self.comm_stream, budget
+        try:
+            return self._combine(x, topk_weights, bias_0, bias_1, handle, num_sms, previous_event,
+                                 previous_event_before_epilogue, async_with_compute_stream,
+                                 allocate_on_comm_stream, apply_topk_weights, force_comm_stream=True)
+        finally:
+            self.comm_stream = saved
+
+    def _cu_budget_stream(self, num_sms: int):
+        """The CU-budget stream for an explicit num_sms (None when 0 or at least the CU count).
+        The handle's default num_sms is the reference's NVLink/SM bandwidth model
+        (get_theoretical_num_sms); on MI355X the combine is HBM-bound and takes the whole chip
+        unless the caller asks for less."""
+        if num_sms <= 0 or not self.use_cuda:
+            return None
+        if num_sms >= torch.cuda.get_device_properties(self.device).multi_processor_count:
+            return None
+        streams = self.__dict__.setdefault('_budget_streams', {})
+        if num_sms not in streams:
+            import ctypes
+            from . import _lib
+            raw = ctypes.c_void_p()
+            _lib.check(self.kernels.lib.deepep_stream_create_cu_budget(num_sms, ctypes.byref(raw)), 'cu_budget stream')
+            streams[num_sms] = (raw.value, torch.cuda.ExternalStream(raw.value, device=self.device))
+        return streams[num_sms][1]
 
     def _combine(self, x, topk_weights, bias_0, bias_1, handle, num_sms, previous_event,
                  previous_event_before_epilogue, async_with_compute_stream, allocate_on_comm_stream,
-                 apply_topk_weights):
+                 apply_topk_weights, force_comm_stream=False):
         # ---- checks of ElasticBuffer::combine (buffer.hpp:1197-1247)
         _assert(self.runtime is not None, 'buffer destroyed')
         _assert(num_sms > 0, 'num_sms > 0')
@@ -995,7 +1028,7 @@ class ElasticBuffer:
         kern = self.kernels
         R = self.num_ranks
         sync_mode = self._sync_mode(previous_event, previous_event_before_epilogue, async_with_compute_stream,
-                                    allocate_on_comm_stream)
+                                    allocate_on_comm_stream) and not force_comm_stream
         if sync_mode:
             compute_stream = None
             stream = torch.cuda.current_stream() if self.use_cuda else None

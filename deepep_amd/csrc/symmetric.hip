@@ -150,6 +150,34 @@ int deepep_sym_close(void* ptr) {
     return e == hipSuccess ? DEEPEP_OK : hip_fail(e, "hipIpcCloseMemHandle");
 }
 
+int deepep_stream_create_cu_budget(int num_cus, deepep_stream_t* stream) {
+    if (stream == nullptr || num_cus < 1) return deepep_amd_set_error(DEEPEP_ERR_INVALID_ARG, "cu_budget: bad arguments");
+    *stream = nullptr;
+    int dev = 0, n = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess) return hip_fail(e, "CU count");
+    if (num_cus > n) num_cus = n;
+    // Mask bit b is CU b / 8 of XCD b % 8 (probed on MI355X, tools/probe_cumask.py), and an XCD whose
+    // bits are all clear is not restricted at all; so the budget is the FIRST num_cus bits: num_cus / 8
+    // CUs on every XCD.
+    uint32_t mask[64] = {};
+    const int words = (n + 31) / 32;
+    if (words > 64) return deepep_amd_set_error(DEEPEP_ERR_UNSUPPORTED, "cu_budget: more than 2048 CUs");
+    for (int b = 0; b < num_cus; ++b) mask[b / 32] |= 1u << (b % 32);
+    hipStream_t s = nullptr;
+    e = hipExtStreamCreateWithCUMask(&s, static_cast<uint32_t>(words), mask);
+    if (e != hipSuccess) return hip_fail(e, "hipExtStreamCreateWithCUMask");
+    *stream = reinterpret_cast<deepep_stream_t>(s);
+    return DEEPEP_OK;
+}
+
+int deepep_stream_destroy(deepep_stream_t stream) {
+    if (stream == nullptr) return DEEPEP_OK;
+    const hipError_t e = hipStreamDestroy(reinterpret_cast<hipStream_t>(stream));
+    return e == hipSuccess ? DEEPEP_OK : hip_fail(e, "hipStreamDestroy");
+}
+
 int deepep_sym_barrier(const uint64_t* peer_flags, int rank, int num_ranks, int64_t epoch, int64_t timeout_us,
                        int32_t* error_flag, deepep_stream_t stream) {
     if (peer_flags == nullptr || num_ranks < 1 || num_ranks > 64 || rank < 0 || rank >= num_ranks || epoch < 1)

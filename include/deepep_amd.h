@@ -45,7 +45,7 @@ extern "C" {
 
 typedef struct ihipStream_t* deepep_stream_t;   /* == hipStream_t */
 
-#define DEEPEP_AMD_ABI_VERSION 5
+#define DEEPEP_AMD_ABI_VERSION 6
 
 #define DEEPEP_OK               0
 #define DEEPEP_ERR_INVALID_ARG  (-1)
@@ -231,6 +231,14 @@ int deepep_combine_reduce_scatter(int weighted,
                                   const int32_t* wtable, int64_t wtable_stride,
                                   const float* wsrc, int num_weights, int64_t weights_offset,
                                   int32_t* error_flag, deepep_stream_t stream);
+
+/* A CU budget: a stream whose kernels run on `num_cus` compute units only
+ * (hipExtStreamCreateWithCUMask, the first num_cus mask bits = num_cus / 8 CUs on every XCD),
+ * leaving the rest to overlapping
+ * compute.  It is how this build honours an explicit num_sms (the reference sizes combine_impl's
+ * grid with it, csrc/kernels/elastic/combine.hpp:135, elastic.py:1086-1088). */
+int deepep_stream_create_cu_budget(int num_cus, deepep_stream_t* stream);
+int deepep_stream_destroy(deepep_stream_t stream);
 
 /* ElasticBuffer::get_combine_buffer_size for one node (num_scaleout_ranks == 1). */
 int64_t deepep_combine_buffer_size(int num_max_tokens_per_rank, int hidden, int num_topk,

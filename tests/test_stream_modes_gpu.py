@@ -81,9 +81,19 @@ def _run_modes(buf, x_src, idx, w, E, T, H, tag):
                             dict(x=fresh(y_exp), handle=ex_handle, topk_weights=ex_w, apply_topk_weights=True,
                                  **common))
         got['weighted'] = out.clone()
+        # an explicit num_sms below the CU count: the kernels run on a CU-budget stream
+        for cus in (40, 100):
+            out, out_w, _ = _launch(buf, 'combine', prev, asyn, before,
+                                    dict(x=fresh(y_exp), handle=ex_handle, topk_weights=ex_w, num_sms=cus, **common))
+            got[f'budget{cus}'], got[f'budget{cus}_w'] = out.clone(), out_w.clone()
+            out.fill_(0)
         torch.cuda.synchronize()
         if mode == (0, 0, 0, 0):
             ref = got
+            for cus in (40, 100):
+                if not (torch.equal(got[f'budget{cus}'], got['expanded_b0']) and
+                        torch.equal(got[f'budget{cus}_w'], got['expanded_w_b0'])):
+                    fails.append(f'{tag}: num_sms={cus} differs from the whole-chip combine')
             continue
         for k, v in got.items():
             if not torch.equal(v, ref[k]):

@@ -42,6 +42,9 @@ for step in "$@"; do
         pmc)    for c in FETCH_SIZE WRITE_SIZE TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum; do
                     run pmc_$c 600 rocprofv3 --pmc $c -d $OUT/pmc_$c -o pmc --output-format csv -- python3 tools/pmc_run.py
                 done ;;
+        pmcphases) for c in FETCH_SIZE WRITE_SIZE; do
+                    run pmcph_$c 300 rocprofv3 --pmc $c -d $OUT/pmcph_$c -o pmc --output-format csv -- python3 tools/pmc_phases.py
+                done ;;
         pmcplain) for c in FETCH_SIZE WRITE_SIZE; do
                     run pmcp_$c 600 rocprofv3 --pmc $c -d $OUT/pmcp_$c -o pmc --output-format csv -- python3 tools/pmc_run.py --plain
                 done ;;

@@ -49,8 +49,45 @@ def pmc(out, workload, algo_bytes, *paths):
     print(json.dumps({workload: entry}, indent=1))
 
 
+def pmc_phases(out, meta_json, *paths):
+    """Per-kernel HBM bytes of tools/pmc_phases.py's launches (kinds told apart by kernel name:
+    combine_rows_kernel<2,...> fused, <0,...> local, <1,...> epilogue, copy_kernel), 2 x FETCH_SIZE +
+    WRITE_SIZE (KiB) as in pmc(), against the algorithmic bytes the run recorded."""
+    algo = json.load(open(meta_json))
+
+    def kind(name):
+        if 'copy_kernel' in name:
+            return 'copy'
+        if 'combine_rows_kernel<2' in name:
+            return 'fused'
+        if 'combine_rows_kernel<0' in name:
+            return 'local'
+        if 'combine_rows_kernel<1' in name:
+            return 'epilogue'
+        return None
+    per = defaultdict(lambda: defaultdict(list))
+    for p in paths:
+        for r in csv.DictReader(open(p)):
+            k = kind(r.get('Kernel_Name', '').replace('(anonymous namespace)::', ''))
+            if k is not None:
+                per[k][r['Counter_Name']].append(float(r['Counter_Value']))
+    res = {}
+    for k, counters in per.items():
+        avg = {c: sum(v) / len(v) for c, v in counters.items()}
+        e = {'counters_avg_per_launch': avg, 'algorithmic_bytes_per_launch': algo[k]}
+        if 'FETCH_SIZE' in avg and 'WRITE_SIZE' in avg:
+            e['hbm_read_bytes_per_launch'] = 2 * avg['FETCH_SIZE'] * 1024
+            e['hbm_write_bytes_per_launch'] = avg['WRITE_SIZE'] * 1024
+            e['traffic_over_algorithmic'] = (e['hbm_read_bytes_per_launch'] + e['hbm_write_bytes_per_launch']) / algo[k]
+        res[k] = e
+    json.dump(res, open(out, 'w'), indent=1, sort_keys=True)
+    print(json.dumps(res, indent=1))
+
+
 if __name__ == '__main__':
-    if sys.argv[1] == 'stats':
+    if sys.argv[1] == 'phases':
+        pmc_phases(sys.argv[2], sys.argv[3], *sys.argv[4:])
+    elif sys.argv[1] == 'stats':
         stats(sys.argv[2], sys.argv[3])
     else:
         pmc(sys.argv[2], sys.argv[3], sys.argv[4], *sys.argv[5:])

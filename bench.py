@@ -453,6 +453,21 @@ def main():
         t_b = sum(ev[4 * i + 2].elapsed_time(ev[4 * i + 3]) for i in range(n_ph)) / n_ph
         sent_rows = sum(c for r_, c in enumerate(handle._recv_counts) if r_ != rank)
         x_bytes = sent_rows * (H * 2 + K * 4)
+        # The dominant GPU kernel at N > 1 is phase A (LOCAL reduce): its algorithmic bytes on this rank
+        # (the valid expanded rows read + one partial row with its K weights written per received
+        # token) over its measured time; the worst rank is reported.
+        n_recv = sum(handle._recv_counts)
+        n_rows = int((handle.recv_src_metadata[:n_recv, 2:] >= 0).sum().item())
+        a_bytes = n_rows * H * 2 + n_recv * (H * 2 + K * 4)
+        a_rate = torch.tensor([a_bytes / (t_a * 1e-3) / 1e9], dtype=torch.float64, device=dev)
+        dist.all_reduce(a_rate, op=dist.ReduceOp.MIN)
+        a_rate = float(a_rate.item())
+        roofline = dict(bound='hbm', achieved=round(a_rate, 1), peak=HBM_PEAK_GBPS, unit='GB/s',
+                        frac=round(a_rate / HBM_PEAK_GBPS, 4), traffic=None,
+                        kernel='combine_rows_kernel<LOCAL> (phase A)', bytes_per_launch=a_bytes,
+                        kernel_us=round(t_a * 1e3, 2),
+                        note='worst rank; unpipelined phase-A launch timed with HIP events; the end-to-end step '
+                             'is bound by the xGMI exchange (see phases, DESIGN.md section 5)')
         vals = torch.tensor([t_a + t_b, t_x, t_a, t_b], dtype=torch.float64, device=dev)
         dist.all_reduce(vals, op=dist.ReduceOp.MAX)
         xb = torch.tensor([float(x_bytes)], dtype=torch.float64, device=dev)

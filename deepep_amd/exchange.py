@@ -1,0 +1,390 @@
+"""The EP > 1 exchanges of ElasticBuffer.combine (a mixin of deepep_amd.buffer.ElasticBuffer).
+
+  RCCL transport   phase A (local reduce) -> all_to_all_single of packed [partial | weights] rows ->
+                   phase B (epilogue), pipelined in source-token chunks; and the single reduction
+                   (rows unreduced, one reduce at the source rank), pipelined the same way
+  xGMI transport   phase A stores straight into the owners' symmetric windows (HIP IPC), device
+                   barriers / split barriers, phase B over the local window; multiple and single
+                   reduction
+
+The per-token arithmetic is the reference's (combine.cuh, combine_reduce_epilogue.cuh in
+/root/reference); the exchange design is DESIGN.md section 5.
+"""
+import itertools
+from typing import List
+
+import torch
+import torch.distributed as dist
+
+from .handle import ChunkPlan, CombinePlan, EPHandle, weight_table, window_tables
+from .kernels import MODE_EPILOGUE, MODE_LOCAL
+from .utils import align
+
+_WINDOW_IDS = itertools.count(1)            # symmetric windows created by this process
+
+
+def _interleave_by_rank(units: torch.Tensor, dest_rank: torch.Tensor, num_ranks: int) -> torch.Tensor:
+    """Reorder a phase-A launch's units (ascending, hence grouped by destination rank) round-robin
+    over the destinations: the waves in flight at any moment then store to every peer at once, so
+    all of xGMI's point-to-point links carry traffic instead of one link at a time.  Units are
+    independent, so the order changes no result."""
+    if units.numel() == 0 or num_ranks == 1:
+        return units
+    d = dest_rank[units]
+    counts = torch.bincount(d, minlength=num_ranks)
+    start = torch.cumsum(counts, 0) - counts
+    pos = torch.arange(units.numel(), device=units.device) - start[d]        # units are sorted by d
+    return units[torch.argsort(pos * num_ranks + d)]
+
+
+class ExchangeMixin:
+    """EP > 1 exchange paths; uses the host attributes of ElasticBuffer (group, ranks, streams,
+    kernels, _mark, _before_epilogue, _all_to_all)."""
+
+    def _a2a_async(self, out: torch.Tensor, inp: torch.Tensor, out_splits: List[int], in_splits: List[int]):
+        """Row all-to-all that returns a waitable (RCCL runs it on its own stream; `wait()` makes the
+        current stream wait).  Tests on a single device replace this method."""
+        o = out.view(torch.uint8).view(out.shape[0], out.shape[1] * out.element_size())
+        i = inp.view(torch.uint8).view(inp.shape[0], inp.shape[1] * inp.element_size())
+        return dist.all_to_all_single(o, i, out_splits, in_splits, group=self.group, async_op=True)
+
+    def _combine_chunks(self, plan, x, expanded, row_w, wsrc, K, hidden, bias_0, bias_1, topk_weights,
+                        combined_x, combined_w, previous_event_before_epilogue, stream) -> None:
+        """EP > 1 combine, chunked: phase A (local reduce per received token) -> all-to-all of
+        packed rows [bf16 partial | fp32 top-k weights] -> phase B (epilogue + bias).  With more
+        than one chunk, phase A of chunk c+1 runs while RCCL moves chunk c and phase B of chunk
+        c runs on a second stream while RCCL moves chunk c+1."""
+        kern = self.kernels
+        w_elems = 0 if topk_weights is None else align(K * 4, 16) // 2
+        row_elems = hidden + w_elems
+        pipelined = len(plan.chunks) > 1 and self.use_cuda
+        if pipelined:
+            if getattr(self, '_stream_b', None) is None:
+                self._stream_b = torch.cuda.Stream(device=self.device)
+            stream_b = self._stream_b
+            stream_b.wait_stream(stream)                  # bias / outputs were produced before this call
+        in_flight = []
+        for ch in plan.chunks:
+            n_send = sum(ch.send_counts)
+            packed = torch.empty((n_send, row_elems), dtype=x.dtype, device=x.device)
+            partial_w = packed[:, hidden:].view(torch.float32)[:, :K] if w_elems else None
+            self._mark(stream)
+            kern.combine_reduce(MODE_LOCAL, x, packed[:, :hidden], n_send, table=ch.table_a, row_weights=row_w,
+                                wtable=ch.wtable_a, wsrc=wsrc, out_weights=partial_w, stream=stream)
+            self._mark(stream)
+            recv = torch.empty((sum(ch.back_counts), row_elems), dtype=x.dtype, device=x.device)
+            if pipelined:
+                work = self._a2a_async(recv, packed, ch.back_counts, ch.send_counts)
+            else:
+                self._all_to_all(recv, packed, ch.back_counts, ch.send_counts)
+                work = None
+            in_flight.append((ch, recv, packed, work))
+        self._before_epilogue(previous_event_before_epilogue)
+        if pipelined and previous_event_before_epilogue is not None:
+            previous_event_before_epilogue.stream_wait(stream_b)
+        for ch, recv, packed, work in in_flight:
+            ctx = torch.cuda.stream(stream_b) if pipelined else self._null_ctx()
+            with ctx:
+                sb = stream_b if pipelined else stream
+                if work is not None:
+                    work.wait()
+                wtable_b, recv_wsrc = None, None
+                if w_elems:
+                    key = (row_elems // 2, hidden // 2)
+                    if key not in ch.wtables:
+                        ch.wtables[key] = weight_table(ch.row_of_lane, *key)
+                    wtable_b = ch.wtables[key]
+                    recv_wsrc = recv.view(torch.float32).view(-1)
+                lo, hi = ch.lo, ch.hi
+                self._mark(sb)
+                kern.combine_reduce(MODE_EPILOGUE, recv[:, :hidden], combined_x[lo:hi], hi - lo, table=ch.table_b,
+                                    bias0=bias_0[lo:hi] if bias_0 is not None else None,
+                                    bias1=bias_1[lo:hi] if bias_1 is not None else None,
+                                    wtable=wtable_b, wsrc=recv_wsrc,
+                                    out_weights=combined_w[lo:hi] if combined_w is not None else None, stream=sb)
+                self._mark(sb)
+        if pipelined:
+            stream.wait_stream(stream_b)
+            for _, recv, packed, _ in in_flight:          # used on stream_b / the RCCL stream
+                recv.record_stream(stream_b)
+                packed.record_stream(stream_b)
+
+    def _combine_single_chunks(self, plan, x, row_w, wsrc, hidden, bias_0, bias_1, combined_x, combined_w,
+                               previous_event_before_epilogue, stream) -> None:
+        """Single-reduction combine over RCCL, chunked like _combine_chunks: the pack of chunk c+1
+        runs while RCCL moves chunk c, and the one reduction of chunk c (weighted: the legacy fma
+        chain) runs on a second stream while RCCL moves chunk c+1."""
+        kern = self.kernels
+        w_elems = 8 if row_w is not None else 0
+        row_elems = hidden + w_elems
+        pipelined = self.use_cuda
+        if pipelined:
+            if getattr(self, '_stream_b', None) is None:
+                self._stream_b = torch.cuda.Stream(device=self.device)
+            stream_b = self._stream_b
+            stream_b.wait_stream(stream)
+        in_flight = []
+        for ch in plan.chunks:
+            n_send = sum(ch.send_counts)
+            send = torch.empty((n_send, row_elems), dtype=x.dtype, device=x.device)
+            send_w = send[:, hidden:].view(torch.float32)[:, :1] if w_elems else None
+            self._mark(stream)
+            kern.combine_reduce(MODE_LOCAL, x, send[:, :hidden], n_send, table=ch.table_a,
+                                wtable=ch.table_a if w_elems else None, wsrc=wsrc if w_elems else None,
+                                out_weights=send_w, stream=stream)
+            self._mark(stream)
+            recv = torch.empty((sum(ch.back_counts), row_elems), dtype=x.dtype, device=x.device)
+            if pipelined:
+                work = self._a2a_async(recv, send, ch.back_counts, ch.send_counts)
+            else:
+                self._all_to_all(recv, send, ch.back_counts, ch.send_counts)
+                work = None
+            in_flight.append((ch, recv, send, work))
+        self._before_epilogue(previous_event_before_epilogue)
+        if pipelined and previous_event_before_epilogue is not None:
+            previous_event_before_epilogue.stream_wait(stream_b)
+        for ch, recv, send, work in in_flight:
+            with (torch.cuda.stream(stream_b) if pipelined else self._null_ctx()):
+                sb = stream_b if pipelined else stream
+                if work is not None:
+                    work.wait()
+                recv_w = recv[:, hidden:].view(torch.float32)[:, 0].contiguous() if w_elems else None
+                lo, hi = ch.lo, ch.hi
+                self._mark(sb)
+                kern.combine_reduce(MODE_EPILOGUE, recv[:, :hidden], combined_x[lo:hi], hi - lo, table=ch.table_b,
+                                    row_weights=recv_w, bias0=bias_0[lo:hi] if bias_0 is not None else None,
+                                    bias1=bias_1[lo:hi] if bias_1 is not None else None,
+                                    wtable=ch.table_b if w_elems else None, wsrc=recv_w,
+                                    out_weights=combined_w[lo:hi] if combined_w is not None else None, stream=sb)
+                self._mark(sb)
+        if pipelined:
+            stream.wait_stream(stream_b)
+            for _, recv, send, _ in in_flight:
+                recv.record_stream(stream_b)
+                send.record_stream(stream_b)
+
+    # ------------------------------------------------------------------ EP > 1 over xGMI windows
+    def _window(self, row_bytes: int):
+        """The symmetric window: `num_bytes` (the reference's symmetric buffer size, buffer.hpp:589-686,
+        which holds every combine layout of the declared shape: min(R, K) or K receive slots x T_max
+        rows) or more if a call needs it; allocated on first use (collective: every rank reaches the
+        same combine)."""
+        slots = self._window_slots
+        need = slots * self.num_max_tokens_per_rank * row_bytes
+        if self._sym is not None and self._sym.data_bytes >= need:
+            return self._sym
+        from .symmetric import SymmetricBuffer
+        old = self._sym
+        if old is not None:
+            self._group_barrier()                 # no rank still uses the old window
+        # the new window is allocated (and exported) before the old one is freed: exporting an
+        # allocation that reuses a freed, previously exported address fails (hipIpcGetMemHandle)
+        self._sym = SymmetricBuffer(self.group, self.rank_idx, self.num_ranks, max(need, self.num_bytes),
+                                    self.device, exchange=self._sym_exchange, timeout_s=self.num_gpu_timeout_secs)
+        if old is not None:
+            old.destroy()
+        # plans cache peer row addresses: they are valid for this window only (a process-unique id,
+        # since one handle may serve several buffers)
+        if getattr(self, '_sym_gen', None) is not None:
+            self._old_sym_gens.add(self._sym_gen)
+        else:
+            self._old_sym_gens = set()
+        self._sym_gen = next(_WINDOW_IDS)
+        return self._sym
+
+    def _window_plan(self, handle: EPHandle, key: tuple):
+        """The handle's cached xGMI plan for `key` under the current window, dropping plans that
+        address an earlier (freed) window."""
+        stale = [k for k in handle._combine_plans if k[0] in ('xgmi', 'xgmi-single') and k[-1] in self._old_sym_gens]
+        for k in stale:
+            del handle._combine_plans[k]
+        return handle._combine_plans.get(key + (self._sym_gen,))
+
+    def _combine_xgmi(self, handle, x, expanded, row_w, wsrc, K, hidden, bias_0, bias_1, topk_weights,
+                      combined_x, combined_w, previous_event_before_epilogue, stream) -> None:
+        """EP > 1 combine over the symmetric windows (the reference's NVLink design on xGMI):
+        barrier (peers done reading their windows) -> phase A storing every partial and its top-k
+        weights straight into the owner's window row slot * T_max + t (combine.cuh:96-106, 215-226)
+        -> all partials landed (comm.cuh:88-129) -> phase B over the local window.  Split into
+        source-token chunks like the RCCL path: phase A of chunk c is followed by a signal on split
+        barrier c, and phase B of chunk c runs on a second stream behind the wait for every rank's
+        signal c, so it overlaps phase A of the later chunks."""
+        R, r = self.num_ranks, self.rank_idx
+        T_max = handle.num_max_tokens_per_rank
+        T = handle.topk_idx.shape[0]
+        rank_layout = R <= K                              # use_rank_layout, combine_utils.cuh:8-13
+        self._window_slots = min(R, K)
+        row_bytes = align(hidden * 2, 16) + align(K * 4, 16)
+        sym = self._window(row_bytes)
+        num_chunks = min(self._num_chunks(handle), 63)
+        key = ('xgmi', R, row_bytes, num_chunks)
+        plan = self._window_plan(handle, key)
+        if plan is None:
+            plan = CombinePlan(num_ranks=R, num_tokens=T, num_topk=K, expanded=expanded)
+            meta = handle.recv_src_metadata
+            recv_counts = handle._recv_counts
+            if recv_counts is None:
+                psum = [0] + [int(v) for v in handle.psum_num_recv_tokens_per_scaleup_rank.tolist()]
+                recv_counts = [psum[i + 1] - psum[i] for i in range(R)]
+            n_recv = sum(recv_counts)
+            plan.recv_counts = recv_counts
+            m = meta[:n_recv].to(torch.int64)
+            src_rank = torch.div(m[:, 1], K, rounding_mode='floor')
+            src_tok = m[:, 0] % T_max
+            slot = torch.full_like(src_rank, r) if rank_layout else m[:, 1] % K
+            out_rows = sym.data_bases_dev[src_rank] + (slot * T_max + src_tok) * row_bytes
+            table_b, row_of_lane = window_tables(handle.topk_idx, handle.num_experts, R, T_max, rank_layout)
+            B = (T_max + num_chunks - 1) // num_chunks
+            chunk_of_row = torch.div(src_tok, B, rounding_mode='floor')
+            plan.chunks = []
+            for c in range(num_chunks):
+                rows = _interleave_by_rank((chunk_of_row == c).nonzero().view(-1), src_rank, R)
+                if expanded:
+                    table_a = m[rows, 2:].to(torch.int32).contiguous()
+                    wtable_a = table_a
+                else:                                         # units are interleaved: explicit rows
+                    table_a = rows.to(torch.int32).view(-1, 1).contiguous()
+                    wtable_a = (rows.view(-1, 1) * K + torch.arange(K, device=rows.device).view(1, K)).to(
+                        torch.int32).contiguous()
+                lo, hi = c * B, min((c + 1) * B, T)
+                plan.chunks.append(ChunkPlan(lo, max(lo, hi), table_a, wtable_a, [], [],
+                                             table_b[lo:hi], row_of_lane[lo:hi]))
+                plan.chunks[-1].out_rows = out_rows[rows].contiguous()
+            plan.window_row_bytes = row_bytes
+            handle._combine_plans[key + (self._sym_gen,)] = plan
+        kern = self.kernels
+        w_off = align(hidden * 2, 16)
+        n_rows = self._window_slots * T_max
+        rows = sym.data[:n_rows * row_bytes].view(torch.bfloat16).view(n_rows, row_bytes // 2)
+        recv_wsrc = sym.data[:n_rows * row_bytes].view(torch.float32) if topk_weights is not None else None
+        pipelined = len(plan.chunks) > 1
+        sym.barrier(stream)                               # peers finished reading their windows
+        if pipelined:
+            if getattr(self, '_stream_b', None) is None:
+                self._stream_b = torch.cuda.Stream(device=self.device)
+            stream_b = self._stream_b
+            stream_b.wait_stream(stream)
+        for c, ch in enumerate(plan.chunks):
+            self._mark(stream)
+            kern.combine_reduce_scatter(x, ch.out_rows.shape[0], ch.out_rows, table=ch.table_a, row_weights=row_w,
+                                        wtable=ch.wtable_a, wsrc=wsrc,
+                                        num_weights=K if topk_weights is not None else 0,
+                                        weights_offset=w_off, stream=stream)
+            self._mark(stream)
+            sym.signal(1 + c, stream)
+        self._before_epilogue(previous_event_before_epilogue)
+        sb = stream_b if pipelined else stream
+        if pipelined and previous_event_before_epilogue is not None:
+            previous_event_before_epilogue.stream_wait(stream_b)
+        for c, ch in enumerate(plan.chunks):
+            sym.wait(1 + c, sb)
+            wtable_b = None
+            if topk_weights is not None:
+                wkey = (row_bytes // 4, w_off // 4)
+                if wkey not in ch.wtables:
+                    ch.wtables[wkey] = weight_table(ch.row_of_lane, *wkey)
+                wtable_b = ch.wtables[wkey]
+            lo, hi = ch.lo, ch.hi
+            self._mark(sb)
+            kern.combine_reduce(MODE_EPILOGUE, rows[:, :hidden], combined_x[lo:hi], hi - lo, table=ch.table_b,
+                                bias0=bias_0[lo:hi] if bias_0 is not None else None,
+                                bias1=bias_1[lo:hi] if bias_1 is not None else None,
+                                wtable=wtable_b, wsrc=recv_wsrc,
+                                out_weights=combined_w[lo:hi] if combined_w is not None else None, stream=sb)
+            self._mark(sb)
+        if pipelined:
+            stream.wait_stream(stream_b)
+
+    def _combine_xgmi_single(self, handle, x, row_w, wsrc, K, hidden, bias_0, bias_1, topk_weights,
+                             combined_x, combined_w, previous_event_before_epilogue, stream) -> None:
+        """Single-reduction combine over the symmetric windows (kDoExpandedSend, combine.cuh:177-213):
+        every valid expanded row of (token t, lane k) is copied unreduced -- with its gating weight in
+        a 16-byte tail when weights are given -- straight into the source rank's window row
+        k * T_max + t (per-top-k slot layout, buffer.hpp:616-633), then one EPILOGUE reduce per token
+        over its K rows (weighted: the legacy low-latency fma chain).  Chunked by source token like
+        _combine_xgmi, phase B of chunk c behind the split barrier of chunk c."""
+        R, r = self.num_ranks, self.rank_idx
+        T_max = handle.num_max_tokens_per_rank
+        T = handle.topk_idx.shape[0]
+        with_w = topk_weights is not None
+        self._window_slots = K
+        w_off = align(hidden * 2, 16)
+        row_bytes = w_off + 16                # the weight tail is always reserved: one window size per buffer
+        sym = self._window(row_bytes)
+        num_chunks = min(self._num_chunks(handle), 63)
+        key = ('xgmi-single', R, row_bytes, num_chunks)
+        plan = self._window_plan(handle, key)
+        if plan is None:
+            plan = CombinePlan(num_ranks=R, num_tokens=T, num_topk=K, expanded=True)
+            meta = handle.recv_src_metadata
+            recv_counts = handle._recv_counts
+            if recv_counts is None:
+                psum = [0] + [int(v) for v in handle.psum_num_recv_tokens_per_scaleup_rank.tolist()]
+                recv_counts = [psum[i + 1] - psum[i] for i in range(R)]
+            m = meta[:sum(recv_counts)].to(torch.int64)
+            slots = m[:, 2:]
+            i_idx, k_idx = (slots >= 0).nonzero(as_tuple=True)           # every valid (received token, lane)
+            rows_exp = slots[i_idx, k_idx]
+            src_rank = torch.div(m[i_idx, 1], K, rounding_mode='floor')
+            src_tok = m[i_idx, 0] % T_max
+            out_rows = sym.data_bases_dev[src_rank] + (k_idx * T_max + src_tok) * row_bytes
+            k_all = torch.arange(K, device=handle.topk_idx.device).view(1, K)
+            t_all = torch.arange(T, device=handle.topk_idx.device).view(T, 1)
+            table_b = torch.where(handle.topk_idx >= 0, k_all * T_max + t_all, torch.full_like(handle.topk_idx, -1))
+            table_b = table_b.to(torch.int32).contiguous()
+            B = (T_max + num_chunks - 1) // num_chunks
+            chunk_of = torch.div(src_tok, B, rounding_mode='floor')
+            plan.chunks = []
+            for c in range(num_chunks):
+                sel = _interleave_by_rank((chunk_of == c).nonzero().view(-1), src_rank, R)
+                lo, hi = c * B, min((c + 1) * B, T)
+                ch = ChunkPlan(lo, max(lo, hi), rows_exp[sel].to(torch.int32).view(-1, 1).contiguous(), None, [], [],
+                               table_b[lo:hi], table_b[lo:hi])
+                ch.out_rows = out_rows[sel].contiguous()
+                plan.chunks.append(ch)
+            plan.window_row_bytes = row_bytes
+            handle._combine_plans[key + (self._sym_gen,)] = plan
+        kern = self.kernels
+        n_rows = K * T_max
+        win = sym.data[:n_rows * row_bytes]
+        rows = win.view(torch.bfloat16).view(n_rows, row_bytes // 2)
+        win_w = win.view(torch.float32).view(K, T_max, row_bytes // 4)[:, :, w_off // 4] if with_w else None
+        recv_w = torch.empty((K, T_max), dtype=torch.float32, device=x.device) if with_w else None
+        pipelined = len(plan.chunks) > 1
+        sym.barrier(stream)                               # peers finished reading their windows
+        if pipelined:
+            if getattr(self, '_stream_b', None) is None:
+                self._stream_b = torch.cuda.Stream(device=self.device)
+            stream_b = self._stream_b
+            stream_b.wait_stream(stream)
+        for c, ch in enumerate(plan.chunks):
+            self._mark(stream)
+            kern.combine_reduce_scatter(x, ch.out_rows.shape[0], ch.out_rows, table=ch.table_a,
+                                        wtable=ch.table_a if with_w else None, wsrc=wsrc if with_w else None,
+                                        num_weights=1 if with_w else 0, weights_offset=w_off, stream=stream)
+            self._mark(stream)
+            sym.signal(1 + c, stream)
+        self._before_epilogue(previous_event_before_epilogue)
+        sb = stream_b if pipelined else stream
+        if pipelined and previous_event_before_epilogue is not None:
+            previous_event_before_epilogue.stream_wait(stream_b)
+        for c, ch in enumerate(plan.chunks):
+            sym.wait(1 + c, sb)
+            lo, hi = ch.lo, ch.hi
+            rw = None
+            if with_w:
+                with torch.cuda.stream(sb):
+                    recv_w[:, lo:hi].copy_(win_w[:, lo:hi])      # the chunk's weights out of the row tails
+                rw = recv_w.view(-1)
+            self._mark(sb)
+            kern.combine_reduce(MODE_EPILOGUE, rows[:, :hidden], combined_x[lo:hi], hi - lo, table=ch.table_b,
+                                row_weights=rw if row_w is not None else None,
+                                bias0=bias_0[lo:hi] if bias_0 is not None else None,
+                                bias1=bias_1[lo:hi] if bias_1 is not None else None,
+                                wtable=ch.table_b if with_w else None, wsrc=rw,
+                                out_weights=combined_w[lo:hi] if combined_w is not None else None, stream=sb)
+            self._mark(sb)
+        if pipelined:
+            stream.wait_stream(stream_b)
+            if recv_w is not None:
+                recv_w.record_stream(stream_b)

@@ -403,7 +403,7 @@ def test_rank_with_no_tokens(world):
 
 def test_interleave_by_rank_is_a_round_robin_permutation():
     """xGMI phase-A units are reordered round-robin over destination ranks (every link busy at once)."""
-    from deepep_amd.buffer import _interleave_by_rank
+    from deepep_amd.exchange import _interleave_by_rank
     dest = torch.tensor([0] * 5 + [1] * 2 + [3] * 4)           # per received row, grouped by rank
     units = torch.tensor([0, 1, 2, 4, 5, 6, 7, 9, 10])          # a chunk's rows (ascending)
     out = _interleave_by_rank(units, dest, 4)

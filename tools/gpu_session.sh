@@ -35,6 +35,7 @@ for step in "$@"; do
         kphase) run kphase 300 python tools/kphase.py ;;
         kcu)    run kcu 300 python tools/kcu.py ;;
         cumask) run cumask 120 python tools/probe_cumask.py ;;
+        probeld) run probeld 300 python tools/probe_ld.py ;;
         pmclist) run pmclist 120 rocprofv3 --list-avail ;;
         smi)    run smi 60 rocm-smi --showclocks --showpower --showtemp ;;
         bench4gloo) export DEEPEP_BENCH_BACKEND=gloo; run bench4gloo 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29657 bench.py --gpus 4 --steps 4 --warmup 2; unset DEEPEP_BENCH_BACKEND ;;

@@ -128,6 +128,10 @@ __device__ __forceinline__ u32x4 acc_pack(const float* acc) {
 // 164.6 us, plain 166.2 us, nt 171.8 us for the gather + store pattern; write-only 8.0 / 7.4 /
 // 5.9 TB/s.  sc1 is the default.
 constexpr int kAuxNT = 2, kAuxSC1 = 16;      // (sc0 = 1)
+// Stores into a peer's symmetric window (the xGMI transport) are system-scope write-through
+// (sc0 sc1): they must be visible to another GPU once the kernel has completed, whatever MTYPE the
+// importing process maps the window with.  Same speed as sc1 (tools/probe_ld.hip).
+constexpr int kAuxSys = 17;
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void* row, int bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(row), 0, bytes, 0x00020000);
@@ -201,7 +205,11 @@ combine_rows_kernel(const Params p) {
         float* const ow = p.out_rows != nullptr
                               ? reinterpret_cast<float*>(reinterpret_cast<char*>(out_row) + p.weights_offset)
                               : p.out_weights + u * p.out_weights_stride;
-        ow[lane] = i >= 0 ? p.wsrc[i] : 0.0f;
+        const float v = i >= 0 ? p.wsrc[i] : 0.0f;
+        if (p.out_rows != nullptr)              // a peer's window: system scope, as the row stores
+            __hip_atomic_store(ow + lane, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        else
+            ow[lane] = v;
     }
 
     int vidx[kVPT];
@@ -360,6 +368,7 @@ template <int kMode, bool kWeighted, int kVPT, bool kFull>
 void launch_aux(const Params& p, const Shape& sh, hipStream_t stream) {
     if (sh.policy == 0) launch_lds<kMode, kWeighted, kVPT, kFull, 0>(p, sh.lds, sh.waves, sh.group, stream);
     else if (sh.policy == 1) launch_lds<kMode, kWeighted, kVPT, kFull, kAuxNT>(p, sh.lds, sh.waves, sh.group, stream);
+    else if (sh.policy == 3) launch_lds<kMode, kWeighted, kVPT, kFull, kAuxSys>(p, sh.lds, sh.waves, sh.group, stream);
     else launch_lds<kMode, kWeighted, kVPT, kFull, kAuxSC1>(p, sh.lds, sh.waves, sh.group, stream);
 }
 
@@ -547,7 +556,7 @@ int launch_combine(int mode, int weighted, const Params& p, deepep_stream_t stre
     sh.vpt = g_config.vec_per_lane > 0 ? g_config.vec_per_lane : (nvec >= 128 ? 2 : 1);
     if (sh.vpt != 1 && sh.vpt != 2) sh.vpt = 2;
     sh.lds = g_config.stage_lds >= 0 ? g_config.stage_lds != 0 : true;
-    sh.policy = g_config.store_policy >= 0 ? g_config.store_policy : 2;
+    sh.policy = p.out_rows != nullptr ? 3 : (g_config.store_policy >= 0 ? g_config.store_policy : 2);
     // units_per_block 4 / 8 forces the workgroup shape; 0 = automatic
     sh.waves = p.units_per_block == 4 ? 4 : (p.units_per_block == 8 ? 8 : (mode == DEEPEP_MODE_LOCAL ? 4 : 8));
     sh.group = g_config.rows_in_flight > 0 ? g_config.rows_in_flight : 8;

@@ -258,6 +258,13 @@ class ExchangeMixin:
         rows = sym.data[:n_rows * row_bytes].view(torch.bfloat16).view(n_rows, row_bytes // 2)
         recv_wsrc = sym.data[:n_rows * row_bytes].view(torch.float32) if topk_weights is not None else None
         pipelined = len(plan.chunks) > 1
+        wkey = (row_bytes // 4, w_off // 4)
+        if topk_weights is not None:
+            # built here, on the caller's stream, BEFORE the phase-B stream forks off it: a table built
+            # inside the phase-B loop would be written on one stream and read on the other
+            for ch in plan.chunks:
+                if wkey not in ch.wtables:
+                    ch.wtables[wkey] = weight_table(ch.row_of_lane, *wkey)
         sym.barrier(stream)                               # peers finished reading their windows
         if pipelined:
             if getattr(self, '_stream_b', None) is None:
@@ -278,12 +285,7 @@ class ExchangeMixin:
             previous_event_before_epilogue.stream_wait(stream_b)
         for c, ch in enumerate(plan.chunks):
             sym.wait(1 + c, sb)
-            wtable_b = None
-            if topk_weights is not None:
-                wkey = (row_bytes // 4, w_off // 4)
-                if wkey not in ch.wtables:
-                    ch.wtables[wkey] = weight_table(ch.row_of_lane, *wkey)
-                wtable_b = ch.wtables[wkey]
+            wtable_b = ch.wtables[wkey] if topk_weights is not None else None
             lo, hi = ch.lo, ch.hi
             self._mark(sb)
             kern.combine_reduce(MODE_EPILOGUE, rows[:, :hidden], combined_x[lo:hi], hi - lo, table=ch.table_b,

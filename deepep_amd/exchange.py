@@ -58,6 +58,12 @@ class ExchangeMixin:
         w_elems = 0 if topk_weights is None else align(K * 4, 16) // 2
         row_elems = hidden + w_elems
         pipelined = len(plan.chunks) > 1 and self.use_cuda
+        wkey = (row_elems // 2, hidden // 2)
+        if w_elems:
+            # every table phase B reads is built before the phase-B stream forks off this one
+            for ch in plan.chunks:
+                if wkey not in ch.wtables:
+                    ch.wtables[wkey] = weight_table(ch.row_of_lane, *wkey)
         if pipelined:
             if getattr(self, '_stream_b', None) is None:
                 self._stream_b = torch.cuda.Stream(device=self.device)
@@ -88,13 +94,8 @@ class ExchangeMixin:
                 sb = stream_b if pipelined else stream
                 if work is not None:
                     work.wait()
-                wtable_b, recv_wsrc = None, None
-                if w_elems:
-                    key = (row_elems // 2, hidden // 2)
-                    if key not in ch.wtables:
-                        ch.wtables[key] = weight_table(ch.row_of_lane, *key)
-                    wtable_b = ch.wtables[key]
-                    recv_wsrc = recv.view(torch.float32).view(-1)
+                wtable_b = ch.wtables[wkey] if w_elems else None
+                recv_wsrc = recv.view(torch.float32).view(-1) if w_elems else None
                 lo, hi = ch.lo, ch.hi
                 self._mark(sb)
                 kern.combine_reduce(MODE_EPILOGUE, recv[:, :hidden], combined_x[lo:hi], hi - lo, table=ch.table_b,

@@ -222,7 +222,8 @@ int deepep_sym_wait(const uint64_t* peer_flags, int rank, int num_ranks, int slo
  * combine.cuh:96-106, 125-176, 215-226): the reduce of deepep_combine_reduce(DEEPEP_MODE_LOCAL, ...)
  * with unit u's bf16 row stored at byte address out_rows[u] (any rank's window, 16-byte aligned)
  * and, when num_weights > 0, its top-k weights (the wtable / wsrc pass-through rule above) at
- * out_rows[u] + weights_offset. */
+ * out_rows[u] + weights_offset.  All these stores are system-scope write-through (sc0 sc1), so
+ * they are visible to the owning GPU once the kernel has completed. */
 int deepep_combine_reduce_scatter(int weighted,
                                   const void* src, int64_t num_src_rows, int64_t src_row_stride,
                                   const int32_t* table, int64_t table_stride, int table_width,

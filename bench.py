@@ -498,26 +498,37 @@ def main():
     if args.fp8_dispatch:
         from deepep_amd.utils import per_token_cast_to_fp8
         x_disp = per_token_cast_to_fp8(x_disp)
-    buf.dispatch(x_disp, topk_idx=topk_idx, topk_weights=topk_w, num_experts=E, do_expand=True)
-    torch.cuda.synchronize()
-    t_d = time.perf_counter()
-    for _ in range(n_disp):
-        buf.dispatch(x_disp, topk_idx=topk_idx, topk_weights=topk_w, num_experts=E, do_expand=True)
-    torch.cuda.synchronize()
-    t_d = (time.perf_counter() - t_d) / n_disp
-    # cached handle: no routing kernels, no host sync (pack -> exchange -> copy)
-    torch.cuda.synchronize()
-    t_c = time.perf_counter()
-    for _ in range(n_disp):
-        buf.dispatch(x_disp, topk_weights=topk_w, do_expand=True, handle=handle)
-    torch.cuda.synchronize()
-    t_c = (time.perf_counter() - t_c) / n_disp
+
+    def time_dispatch():
+        _, _, _, h, _ = buf.dispatch(x_disp, topk_idx=topk_idx, topk_weights=topk_w, num_experts=E, do_expand=True)
+        torch.cuda.synchronize()
+        t_d = time.perf_counter()
+        for _ in range(n_disp):
+            buf.dispatch(x_disp, topk_idx=topk_idx, topk_weights=topk_w, num_experts=E, do_expand=True)
+        torch.cuda.synchronize()
+        t_d = (time.perf_counter() - t_d) / n_disp
+        # cached handle: no routing kernels, no host sync (pack -> exchange -> copy)
+        t_c = time.perf_counter()
+        for _ in range(n_disp):
+            buf.dispatch(x_disp, topk_weights=topk_w, do_expand=True, handle=h)
+        torch.cuda.synchronize()
+        return t_d, (time.perf_counter() - t_c) / n_disp
+
+    t_d, t_c = time_dispatch()
     elem = 1 if args.fp8_dispatch else 2
     disp_bytes = T * H * elem + handle.num_expanded_tokens * H * elem     # read x once, write every expanded row
     dispatch = dict(ms=round(t_d * 1e3, 3), gbps=round(disp_bytes / t_d / 1e9, 1),
                     cached_ms=round(t_c * 1e3, 3), cached_gbps=round(disp_bytes / t_c / 1e9, 1),
+                    transport=buf.transport if world > 1 else 'local',
                     note='ElasticBuffer.dispatch(do_expand=True) wall time incl. host count syncs; cached = '
                          'dispatch(handle=...) (no sync); bytes = x read once + expanded rows written')
+    if world > 1 and buf.transport != 'xgmi' and os.environ.get('DEEPEP_BENCH_XGMI', '1') != '0':
+        # the same dispatch with the rows pushed straight into the peers' symmetric windows
+        buf.transport = 'xgmi'
+        t_dx, t_cx = time_dispatch()
+        buf.transport = 'rccl'
+        dispatch.update(xgmi_ms=round(t_dx * 1e3, 3), xgmi_cached_ms=round(t_cx * 1e3, 3),
+                        xgmi_cached_gbps=round(disp_bytes / t_cx / 1e9, 1))
     del x_disp
 
     loopback = None

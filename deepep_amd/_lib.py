@@ -11,7 +11,7 @@ from typing import Optional
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('DEEPEP_AMD_LIB', os.path.join(_HERE, 'libdeepep_amd.so'))
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 MODE_LOCAL, MODE_EPILOGUE, MODE_FUSED = 0, 1, 2
 
@@ -44,7 +44,7 @@ SIGNATURES = {
     'deepep_dispatch_route': (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P]),
     'deepep_dispatch_expert_counts': (_I, [_P, _I, _I, _I, _P, _P]),
     'deepep_dispatch_pack': (_I, [_P, _I64, _I, _P, _I64, _I, _P, _P, _I, _I, _I, _P, _P, _I,
-                                  _P, _I64, _I, _I, _I, _I, _P]),
+                                  _P, _P, _I64, _I, _I, _I, _I, _P]),
     'deepep_dispatch_count': (_I, [_P, _I64, _I, _I, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P]),
     'deepep_dispatch_scan': (_I, [_P, _I, _I, _I, _I, _P, _P, _P]),
     'deepep_dispatch_slots': (_I, [_P, _I64, _I, _I, _I, _I, _I, _P, _P, _P]),

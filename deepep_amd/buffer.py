@@ -367,11 +367,17 @@ class ElasticBuffer(ExchangeMixin):
             # dispatch is then pack -> exchange -> copy, with no host sync (graph-capturable at EP = 1),
             # as the reference's cached mode skips its notify phase (elastic.py:855-1033).
             cached = handle if handle is not None and handle._send_counts is not None else None
+            # EP > 1 over xGMI: the pack kernel stores every row straight into its destination's
+            # symmetric window (dispatch.cuh:373-392's push), no RCCL exchange for the rows
+            use_xgmi = R > 1 and self.transport == 'xgmi' and self.use_cuda
+            peer_offsets = None
             if cached is not None:
                 _assert(do_expand == handle.do_expand, 'do_expand must match the cached handle')
                 dst_slot = cached.dst_buffer_slot_idx
                 send_counts_l, recv_counts_l = cached._send_counts, cached._recv_counts
                 send_offsets = cached._send_offsets
+                peer_offsets = getattr(cached, '_peer_offsets', None)
+                use_xgmi = use_xgmi and peer_offsets is not None      # a handle made by the RCCL path
             else:
                 # --- send side: destination slots (deterministic ranks), one packed row per (token, dest)
                 dst_slot = torch.empty((T, R), dtype=torch.int32, device=dev)
@@ -380,34 +386,57 @@ class ElasticBuffer(ExchangeMixin):
                 expert_hist = torch.empty((num_experts,), dtype=torch.int32, device=dev)
                 kern.dispatch_expert_counts(idx64, num_experts, expert_hist, stream=stream)
                 # notify (dispatch.cuh:79-258): every destination gets [tokens | tokens per local expert]
-                # from this rank; one exchange and ONE host sync size every receive-side allocation
+                # from this rank; one exchange and ONE host sync size every receive-side allocation.
+                # The xGMI transport pushes rows straight into the peers' windows, so every rank needs
+                # the whole [source, destination] count matrix (its rows' offset in a peer's window is
+                # what the lower source ranks send there): the notify is all-gathered instead.
                 notify = torch.cat([send_counts.view(R, 1), expert_hist.view(R, epr)], dim=1)
                 if R == 1:
                     recv_notify = notify
+                elif use_xgmi:
+                    everyone = torch.empty((R * R, 1 + epr), dtype=notify.dtype, device=dev)
+                    self._a2a(everyone, notify.repeat(R, 1))
+                    recv_notify = everyone.view(R, R, 1 + epr)[:, r]
                 else:
                     recv_notify = torch.empty_like(notify)
                     self._a2a(recv_notify, notify)
-                host = [int(v) for v in torch.cat([send_counts, recv_notify.view(-1)]).tolist()]   # host sync
+                host = [int(v) for v in torch.cat([send_counts, (everyone if R > 1 and use_xgmi else
+                                                                 recv_notify).reshape(-1)]).tolist()]   # host sync
                 send_counts_l = host[:R]
-                rows = [host[R + i * (1 + epr): R + (i + 1) * (1 + epr)] for i in range(R)]
+                if R > 1 and use_xgmi:
+                    grid = [[host[R + (s * R + d) * (1 + epr): R + (s * R + d + 1) * (1 + epr)] for d in range(R)]
+                            for s in range(R)]
+                    rows = [grid[s][r] for s in range(R)]
+                    peer_offsets = torch.tensor([sum(grid[s][d][0] for s in range(r)) for d in range(R)],
+                                                dtype=torch.int32).to(dev, non_blocking=True)
+                else:
+                    rows = [host[R + i * (1 + epr): R + (i + 1) * (1 + epr)] for i in range(R)]
                 recv_counts_l = [row[0] for row in rows]
                 expert_counts_l = [sum(row[1 + e] for row in rows) for e in range(epr)]
                 recv_counts_t = recv_notify[:, 0].contiguous()
                 send_offsets = (torch.cumsum(send_counts, 0) - send_counts).to(torch.int32)
             N = sum(recv_counts_l)
             x_bytes = x.contiguous().view(torch.uint8).view(T, H * x.element_size())
-            sf_bytes = sf.contiguous().view(torch.uint8).view(T, -1) if sf is not None else None
+            sf_bytes = sf.contiguous().view(torch.uint8).view(T, sf.shape[1] * sf.element_size()) if sf is not None else None
             # One rank: nothing is exchanged, so the packed rows carry only the routing metadata and
             # the copy reads x (and the scale factors) once, straight from the caller's tensors.
             direct = R == 1
             layout = (RowLayout.make(0, 0, K) if direct else
                       RowLayout.make(x_bytes.shape[1], sf_bytes.shape[1] if sf is not None else 0, K))
-            packed = torch.empty((sum(send_counts_l), layout.row_bytes), dtype=torch.uint8, device=dev)
-            kern.dispatch_pack(x_bytes[:, :0] if direct else x_bytes, None if direct else sf_bytes, idx64, w,
-                               r * num_max_tokens_per_rank, dst_slot, send_offsets, packed, layout, stream=stream)
+            if use_xgmi:
+                sym = self._window(layout.row_bytes, slots=R, rows_per_slot=num_max_tokens_per_rank)
+                sym.barrier(stream)                               # peers finished reading their windows
+                kern.dispatch_pack(x_bytes, sf_bytes, idx64, w, r * num_max_tokens_per_rank, dst_slot,
+                                   peer_offsets, None, layout, dest_bases=sym.data_bases_dev, stream=stream)
+                sym.barrier(stream)                               # every row landed
+                recv_packed = sym.data[:N * layout.row_bytes].view(N, layout.row_bytes)
+            else:
+                packed = torch.empty((sum(send_counts_l), layout.row_bytes), dtype=torch.uint8, device=dev)
+                kern.dispatch_pack(x_bytes[:, :0] if direct else x_bytes, None if direct else sf_bytes, idx64, w,
+                                   r * num_max_tokens_per_rank, dst_slot, send_offsets, packed, layout, stream=stream)
             if R == 1:
                 recv_packed = packed
-            else:
+            elif not use_xgmi:
                 recv_packed = torch.empty((N, layout.row_bytes), dtype=torch.uint8, device=dev)
                 self._a2a(recv_packed, packed, recv_counts_l, send_counts_l)
             # --- receive side (dispatch_copy_epilogue_impl): metadata, expert layout, copies
@@ -490,6 +519,7 @@ class ElasticBuffer(ExchangeMixin):
             handle._recv_counts = recv_counts_l
             handle._send_counts = send_counts_l
             handle._send_offsets = send_offsets
+            handle._peer_offsets = peer_offsets
             handle._recv_topk_idx = recv_idx64
         out_x = (out_x, out_sf) if out_sf is not None else out_x
         return out_x, out_idx, out_w, handle, EventOverlap(event)

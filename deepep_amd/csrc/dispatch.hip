@@ -123,35 +123,59 @@ expert_hist_kernel(const int64_t* __restrict__ topk_idx, int64_t n, int E, int32
 
 // ---------------------------------------------------------------- pack: one wave per token
 // packed row layout (bytes): [x | sf @sf_off | topk_idx (int64) @idx_off | weights @w_off | src @src_off]
+// Row of (token t, destination r): base_r + (send_offsets[r] + dst_slot[t][r]) * row_bytes, base_r =
+// dest_bases[r] (a peer's symmetric window: the xGMI transport, system-scope write-through stores,
+// dispatch.cuh:373-392's push) or `packed` for every r (one local buffer for the RCCL all-to-all).
+template <bool kPeer>
+__device__ __forceinline__ void put16(uint8_t* row, int off, const u32x4& v, int row_bytes) {
+    if constexpr (kPeer) {
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(row, 0, row_bytes, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 17);          // sc0 sc1: system scope
+    } else {
+        *reinterpret_cast<u32x4*>(row + off) = v;
+    }
+}
+
+template <bool kPeer, typename V>
+__device__ __forceinline__ void put(V* p, V v) {
+    if constexpr (kPeer) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else *p = v;
+}
+
+template <bool kPeer>
 __global__ void __launch_bounds__(64)
 pack_kernel(const uint8_t* __restrict__ x, int64_t x_stride, int x_bytes,
             const uint8_t* __restrict__ sf, int64_t sf_stride, int sf_bytes,
             const int64_t* __restrict__ topk_idx, const float* __restrict__ topk_weights, int K,
             int32_t src_base, const int32_t* __restrict__ dst_slot, const int32_t* __restrict__ send_offsets, int R,
-            uint8_t* __restrict__ packed, int64_t row_bytes, int sf_off, int idx_off, int w_off, int src_off) {
+            uint8_t* __restrict__ packed, const uint64_t* __restrict__ dest_bases, int64_t row_bytes,
+            int sf_off, int idx_off, int w_off, int src_off) {
     const int t = blockIdx.x, lane = threadIdx.x;
-    // lane r holds the destination row for rank r; the set bits of `dmask` are the destinations
-    int64_t my_row = -1;
+    // lane r holds the byte address of the destination row for rank r (0: not routed to r)
+    uint64_t my_row = 0;
     if (lane < R) {
         const int32_t s = dst_slot[static_cast<int64_t>(t) * R + lane];
-        if (s >= 0) my_row = static_cast<int64_t>(send_offsets[lane]) + s;
+        if (s >= 0) {
+            const uint64_t base = kPeer ? dest_bases[lane] : reinterpret_cast<uint64_t>(packed);
+            my_row = base + static_cast<uint64_t>(static_cast<int64_t>(send_offsets[lane]) + s) * row_bytes;
+        }
     }
-    const uint64_t dmask = __ballot(my_row >= 0);
+    const uint64_t dmask = __ballot(my_row != 0);
     auto row_of = [&](int r) -> uint8_t* {
-        const int64_t lo = __builtin_amdgcn_readlane(static_cast<int>(my_row & 0xffffffff), r);
-        const int64_t hi = __builtin_amdgcn_readlane(static_cast<int>(my_row >> 32), r);
-        return packed + ((hi << 32) | (lo & 0xffffffff)) * row_bytes;
+        const uint64_t lo = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(my_row & 0xffffffffu), r));
+        const uint64_t hi = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(my_row >> 32), r));
+        return reinterpret_cast<uint8_t*>((hi << 32) | lo);
     };
     const u32x4* xs = reinterpret_cast<const u32x4*>(x + t * x_stride);
     for (int v = lane; v < x_bytes / 16; v += 64) {
         const u32x4 val = __builtin_nontemporal_load(xs + v);
         for (uint64_t m = dmask; m; m &= m - 1)
-            reinterpret_cast<u32x4*>(row_of(__builtin_ctzll(m)))[v] = val;
+            put16<kPeer>(row_of(__builtin_ctzll(m)), v * 16, val, static_cast<int>(row_bytes));
     }
     for (int v = lane; v < sf_bytes / 4; v += 64) {
         const uint32_t val = reinterpret_cast<const uint32_t*>(sf + t * sf_stride)[v];
         for (uint64_t m = dmask; m; m &= m - 1)
-            reinterpret_cast<uint32_t*>(row_of(__builtin_ctzll(m)) + sf_off)[v] = val;
+            put<kPeer>(reinterpret_cast<uint32_t*>(row_of(__builtin_ctzll(m)) + sf_off) + v, val);
     }
     int64_t e = 0;
     float w = 0.0f;
@@ -162,10 +186,10 @@ pack_kernel(const uint8_t* __restrict__ x, int64_t x_stride, int x_bytes,
     for (uint64_t m = dmask; m; m &= m - 1) {
         uint8_t* row = row_of(__builtin_ctzll(m));
         if (lane < K) {
-            reinterpret_cast<int64_t*>(row + idx_off)[lane] = e;
-            reinterpret_cast<float*>(row + w_off)[lane] = w;
+            put<kPeer>(reinterpret_cast<int64_t*>(row + idx_off) + lane, e);
+            put<kPeer>(reinterpret_cast<float*>(row + w_off) + lane, w);
         }
-        if (lane == 0) *reinterpret_cast<int32_t*>(row + src_off) = src_base + t;
+        if (lane == 0) put<kPeer>(reinterpret_cast<int32_t*>(row + src_off), static_cast<int32_t>(src_base + t));
     }
 }
 
@@ -410,18 +434,27 @@ int deepep_dispatch_pack(const void* x, int64_t x_row_stride_bytes, int x_bytes,
                          const void* sf, int64_t sf_row_stride_bytes, int sf_bytes,
                          const int64_t* topk_idx, const float* topk_weights, int num_tokens, int num_topk,
                          int32_t src_base, const int32_t* dst_slot, const int32_t* send_offsets, int num_ranks,
-                         void* packed, int64_t row_bytes, int sf_off, int idx_off, int w_off, int src_off,
-                         deepep_stream_t stream) {
+                         void* packed, const uint64_t* dest_bases, int64_t row_bytes,
+                         int sf_off, int idx_off, int w_off, int src_off, deepep_stream_t stream) {
     if (num_tokens == 0) return DEEPEP_OK;
     if (num_tokens < 0 || num_topk < 1 || num_topk > 32 || num_ranks < 1 || num_ranks > 64 || x_bytes % 16 ||
-        sf_bytes % 4 || row_bytes % 16 || !a16(x) || !a16(packed) || x_row_stride_bytes % 16 || idx_off % 8 ||
-        w_off % 4 || src_off % 4 || (sf_bytes > 0 && sf == nullptr))
+        sf_bytes % 4 || row_bytes % 16 || !a16(x) || (dest_bases == nullptr && !a16(packed)) ||
+        x_row_stride_bytes % 16 || idx_off % 8 || w_off % 4 || src_off % 4 || (sf_bytes > 0 && sf == nullptr) ||
+        (dest_bases == nullptr && packed == nullptr))
         return deepep_amd_set_error(DEEPEP_ERR_INVALID_ARG, "dispatch_pack: invalid arguments or alignment");
-    hipLaunchKernelGGL(pack_kernel, dim3(num_tokens), dim3(64), 0, reinterpret_cast<hipStream_t>(stream),
-                       static_cast<const uint8_t*>(x), x_row_stride_bytes, x_bytes,
-                       static_cast<const uint8_t*>(sf), sf_row_stride_bytes, sf_bytes,
-                       topk_idx, topk_weights, num_topk, src_base, dst_slot, send_offsets, num_ranks,
-                       static_cast<uint8_t*>(packed), row_bytes, sf_off, idx_off, w_off, src_off);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (dest_bases != nullptr)
+        hipLaunchKernelGGL(pack_kernel<true>, dim3(num_tokens), dim3(64), 0, s,
+                           static_cast<const uint8_t*>(x), x_row_stride_bytes, x_bytes,
+                           static_cast<const uint8_t*>(sf), sf_row_stride_bytes, sf_bytes,
+                           topk_idx, topk_weights, num_topk, src_base, dst_slot, send_offsets, num_ranks,
+                           static_cast<uint8_t*>(packed), dest_bases, row_bytes, sf_off, idx_off, w_off, src_off);
+    else
+        hipLaunchKernelGGL(pack_kernel<false>, dim3(num_tokens), dim3(64), 0, s,
+                           static_cast<const uint8_t*>(x), x_row_stride_bytes, x_bytes,
+                           static_cast<const uint8_t*>(sf), sf_row_stride_bytes, sf_bytes,
+                           topk_idx, topk_weights, num_topk, src_base, dst_slot, send_offsets, num_ranks,
+                           static_cast<uint8_t*>(packed), dest_bases, row_bytes, sf_off, idx_off, w_off, src_off);
     return launch_status("dispatch_pack");
 }
 

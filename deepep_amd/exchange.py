@@ -11,7 +11,7 @@ The per-token arithmetic is the reference's (combine.cuh, combine_reduce_epilogu
 /root/reference); the exchange design is DESIGN.md section 5.
 """
 import itertools
-from typing import List
+from typing import List, Optional
 
 import torch
 import torch.distributed as dist
@@ -165,13 +165,13 @@ class ExchangeMixin:
                 send.record_stream(stream_b)
 
     # ------------------------------------------------------------------ EP > 1 over xGMI windows
-    def _window(self, row_bytes: int):
+    def _window(self, row_bytes: int, slots: Optional[int] = None, rows_per_slot: Optional[int] = None):
         """The symmetric window: `num_bytes` (the reference's symmetric buffer size, buffer.hpp:589-686,
         which holds every combine layout of the declared shape: min(R, K) or K receive slots x T_max
         rows) or more if a call needs it; allocated on first use (collective: every rank reaches the
         same combine)."""
-        slots = self._window_slots
-        need = slots * self.num_max_tokens_per_rank * row_bytes
+        slots = self._window_slots if slots is None else slots
+        need = slots * (rows_per_slot or self.num_max_tokens_per_rank) * row_bytes
         if self._sym is not None and self._sym.data_bytes >= need:
             return self._sym
         from .symmetric import SymmetricBuffer
@@ -216,7 +216,7 @@ class ExchangeMixin:
         rank_layout = R <= K                              # use_rank_layout, combine_utils.cuh:8-13
         self._window_slots = min(R, K)
         row_bytes = align(hidden * 2, 16) + align(K * 4, 16)
-        sym = self._window(row_bytes)
+        sym = self._window(row_bytes, rows_per_slot=T_max)
         num_chunks = min(self._num_chunks(handle), 63)
         key = ('xgmi', R, row_bytes, num_chunks)
         plan = self._window_plan(handle, key)
@@ -313,7 +313,7 @@ class ExchangeMixin:
         self._window_slots = K
         w_off = align(hidden * 2, 16)
         row_bytes = w_off + 16                # the weight tail is always reserved: one window size per buffer
-        sym = self._window(row_bytes)
+        sym = self._window(row_bytes, rows_per_slot=T_max)
         num_chunks = min(self._num_chunks(handle), 63)
         key = ('xgmi-single', R, row_bytes, num_chunks)
         plan = self._window_plan(handle, key)

@@ -170,15 +170,19 @@ class HipKernels:
         _lib.check(rc, 'dispatch_expert_counts')
 
     def dispatch_pack(self, x_bytes, sf_bytes, topk_idx, topk_weights, src_base, dst_slot, send_offsets,
-                      packed, layout: RowLayout, stream=None):
-        """x_bytes / sf_bytes: [T, bytes] uint8 views (rows may be strided)."""
+                      packed, layout: RowLayout, dest_bases=None, stream=None):
+        """x_bytes / sf_bytes: [T, bytes] uint8 views (rows may be strided).  dest_bases: optional
+        int64 [R] device tensor of per-destination buffer addresses (peer windows) instead of `packed`."""
         T, K = topk_idx.shape
+        if dest_bases is not None:
+            _require(dest_bases.is_cuda and dest_bases.dtype == torch.int64 and dest_bases.is_contiguous() and
+                     dest_bases.numel() == dst_slot.shape[1], 'dest_bases must be int64 [num_ranks] on the GPU')
         rc = self.lib.deepep_dispatch_pack(
             ptr(x_bytes), x_bytes.stride(0) if T else layout.x_bytes, layout.x_bytes,
             ptr(sf_bytes), sf_bytes.stride(0) if sf_bytes is not None and T else 0, layout.sf_bytes,
             ptr(topk_idx), ptr(topk_weights), T, K, src_base, ptr(dst_slot), ptr(send_offsets),
-            dst_slot.shape[1], ptr(packed), layout.row_bytes, layout.sf_off, layout.idx_off, layout.w_off,
-            layout.src_off, _stream_handle(stream))
+            dst_slot.shape[1], ptr(packed), ptr(dest_bases), layout.row_bytes, layout.sf_off, layout.idx_off,
+            layout.w_off, layout.src_off, _stream_handle(stream))
         _lib.check(rc, 'dispatch_pack')
 
     def dispatch_count(self, packed, layout: RowLayout, num_recv, rank, num_local_experts, rank_psum, meta,

@@ -45,7 +45,7 @@ extern "C" {
 
 typedef struct ihipStream_t* deepep_stream_t;   /* == hipStream_t */
 
-#define DEEPEP_AMD_ABI_VERSION 6
+#define DEEPEP_AMD_ABI_VERSION 7
 
 #define DEEPEP_OK               0
 #define DEEPEP_ERR_INVALID_ARG  (-1)
@@ -147,14 +147,16 @@ int deepep_dispatch_route(const int64_t* topk_idx, int num_tokens, int num_topk,
 int deepep_dispatch_expert_counts(const int64_t* topk_idx, int num_tokens, int num_topk, int num_experts,
                                   int32_t* counts, deepep_stream_t stream);
 
-/* Write packed row send_offsets[r] + dst_slot[t][r] for every (token t, destination r);
- * src_global_idx = src_base + t.  topk_weights may be NULL (zeros are sent). */
+/* Write packed row send_offsets[r] + dst_slot[t][r] for every (token t, destination r), in `packed`
+ * (dest_bases NULL: one local buffer for an all-to-all) or in rank r's buffer at dest_bases[r] (device
+ * uint64 [num_ranks]: the peers' symmetric windows, system-scope stores -- the xGMI push of
+ * dispatch.cuh:373-392); src_global_idx = src_base + t.  topk_weights may be NULL (zeros are sent). */
 int deepep_dispatch_pack(const void* x, int64_t x_row_stride_bytes, int x_bytes,
                          const void* sf, int64_t sf_row_stride_bytes, int sf_bytes,
                          const int64_t* topk_idx, const float* topk_weights, int num_tokens, int num_topk,
                          int32_t src_base, const int32_t* dst_slot, const int32_t* send_offsets, int num_ranks,
-                         void* packed, int64_t row_bytes, int sf_off, int idx_off, int w_off, int src_off,
-                         deepep_stream_t stream);
+                         void* packed, const uint64_t* dest_bases, int64_t row_bytes,
+                         int sf_off, int idx_off, int w_off, int src_off, deepep_stream_t stream);
 
 /* Receive side, pass 1: src_metadata columns 0-1 ({src_global_idx, src_rank * K + master lane}),
  * recv_topk_idx (local expert or -1, int64 [num_recv][K], may be NULL) and per-256-row expert

@@ -68,7 +68,8 @@ class OracleKernels:
         counts.copy_(torch.bincount(valid, minlength=num_experts)[:num_experts].to(torch.int32))
 
     def dispatch_pack(self, x_bytes, sf_bytes, topk_idx, topk_weights, src_base, dst_slot, send_offsets,
-                      packed, layout, stream=None):
+                      packed, layout, dest_bases=None, stream=None):
+        assert dest_bases is None, 'the CPU stand-in packs into one local buffer'
         t_idx, r_idx = (dst_slot >= 0).nonzero(as_tuple=True)
         dest = (send_offsets[r_idx] + dst_slot[t_idx, r_idx]).long()
         K = layout.num_topk

@@ -77,6 +77,47 @@ def _worker(rank, world, port, seed, T, H, K, queue, empty_rank=-1, chunks=0):
             os.environ['DEEPEP_TRANSPORT'] = transport
             bufs[transport] = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=T, hidden=H, num_topk=K,
                                             explicitly_destroy=True, num_gpu_timeout_secs=20)
+        # dispatch over xGMI (rows pushed into the peers' windows) == dispatch over RCCL, bit for bit:
+        # bf16 and fp8 + scale-factor payloads, reduced / expanded layouts, fresh and cached handles
+        idx_t, w_t = torch.from_numpy(idx_all[rank]).to(dev), torch.from_numpy(w_all[rank]).to(dev)
+
+        def as_bytes(v):
+            if isinstance(v, tuple):
+                return [as_bytes(u) for u in v]
+            return None if v is None else v.contiguous().view(torch.uint8).cpu()
+
+        def same(a, b):
+            a, b = as_bytes(a), as_bytes(b)
+            if isinstance(a, list):
+                return all(same(u, v) for u, v in zip(a, b))
+            return (a is None and b is None) or (a is not None and b is not None and torch.equal(a, b))
+
+        g = torch.Generator(device=dev).manual_seed(1000 + rank)
+        payloads = []
+        for _ in range(2):
+            xb = torch.randn((Ts[rank], H), device=dev, generator=g).to(torch.bfloat16)
+            x8 = torch.randn((Ts[rank], H), device=dev, generator=g).to(torch.float8_e4m3fn)
+            sf = torch.rand((Ts[rank], H // 128), device=dev, generator=g)
+            payloads.append((xb, (x8, sf)))
+        for kind in (0, 1):
+            for do_expand in (False, True):
+                res = {t: b.dispatch(payloads[0][kind], topk_idx=idx_t, topk_weights=w_t, num_experts=E,
+                                     do_expand=do_expand) for t, b in bufs.items()}
+                cached = {t: b.dispatch(payloads[1][kind], handle=res[t][3], do_expand=do_expand) for t, b in bufs.items()}
+                for tag, got in (('fresh', res), ('cached', cached)):
+                    a, b = got['xgmi'], got['rccl']
+                    for i, name in enumerate(('recv_x', 'recv_topk_idx', 'recv_topk_weights')):
+                        if not same(a[i], b[i]):
+                            failures.append(f'dispatch {tag} kind {kind} expand {do_expand}: {name} xgmi != rccl')
+                    ha, hb = a[3], b[3]
+                    for name in ('recv_src_metadata', 'psum_num_recv_tokens_per_scaleup_rank',
+                                 'psum_num_recv_tokens_per_expert', 'num_unaligned_recv_tokens_per_expert'):
+                        if not same(getattr(ha, name), getattr(hb, name)):
+                            failures.append(f'dispatch {tag} kind {kind} expand {do_expand}: {name} xgmi != rccl')
+                    if ha.num_recv_tokens_per_expert_list != hb.num_recv_tokens_per_expert_list:
+                        failures.append(f'dispatch {tag} kind {kind} expand {do_expand}: expert list')
+        if bufs['xgmi']._sym is None:
+            failures.append('xgmi dispatch did not create its window')
         x = torch.zeros((Ts[rank], H), dtype=torch.bfloat16, device=dev)
         buf = bufs['xgmi']
         _, _, ex_w, handle, _ = buf.dispatch(x, topk_idx=torch.from_numpy(idx_all[rank]).to(dev),

@@ -175,6 +175,51 @@ def _bench_xgmi(buf, y, handle, ex_w, weighted, total_bytes, steps, warmup, dev)
                      'symmetric windows over xGMI, device barriers, phase B from the local window')
 
 
+def _bench_xgmi_dispatch(buf, x, topk_idx, topk_w, E, disp_bytes, time_dispatch, dev):
+    """The dispatch with every packed row stored straight into its destination's symmetric window
+    (DEEPEP_TRANSPORT=xgmi), checked bit for bit against the RCCL dispatch of the same batch.
+    Failures are reported, never raised."""
+    from deepep_amd import ElasticBuffer
+
+    def agree(ok: bool) -> bool:
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return bool(t.item())
+
+    ref = buf.dispatch(x, topk_idx=topk_idx, topk_weights=topk_w, num_experts=E, do_expand=True)
+    torch.cuda.synchronize()
+    err, equal, xb = None, False, None
+    try:
+        xb = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=buf.num_max_tokens_per_rank,
+                           hidden=buf_hidden(x), num_topk=topk_idx.shape[1], explicitly_destroy=True,
+                           num_gpu_timeout_secs=5)
+        xb.transport = 'xgmi'
+        got = xb.dispatch(x, topk_idx=topk_idx, topk_weights=topk_w, num_experts=E, do_expand=True)
+        torch.cuda.synchronize()
+        xb._sym.check()
+        rx, gx = (ref[0][0], got[0][0]) if isinstance(ref[0], tuple) else (ref[0], got[0])
+        equal = (torch.equal(rx.view(torch.uint8), gx.view(torch.uint8)) and torch.equal(ref[2], got[2]) and
+                 torch.equal(ref[3].recv_src_metadata, got[3].recv_src_metadata))
+    except Exception as e:          # noqa: BLE001 -- reported in the JSON line
+        err = f'{type(e).__name__}: {e}'[:300]
+    if not agree(err is None):
+        if xb is not None:
+            xb.destroy()
+        return dict(error=err or 'failed on another rank')
+    equal_all = agree(equal)
+    t_d, t_c = time_dispatch(xb)
+    timed_out = not agree(int(xb._sym.error_flag.item()) == 0)
+    xb.destroy()
+    return dict(ms=round(t_d * 1e3, 3), cached_ms=round(t_c * 1e3, 3), cached_gbps=round(disp_bytes / t_c / 1e9, 1),
+                bitwise_equal_to_rccl=equal_all, barrier_timeout=timed_out,
+                note='rows pushed straight into the destinations\' symmetric windows (system-scope stores), '
+                     'device barriers, receive-side kernels on the local window; per-rank wall time')
+
+
+def buf_hidden(x) -> int:
+    return (x[0] if isinstance(x, tuple) else x).shape[1]
+
+
 def _calc_diff(a: torch.Tensor, b: torch.Tensor) -> float:
     """deep_ep/utils/math.py:5-9."""
     a, b = a.double() + 1, b.double() + 1
@@ -499,22 +544,22 @@ def main():
         from deepep_amd.utils import per_token_cast_to_fp8
         x_disp = per_token_cast_to_fp8(x_disp)
 
-    def time_dispatch():
-        _, _, _, h, _ = buf.dispatch(x_disp, topk_idx=topk_idx, topk_weights=topk_w, num_experts=E, do_expand=True)
+    def time_dispatch(b):
+        _, _, _, h, _ = b.dispatch(x_disp, topk_idx=topk_idx, topk_weights=topk_w, num_experts=E, do_expand=True)
         torch.cuda.synchronize()
         t_d = time.perf_counter()
         for _ in range(n_disp):
-            buf.dispatch(x_disp, topk_idx=topk_idx, topk_weights=topk_w, num_experts=E, do_expand=True)
+            b.dispatch(x_disp, topk_idx=topk_idx, topk_weights=topk_w, num_experts=E, do_expand=True)
         torch.cuda.synchronize()
         t_d = (time.perf_counter() - t_d) / n_disp
         # cached handle: no routing kernels, no host sync (pack -> exchange -> copy)
         t_c = time.perf_counter()
         for _ in range(n_disp):
-            buf.dispatch(x_disp, topk_weights=topk_w, do_expand=True, handle=h)
+            b.dispatch(x_disp, topk_weights=topk_w, do_expand=True, handle=h)
         torch.cuda.synchronize()
         return t_d, (time.perf_counter() - t_c) / n_disp
 
-    t_d, t_c = time_dispatch()
+    t_d, t_c = time_dispatch(buf)
     elem = 1 if args.fp8_dispatch else 2
     disp_bytes = T * H * elem + handle.num_expanded_tokens * H * elem     # read x once, write every expanded row
     dispatch = dict(ms=round(t_d * 1e3, 3), gbps=round(disp_bytes / t_d / 1e9, 1),
@@ -522,13 +567,8 @@ def main():
                     transport=buf.transport if world > 1 else 'local',
                     note='ElasticBuffer.dispatch(do_expand=True) wall time incl. host count syncs; cached = '
                          'dispatch(handle=...) (no sync); bytes = x read once + expanded rows written')
-    if world > 1 and buf.transport != 'xgmi' and os.environ.get('DEEPEP_BENCH_XGMI', '1') != '0':
-        # the same dispatch with the rows pushed straight into the peers' symmetric windows
-        buf.transport = 'xgmi'
-        t_dx, t_cx = time_dispatch()
-        buf.transport = 'rccl'
-        dispatch.update(xgmi_ms=round(t_dx * 1e3, 3), xgmi_cached_ms=round(t_cx * 1e3, 3),
-                        xgmi_cached_gbps=round(disp_bytes / t_cx / 1e9, 1))
+    if world > 1 and os.environ.get('DEEPEP_BENCH_XGMI', '1') != '0':
+        dispatch['xgmi'] = _bench_xgmi_dispatch(buf, x_disp, topk_idx, topk_w, E, disp_bytes, time_dispatch, dev)
     del x_disp
 
     loopback = None

@@ -77,3 +77,17 @@ def test_product_fails_loudly_without_library(tmp_path, monkeypatch):
     from deepep_amd import _lib
     with pytest.raises(_lib.LibraryMissing):
         _lib.load(str(tmp_path / 'missing.so'))
+
+
+def test_header_is_plain_c():
+    """include/deepep_amd.h compiles as strict ISO C (what a cgo / C FFI consumer includes), and the
+    C consumer of tests/abi_c builds against it with -Werror."""
+    import subprocess
+    import __graft_entry__ as g
+    src = '#include "deepep_amd.h"\nint main(void) { return deepep_amd_abi_version() == DEEPEP_AMD_ABI_VERSION ? 0 : 1; }\n'
+    r = subprocess.run(['gcc', '-std=c99', '-pedantic', '-Wall', '-Wextra', '-Werror', '-fsyntax-only',
+                        '-I', os.path.join(ROOT, 'include'), '-x', 'c', '-'], input=src, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    r = subprocess.run(['gcc', '-std=c11', '-Wall', '-Wextra', '-Werror', '-D__HIP_PLATFORM_AMD__',
+                        '-I/opt/rocm/include', '-fsyntax-only', g.C_CONSUMER + '.c'], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr

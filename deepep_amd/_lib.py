@@ -11,7 +11,7 @@ from typing import Optional
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('DEEPEP_AMD_LIB', os.path.join(_HERE, 'libdeepep_amd.so'))
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 MODE_LOCAL, MODE_EPILOGUE, MODE_FUSED = 0, 1, 2
 

@@ -13,7 +13,8 @@
 // window is ever cached, so no invalidation protocol is needed between the writers' kernels and
 // the reader's.  The barrier is a one-workgroup kernel: thread s publishes `epoch` into rank s's
 // flag slot [rank] with a system-scope release store and then waits, with a system-scope acquire
-// load, until its own slot [s] reaches `epoch`.  Epochs only grow, so flags never need resetting.
+// load, until its own slot [s] reaches `epoch`.  Epochs only grow, so flags never need resetting;
+// they are counted on the device, so the barriers replay correctly inside a captured HIP graph.
 // A wall-clock timeout (the reference's num_gpu_timeout_secs, comm.cuh:30-54) sets bit 2 of the
 // error flag and lets the kernel finish instead of trapping, so a lost peer never hangs the GPU.
 #include <hip/hip_runtime.h>
@@ -32,15 +33,30 @@ int hip_fail(hipError_t e, const char* what) {
     return deepep_amd_set_error(DEEPEP_ERR_HIP, buf);
 }
 
-__global__ void __launch_bounds__(64)
-sym_barrier_kernel(const uint64_t* peer_flags, int rank, int num_ranks, int64_t epoch, int64_t timeout_ticks,
-                   int32_t* error_flag) {
-    const int s = static_cast<int>(threadIdx.x);
-    if (s >= num_ranks) return;
-    __threadfence_system();
-    int64_t* theirs = reinterpret_cast<int64_t*>(peer_flags[s]);
-    __hip_atomic_store(theirs + rank, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    const int64_t* mine = reinterpret_cast<const int64_t*>(peer_flags[rank]);
+// Epochs counted on the device (argument <= 0): the next epoch comes from this rank's own counter
+// in its window header, so a captured HIP graph replays with fresh epochs.  Counter table: int64
+// [2][kSlots] after the flag table -- row 0 = publishes per slot (barrier = slot 0, signals),
+// row 1 = waits per slot.  Only the launching kernel touches its counter (one thread, one
+// stream-ordered kernel at a time per slot).
+constexpr int kSlots = DEEPEP_SYM_FLAG_SLOTS;
+
+__device__ __forceinline__ int64_t next_epoch(const uint64_t* peer_flags, int rank, int row, int slot, int64_t given) {
+    __shared__ int64_t s_epoch;
+    if (threadIdx.x == 0) {
+        int64_t e = given;
+        if (e <= 0) {
+            int64_t* cnt = reinterpret_cast<int64_t*>(peer_flags[rank]) + kSlots * 64 + row * kSlots + slot;
+            e = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+            __hip_atomic_store(cnt, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s_epoch = e;
+    }
+    __syncthreads();
+    return s_epoch;
+}
+
+__device__ __forceinline__ void wait_slots(const int64_t* mine, int s, int64_t epoch, int64_t timeout_ticks,
+                                           int32_t* error_flag) {
     const uint64_t t0 = wall_clock64();
     while (__hip_atomic_load(mine + s, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
         if (static_cast<int64_t>(wall_clock64() - t0) > timeout_ticks) {
@@ -49,14 +65,27 @@ sym_barrier_kernel(const uint64_t* peer_flags, int rank, int num_ranks, int64_t 
         }
         __builtin_amdgcn_s_sleep(2);
     }
+}
+
+__global__ void __launch_bounds__(64)
+sym_barrier_kernel(const uint64_t* peer_flags, int rank, int num_ranks, int64_t epoch, int64_t timeout_ticks,
+                   int32_t* error_flag) {
+    epoch = next_epoch(peer_flags, rank, 0, 0, epoch);
+    const int s = static_cast<int>(threadIdx.x);
+    if (s >= num_ranks) return;
+    __threadfence_system();
+    int64_t* theirs = reinterpret_cast<int64_t*>(peer_flags[s]);
+    __hip_atomic_store(theirs + rank, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    wait_slots(reinterpret_cast<const int64_t*>(peer_flags[rank]), s, epoch, timeout_ticks, error_flag);
     __threadfence_system();
 }
 
 // Split barrier for pipelining: `signal` publishes `value` into slot `slot` of every rank's flag
 // table (after this stream's earlier work), `wait` waits for every rank's signal in this rank's
-// table.  Flag table of a window: int64 [kMaxSlots][64], slot 0 is the full barrier above.
+// table.  Flag table of a window: int64 [kSlots][64], slot 0 is the full barrier above.
 __global__ void __launch_bounds__(64)
 sym_signal_kernel(const uint64_t* peer_flags, int rank, int num_ranks, int slot, int64_t value) {
+    value = next_epoch(peer_flags, rank, 0, slot, value);
     const int s = static_cast<int>(threadIdx.x);
     if (s >= num_ranks) return;
     __threadfence_system();
@@ -67,17 +96,11 @@ sym_signal_kernel(const uint64_t* peer_flags, int rank, int num_ranks, int slot,
 __global__ void __launch_bounds__(64)
 sym_wait_kernel(const uint64_t* peer_flags, int rank, int num_ranks, int slot, int64_t value, int64_t timeout_ticks,
                 int32_t* error_flag) {
+    value = next_epoch(peer_flags, rank, 1, slot, value);
     const int s = static_cast<int>(threadIdx.x);
     if (s >= num_ranks) return;
-    const int64_t* mine = reinterpret_cast<const int64_t*>(peer_flags[rank]) + static_cast<int64_t>(slot) * 64;
-    const uint64_t t0 = wall_clock64();
-    while (__hip_atomic_load(mine + s, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < value) {
-        if (static_cast<int64_t>(wall_clock64() - t0) > timeout_ticks) {
-            if (error_flag != nullptr) atomicOr(error_flag, 2);
-            break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-    }
+    wait_slots(reinterpret_cast<const int64_t*>(peer_flags[rank]) + static_cast<int64_t>(slot) * 64, s, value,
+               timeout_ticks, error_flag);
     __threadfence_system();
 }
 
@@ -180,7 +203,7 @@ int deepep_stream_destroy(deepep_stream_t stream) {
 
 int deepep_sym_barrier(const uint64_t* peer_flags, int rank, int num_ranks, int64_t epoch, int64_t timeout_us,
                        int32_t* error_flag, deepep_stream_t stream) {
-    if (peer_flags == nullptr || num_ranks < 1 || num_ranks > 64 || rank < 0 || rank >= num_ranks || epoch < 1)
+    if (peer_flags == nullptr || num_ranks < 1 || num_ranks > 64 || rank < 0 || rank >= num_ranks)
         return deepep_amd_set_error(DEEPEP_ERR_INVALID_ARG, "sym_barrier: bad arguments");
     int rc = DEEPEP_OK;
     const int64_t ticks = timeout_ticks(timeout_us, &rc);
@@ -194,7 +217,7 @@ int deepep_sym_barrier(const uint64_t* peer_flags, int rank, int num_ranks, int6
 int deepep_sym_signal(const uint64_t* peer_flags, int rank, int num_ranks, int slot, int64_t value,
                       deepep_stream_t stream) {
     if (peer_flags == nullptr || num_ranks < 1 || num_ranks > 64 || rank < 0 || rank >= num_ranks || slot < 1 ||
-        slot >= DEEPEP_SYM_FLAG_SLOTS || value < 1)
+        slot >= DEEPEP_SYM_FLAG_SLOTS)
         return deepep_amd_set_error(DEEPEP_ERR_INVALID_ARG, "sym_signal: bad arguments");
     hipLaunchKernelGGL(sym_signal_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream),
                        peer_flags, rank, num_ranks, slot, value);
@@ -205,7 +228,7 @@ int deepep_sym_signal(const uint64_t* peer_flags, int rank, int num_ranks, int s
 int deepep_sym_wait(const uint64_t* peer_flags, int rank, int num_ranks, int slot, int64_t value, int64_t timeout_us,
                     int32_t* error_flag, deepep_stream_t stream) {
     if (peer_flags == nullptr || num_ranks < 1 || num_ranks > 64 || rank < 0 || rank >= num_ranks || slot < 1 ||
-        slot >= DEEPEP_SYM_FLAG_SLOTS || value < 1)
+        slot >= DEEPEP_SYM_FLAG_SLOTS)
         return deepep_amd_set_error(DEEPEP_ERR_INVALID_ARG, "sym_wait: bad arguments");
     int rc = DEEPEP_OK;
     const int64_t ticks = timeout_ticks(timeout_us, &rc);

@@ -9,7 +9,8 @@ HIP IPC, and opens every peer's window (deepep_sym_import); kernels then store i
 peer's HBM over xGMI.  Layout of a window:
 
     [0, HEADER_BYTES)        int64 flags[64 slots][64 ranks]: barrier epochs written by the peers
-                             (slot 0: the full barrier; slots 1..63: split barriers of pipelined phases)
+                             (slot 0: the full barrier; slots 1..63: split barriers of pipelined phases),
+                             then int64 counters[2][64 slots]: this rank's device-side epoch counts
     [HEADER_BYTES, ...)      data: the combine receive rows (see ElasticBuffer._combine_xgmi)
 """
 import ctypes
@@ -78,26 +79,28 @@ class SymmetricBuffer:
             bases.append(int(p.value))
         return bases
 
+    # Epochs are counted on the device (epoch argument 0): every launch -- including each replay of a
+    # captured HIP graph -- takes the next one from this rank's counter in its window header.  The
+    # host-side counts below are for tracing only.
     def barrier(self, stream) -> None:
         """Device-side group barrier on `stream` (all ranks must call it the same number of times)."""
         self.epoch += 1
         handle = stream.cuda_stream if stream is not None else torch.cuda.current_stream().cuda_stream
-        _lib.check(self.lib.deepep_sym_barrier(self.bases_dev.data_ptr(), self.rank, self.num_ranks, self.epoch,
+        _lib.check(self.lib.deepep_sym_barrier(self.bases_dev.data_ptr(), self.rank, self.num_ranks, 0,
                                                self.timeout_us, self.error_flag.data_ptr(), handle), 'sym_barrier')
 
     def signal(self, slot: int, stream) -> None:
         """Publish this rank's arrival at split barrier `slot` (1..63) after `stream`'s earlier work."""
         self._slot_epoch[slot] += 1
         handle = stream.cuda_stream if stream is not None else torch.cuda.current_stream().cuda_stream
-        _lib.check(self.lib.deepep_sym_signal(self.bases_dev.data_ptr(), self.rank, self.num_ranks, slot,
-                                              self._slot_epoch[slot], handle), 'sym_signal')
+        _lib.check(self.lib.deepep_sym_signal(self.bases_dev.data_ptr(), self.rank, self.num_ranks, slot, 0, handle),
+                   'sym_signal')
 
     def wait(self, slot: int, stream) -> None:
-        """Make `stream` wait until every rank has signalled `slot` as often as this rank has."""
+        """Make `stream` wait until every rank has signalled `slot` as often as this rank waited on it."""
         handle = stream.cuda_stream if stream is not None else torch.cuda.current_stream().cuda_stream
-        _lib.check(self.lib.deepep_sym_wait(self.bases_dev.data_ptr(), self.rank, self.num_ranks, slot,
-                                            self._slot_epoch[slot], self.timeout_us, self.error_flag.data_ptr(),
-                                            handle), 'sym_wait')
+        _lib.check(self.lib.deepep_sym_wait(self.bases_dev.data_ptr(), self.rank, self.num_ranks, slot, 0,
+                                            self.timeout_us, self.error_flag.data_ptr(), handle), 'sym_wait')
 
     def check(self) -> None:
         """Raise if a barrier timed out (host sync)."""

@@ -45,7 +45,7 @@ extern "C" {
 
 typedef struct ihipStream_t* deepep_stream_t;   /* == hipStream_t */
 
-#define DEEPEP_AMD_ABI_VERSION 7
+#define DEEPEP_AMD_ABI_VERSION 8
 
 #define DEEPEP_OK               0
 #define DEEPEP_ERR_INVALID_ARG  (-1)
@@ -202,18 +202,24 @@ int deepep_sym_import(const void* handle, void** ptr);      /* a peer's window, 
 int deepep_sym_close(void* ptr);
 
 /* Group barrier on the stream: peer_flags (device, uint64 [num_ranks]) holds the address of every
- * rank's int64 flag array (num_ranks slots, in its window).  Rank r stores `epoch` into slot [r] of
- * every rank's array (system-scope release) and waits until its own slots all reach `epoch`
- * (system-scope acquire); epochs must grow by one per call.  After timeout_us (<= 0: 100 s) the
- * wait gives up and sets bit 2 of *error_flag (comm.cuh:30-54 traps instead). */
+ * rank's window header (int64 flag table [DEEPEP_SYM_FLAG_SLOTS][64], then int64 epoch counters
+ * [2][DEEPEP_SYM_FLAG_SLOTS]; DEEPEP_SYM_HEADER_BYTES in all, zero at allocation).  Rank r stores
+ * the epoch into entry [r] of slot 0 of every rank's table (system-scope release) and waits until
+ * its own entries all reach it (system-scope acquire).  epoch <= 0: the next epoch is counted on
+ * the device (this rank's counter), so a captured HIP graph replays with fresh epochs -- use it
+ * for every call of a window, or host epochs (growing by one per call) for every call, not both.
+ * After timeout_us (<= 0: 100 s) the wait gives up and sets bit 2 of *error_flag (comm.cuh:30-54
+ * traps instead). */
+#define DEEPEP_SYM_HEADER_BYTES 65536
 int deepep_sym_barrier(const uint64_t* peer_flags, int rank, int num_ranks, int64_t epoch, int64_t timeout_us,
                        int32_t* error_flag, deepep_stream_t stream);
 
 /* Split barrier for pipelined phases, on flag slot 1 <= slot < DEEPEP_SYM_FLAG_SLOTS of the same
- * tables (int64 [DEEPEP_SYM_FLAG_SLOTS][64] per window; slot 0 is deepep_sym_barrier's):
- * deepep_sym_signal stores `value` into slot `slot`, entry [rank], of every rank's table after the
- * stream's earlier work (system-scope release); deepep_sym_wait waits until every entry of slot
- * `slot` of this rank's table reaches `value` (timeout as deepep_sym_barrier). */
+ * tables (slot 0 is deepep_sym_barrier's): deepep_sym_signal stores `value` into slot `slot`, entry
+ * [rank], of every rank's table after the stream's earlier work (system-scope release);
+ * deepep_sym_wait waits until every entry of slot `slot` of this rank's table reaches `value`
+ * (timeout as deepep_sym_barrier).  value <= 0: counted on the device, signals and waits each
+ * with their own per-slot counter (the n-th wait of a slot waits for every rank's n-th signal). */
 #define DEEPEP_SYM_FLAG_SLOTS 64
 int deepep_sym_signal(const uint64_t* peer_flags, int rank, int num_ranks, int slot, int64_t value,
                       deepep_stream_t stream);

@@ -138,6 +138,29 @@ def _worker(rank, world, port, seed, T, H, K, queue, empty_rank=-1, chunks=0):
                         failures.append(f'{transport} combined_x (bias {nb}, call {it})')
                     if not np.array_equal(out_w.cpu().numpy(), expect[rank][1]):
                         failures.append(f'{transport} combined_topk_weights (bias {nb}, call {it})')
+        # HIP graph: the whole xGMI combine (device barrier, phase A stores into the peers' windows,
+        # split signal / wait, phase B) captured once and replayed; the barrier epochs are counted on
+        # the device, so every replay -- and eager calls in between -- synchronise correctly
+        xb = bufs['xgmi']
+        g_in, g_bias = _bf16(x_exp_all[rank], dev), _bf16(b_all[rank], dev)
+        xb.combine(g_in, handle, topk_weights=ex_w, bias=g_bias)          # plans cached outside capture
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            g_out, g_w, _ = xb.combine(g_in, handle, topk_weights=ex_w, bias=g_bias)
+        for it in range(4):
+            g_out.zero_()
+            graph.replay()
+            torch.cuda.synchronize()
+            if not (np.array_equal(_u16(g_out), expect[rank][0]) and np.array_equal(g_w.cpu().numpy(), expect[rank][1])):
+                failures.append(f'xgmi combine graph replay {it}')
+            if it == 1:                                                  # an eager call between replays
+                out, _, _ = xb.combine(g_in, handle, topk_weights=ex_w, bias=g_bias)
+                torch.cuda.synchronize()
+                if not np.array_equal(_u16(out), expect[rank][0]):
+                    failures.append('xgmi eager combine between graph replays')
+        xb._sym.check()
+        del graph
         # gating-weighted variant: xGMI and RCCL paths agree bit for bit
         outs = {}
         for transport, b in bufs.items():

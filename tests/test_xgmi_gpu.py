@@ -116,6 +116,16 @@ def _worker(rank, world, port, seed, T, H, K, queue, empty_rank=-1, chunks=0):
                             failures.append(f'dispatch {tag} kind {kind} expand {do_expand}: {name} xgmi != rccl')
                     if ha.num_recv_tokens_per_expert_list != hb.num_recv_tokens_per_expert_list:
                         failures.append(f'dispatch {tag} kind {kind} expand {do_expand}: expert list')
+                # a cached-handle xGMI dispatch (no host sync) captured into a HIP graph, replayed
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph):
+                    g_res = bufs['xgmi'].dispatch(payloads[1][kind], handle=res['xgmi'][3], do_expand=do_expand)
+                for it in range(2):
+                    graph.replay()
+                    torch.cuda.synchronize()
+                    if not all(same(g_res[i], cached['xgmi'][i]) for i in (0, 2)):
+                        failures.append(f'dispatch graph replay {it} kind {kind} expand {do_expand}')
+                del graph, g_res
         if bufs['xgmi']._sym is None:
             failures.append('xgmi dispatch did not create its window')
         x = torch.zeros((Ts[rank], H), dtype=torch.bfloat16, device=dev)

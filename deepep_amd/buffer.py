@@ -625,13 +625,21 @@ class ElasticBuffer(ExchangeMixin):
         # An explicit num_sms below the CU count: the combine's kernels run on a stream restricted to
         # that many CUs (the reference's combine_impl grid, combine.hpp:135), the rest stay free for
         # compute.  That stream plays the comm stream, so the call takes the async-capable path.
+        # The budget stream is ordered with the regular comm stream both ways: the symmetric window
+        # (xGMI transport) is shared by every call, and an earlier async dispatch / a later call on
+        # the comm stream must not overlap this combine's use of it.
+        capturing = torch.cuda.is_current_stream_capturing()
         saved, self.comm_stream = self.comm_stream, budget
+        if not capturing:
+            budget.wait_stream(saved)
         try:
             return self._combine(x, topk_weights, bias_0, bias_1, handle, num_sms, previous_event,
                                  previous_event_before_epilogue, async_with_compute_stream,
                                  allocate_on_comm_stream, apply_topk_weights, force_comm_stream=True)
         finally:
             self.comm_stream = saved
+            if not capturing:
+                saved.wait_stream(budget)
 
     def _cu_budget_stream(self, num_sms: int):
         """The CU-budget stream for an explicit num_sms (None when 0 or at least the CU count).

@@ -422,19 +422,27 @@ def main():
         kern_us = k0.elapsed_time(k1) * 1e3 / args.steps
         # the reference's protocol (deep_ep/utils/testing.py:12-21, bench_kineto): a 256 MB+ cache flush
         # before every launch, each launch timed alone (here: 512 MB written, HIP events around the kernel)
+        # The write flush leaves up to the caches' size of dirty lines that this launch then writes
+        # back (tools/kflush.py: +11 us on one box, and no change after a 200 us idle); a read flush
+        # (a reduction over the same 512 MB) evicts as much without dirtying, so it isolates the kernel.
         flush = torch.empty((512 << 20) // 4, dtype=torch.int32, device=dev)
-        fl_us = []
-        for _ in range(0 if args.no_flushed else min(args.steps, 50)):
-            flush.zero_()
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a.record(stream)
-            launch()
-            b.record(stream)
-            fl_us.append((a, b))
-        torch.cuda.synchronize()
-        fl_us = sorted(a.elapsed_time(b) * 1e3 for a, b in fl_us)
-        kern_us_flushed = fl_us[len(fl_us) // 2] if fl_us else None
-        del flush
+        sink = torch.empty((), dtype=torch.int64, device=dev)
+
+        def flushed_median(before):
+            evs = []
+            for _ in range(0 if args.no_flushed else min(args.steps, 50)):
+                before()
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record(stream)
+                launch()
+                b.record(stream)
+                evs.append((a, b))
+            torch.cuda.synchronize()
+            v = sorted(a.elapsed_time(b) * 1e3 for a, b in evs)
+            return v[len(v) // 2] if v else None
+        kern_us_flushed = flushed_median(flush.zero_)
+        kern_us_read_flushed = flushed_median(lambda: torch.sum(flush, dim=0, dtype=torch.int64, out=sink))
+        del flush, sink
         achieved = bytes_rank / (kern_us * 1e-6) / 1e9
         # same-run memory reference: a device-to-device copy of the expanded rows (boxes differ by up
         # to ~20 % in copy bandwidth; this contextualises `achieved`)
@@ -480,6 +488,8 @@ def main():
                         frac=round(achieved / HBM_PEAK_GBPS, 4), traffic=_pmc_traffic(workload),
                         kernel='combine_rows_kernel<FUSED>', kernel_us=round(kern_us, 2),
                         kernel_us_flushed_median=None if kern_us_flushed is None else round(kern_us_flushed, 2),
+                        kernel_us_read_flushed_median=(None if kern_us_read_flushed is None
+                                                       else round(kern_us_read_flushed, 2)),
                         bytes_per_launch=bytes_rank, in_region_us_per_step=round(comm_ms * 1e3, 2),
                         same_run_d2d_copy_gbps=round(copy_gbps, 1), single_reduction_phase_b=single_b)
 

@@ -32,6 +32,7 @@ for step in "$@"; do
         pcopy)  run pcopy 600 python tools/probe_copy.py ;;
         kwaves) run kwaves 600 python tools/kbench_waves.py ;;
         kvar)   run kvar 300 python tools/kvar.py ;;
+        kflush) run kflush 300 python tools/kflush.py ;;
         kphase) run kphase 300 python tools/kphase.py ;;
         kcu)    run kcu 300 python tools/kcu.py ;;
         cumask) run cumask 120 python tools/probe_cumask.py ;;

@@ -191,7 +191,7 @@ def _bench_xgmi_dispatch(buf, x, topk_idx, topk_w, E, disp_bytes, time_dispatch,
     err, equal, xb = None, False, None
     try:
         xb = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=buf.num_max_tokens_per_rank,
-                           hidden=buf_hidden(x), num_topk=topk_idx.shape[1], explicitly_destroy=True,
+                           hidden=_hidden_of(x), num_topk=topk_idx.shape[1], explicitly_destroy=True,
                            num_gpu_timeout_secs=5)
         xb.transport = 'xgmi'
         got = xb.dispatch(x, topk_idx=topk_idx, topk_weights=topk_w, num_experts=E, do_expand=True)
@@ -216,7 +216,7 @@ def _bench_xgmi_dispatch(buf, x, topk_idx, topk_w, E, disp_bytes, time_dispatch,
                      'device barriers, receive-side kernels on the local window; per-rank wall time')
 
 
-def buf_hidden(x) -> int:
+def _hidden_of(x) -> int:
     return (x[0] if isinstance(x, tuple) else x).shape[1]
 
 

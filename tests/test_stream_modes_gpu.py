@@ -111,7 +111,11 @@ def _inputs(T, H, K, E, seed):
     return x, idx, w
 
 
-def test_stream_modes_ep1():
+@pytest.mark.parametrize('avoid_record_stream', [0, 1])
+def test_stream_modes_ep1(monkeypatch, avoid_record_stream):
+    """avoid_record_stream: EP_AVOID_RECORD_STREAM=1 (event.py:17-30), the async tensors are kept
+    alive by the returned event instead of record_stream."""
+    monkeypatch.setenv('EP_AVOID_RECORD_STREAM', str(avoid_record_stream))
     import torch.distributed as dist
     from deepep_amd import ElasticBuffer
     if not dist.is_initialized():

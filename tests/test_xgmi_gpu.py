@@ -261,7 +261,8 @@ def _worker(rank, world, port, seed, T, H, K, queue, empty_rank=-1, chunks=0):
 
 @pytest.mark.parametrize('world,T,H,K,empty_rank,chunks', [
     (2, 96, 1024, 8, -1, 0), (4, 64, 7168, 8, -1, 0), (4, 80, 256, 2, -1, 0), (3, 40, 512, 4, 1, 0),
-    (2, 96, 1024, 8, -1, 3), (4, 80, 256, 2, -1, 5), (3, 40, 512, 4, 1, 4)])
+    (2, 96, 1024, 8, -1, 3), (4, 80, 256, 2, -1, 5), (3, 40, 512, 4, 1, 4),
+    (8, 48, 512, 8, -1, 2)])                                  # the node's full EP = 8 (8 processes)
 def test_xgmi_transport_matches_oracle(world, T, H, K, empty_rank, chunks):
     """chunks > 0: the pipelined schedule (phase A per source-token chunk + split barrier, phase B
     of each chunk on a second stream)."""

@@ -583,21 +583,36 @@ def main():
 
     loopback = None
     if world == 1 and not args.no_loopback:
-        # Host-staged loopback (north_star): pinned host rows -> H2D -> combine -> D2H.
+        # Host-staged loopback (north_star): pinned host rows -> H2D -> combine -> D2H, batches back to
+        # back.  The D2H of batch i runs on its own stream, so it overlaps the H2D of batch i + 1 (PCIe
+        # is full duplex); the serial chain is timed as well.
         host_y = torch.empty(y.shape, dtype=y.dtype, pin_memory=True).copy_(y)
         host_out = torch.empty((T, H), dtype=torch.bfloat16, pin_memory=True)
         dev_y = torch.empty_like(y)
-        torch.cuda.synchronize()
-        n_lb = 3
-        t_lb = time.perf_counter()
-        for _ in range(n_lb):
-            dev_y.copy_(host_y, non_blocking=True)
-            o, _, _ = buf.combine(dev_y, handle, topk_weights=ex_w, apply_topk_weights=weighted)
-            host_out.copy_(o, non_blocking=True)
-        torch.cuda.synchronize()
-        el_lb = (time.perf_counter() - t_lb) / n_lb
+        d2h = torch.cuda.Stream(device=dev)
+        n_lb = 4
+
+        def loop(overlap: bool) -> float:
+            torch.cuda.synchronize()
+            t_lb = time.perf_counter()
+            for _ in range(n_lb):
+                dev_y.copy_(host_y, non_blocking=True)
+                o, _, _ = buf.combine(dev_y, handle, topk_weights=ex_w, apply_topk_weights=weighted)
+                if overlap:
+                    d2h.wait_stream(torch.cuda.current_stream())
+                    with torch.cuda.stream(d2h):
+                        host_out.copy_(o, non_blocking=True)
+                    o.record_stream(d2h)
+                else:
+                    host_out.copy_(o, non_blocking=True)
+            torch.cuda.synchronize()
+            return (time.perf_counter() - t_lb) / n_lb
+        el_serial = loop(False)
+        el_lb = loop(True)
         loopback = dict(gbps=round(bytes_rank / el_lb / 1e9, 2), ms_per_batch=round(el_lb * 1e3, 2),
-                        note='algorithmic bytes / (H2D of the expanded rows + combine + D2H of the output)')
+                        serial_gbps=round(bytes_rank / el_serial / 1e9, 2), serial_ms_per_batch=round(el_serial * 1e3, 2),
+                        note='algorithmic bytes / (H2D of the expanded rows + combine + D2H of the output) per batch, '
+                             'batches back to back with the D2H overlapping the next H2D; serial = one chain')
         del host_y, host_out, dev_y
 
     # EP > 1: both transports are complete implementations of the same combine, timed with the same

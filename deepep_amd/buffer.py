@@ -61,6 +61,29 @@ def calculate_buffer_size(num_ranks: int, num_max_tokens_per_rank: int, hidden: 
     return align(max(dispatch_bytes, combine_bytes), BUFFER_ALIGNMENT)
 
 
+def notify_layout(notify: List[int], num_ranks: int, rank: int, experts_per_rank: int, all_gathered: bool):
+    """Host view of the dispatch notify (dispatch.cuh:79-258; buffer.hpp:1017-1064's CPU wait).
+    Each record is [tokens | tokens per local expert] (1 + experts_per_rank ints) from a source to a
+    destination.  `notify` holds the records this rank received, one per source (all_gathered
+    False), or every rank's records to every destination, [source][destination] (all_gathered True:
+    the xGMI push needs them).  Returns (tokens this rank sends per destination -- only when
+    all_gathered, else None -- tokens received per source, rows received per local expert, and,
+    when all_gathered, the row offset of this rank's rows inside every destination's receive window:
+    the rows the lower source ranks send there come first)."""
+    R, r, w = num_ranks, rank, 1 + experts_per_rank
+    if all_gathered:
+        grid = [[notify[(s * R + d) * w:(s * R + d + 1) * w] for d in range(R)] for s in range(R)]
+        rows = [grid[s][r] for s in range(R)]
+        sends = [grid[r][d][0] for d in range(R)]
+        offsets = [sum(grid[s][d][0] for s in range(r)) for d in range(R)]
+    else:
+        rows = [notify[i * w:(i + 1) * w] for i in range(R)]
+        sends, offsets = None, None
+    recv = [row[0] for row in rows]
+    experts = [sum(row[1 + e] for row in rows) for e in range(experts_per_rank)]
+    return sends, recv, experts, offsets
+
+
 class ElasticBuffer(ExchangeMixin):
     """The elastic EP buffer (single node): dispatch produces an EPHandle, combine reduces.
     The EP > 1 exchanges of the combine (RCCL all-to-all, xGMI windows) live in ExchangeMixin
@@ -403,16 +426,10 @@ class ElasticBuffer(ExchangeMixin):
                 host = [int(v) for v in torch.cat([send_counts, (everyone if R > 1 and use_xgmi else
                                                                  recv_notify).reshape(-1)]).tolist()]   # host sync
                 send_counts_l = host[:R]
-                if R > 1 and use_xgmi:
-                    grid = [[host[R + (s * R + d) * (1 + epr): R + (s * R + d + 1) * (1 + epr)] for d in range(R)]
-                            for s in range(R)]
-                    rows = [grid[s][r] for s in range(R)]
-                    peer_offsets = torch.tensor([sum(grid[s][d][0] for s in range(r)) for d in range(R)],
-                                                dtype=torch.int32).to(dev, non_blocking=True)
-                else:
-                    rows = [host[R + i * (1 + epr): R + (i + 1) * (1 + epr)] for i in range(R)]
-                recv_counts_l = [row[0] for row in rows]
-                expert_counts_l = [sum(row[1 + e] for row in rows) for e in range(epr)]
+                _, recv_counts_l, expert_counts_l, offs = notify_layout(host[R:], R, r, epr,
+                                                                        all_gathered=R > 1 and use_xgmi)
+                if offs is not None:
+                    peer_offsets = torch.tensor(offs, dtype=torch.int32).to(dev, non_blocking=True)
                 recv_counts_t = recv_notify[:, 0].contiguous()
                 send_offsets = (torch.cumsum(send_counts, 0) - send_counts).to(torch.int32)
             N = sum(recv_counts_l)

@@ -411,3 +411,32 @@ def test_interleave_by_rank_is_a_round_robin_permutation():
     assert out.tolist() == [0, 5, 7, 1, 6, 9, 2, 10, 4]
     assert _interleave_by_rank(units, dest, 1).tolist() == units.tolist()
     assert _interleave_by_rank(units[:0], dest, 4).numel() == 0
+
+
+def test_notify_layout_matches_brute_force():
+    """The dispatch notify on the host: per-rank view and the all-gathered view (xGMI push) agree,
+    and every source's rows land in disjoint, packed, source-ordered ranges of each destination."""
+    from deepep_amd.buffer import notify_layout
+    rng = np.random.default_rng(5)
+    for R, epr in ((1, 4), (2, 3), (3, 1), (8, 32)):
+        counts = rng.integers(0, 50, size=(R, R, epr))            # [source][destination][local expert]
+        rec = np.concatenate([counts.sum(-1, keepdims=True), counts], axis=-1)   # [tokens | per expert]
+        # a token counts once per destination in `tokens` even if it hits several of its experts
+        rec[..., 0] = np.minimum(rec[..., 0], rng.integers(0, 60, size=(R, R)))
+        everyone = [int(v) for v in rec.reshape(-1)]
+        spans = {}
+        for r in range(R):
+            mine = [int(v) for v in rec[:, r].reshape(-1)]
+            _, recv_a, exp_a, off_none = notify_layout(mine, R, r, epr, all_gathered=False)
+            sends, recv_b, exp_b, offs = notify_layout(everyone, R, r, epr, all_gathered=True)
+            assert off_none is None and recv_a == recv_b and exp_a == exp_b
+            assert recv_a == [int(v) for v in rec[:, r, 0]]
+            assert exp_a == [int(v) for v in rec[:, r, 1:].sum(0)]
+            assert sends == [int(v) for v in rec[r, :, 0]]
+            for d in range(R):
+                spans.setdefault(d, []).append((offs[d], offs[d] + sends[d], r))
+        for d, sp in spans.items():                               # packed by source rank, no overlap
+            sp.sort()
+            assert [s[2] for s in sp] == list(range(R)) and sp[0][0] == 0
+            assert all(a[1] == b[0] for a, b in zip(sp, sp[1:]))
+            assert sp[-1][1] == int(rec[:, d, 0].sum())

@@ -141,6 +141,8 @@ class ElasticBuffer(ExchangeMixin):
         # (phase A stores straight into the owners' symmetric windows, deepep_amd/symmetric.py)
         self.transport = os.environ.get('DEEPEP_TRANSPORT', 'rccl')
         _assert(self.transport in ('rccl', 'xgmi'), 'DEEPEP_TRANSPORT must be rccl or xgmi')
+        # xGMI combine: CUs for phase A while phase B of earlier chunks runs (0 = the whole chip)
+        self.phase_a_cus = int(os.environ.get('DEEPEP_PHASE_A_CUS', 0))
         self._sym = None
         self._sym_exchange = None     # test hook: ranks sharing one process exchange window bases directly
         self._group_barrier()

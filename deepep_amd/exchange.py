@@ -272,14 +272,23 @@ class ExchangeMixin:
                 self._stream_b = torch.cuda.Stream(device=self.device)
             stream_b = self._stream_b
             stream_b.wait_stream(stream)
+        # Optional CU budget for phase A (DEEPEP_PHASE_A_CUS): its stores wait on the xGMI links, so
+        # its waves can hold CUs long after their loads; fewer CUs for it leave the rest to phase B
+        # of the earlier chunks.  Results are identical; only the overlap changes.
+        sa = self._cu_budget_stream(self.phase_a_cus) if pipelined and self.phase_a_cus else None
+        sa = stream if sa is None else sa
+        if sa is not stream:
+            sa.wait_stream(stream)
         for c, ch in enumerate(plan.chunks):
-            self._mark(stream)
+            self._mark(sa)
             kern.combine_reduce_scatter(x, ch.out_rows.shape[0], ch.out_rows, table=ch.table_a, row_weights=row_w,
                                         wtable=ch.wtable_a, wsrc=wsrc,
                                         num_weights=K if topk_weights is not None else 0,
-                                        weights_offset=w_off, stream=stream)
-            self._mark(stream)
-            sym.signal(1 + c, stream)
+                                        weights_offset=w_off, stream=sa)
+            self._mark(sa)
+            sym.signal(1 + c, sa)
+        if sa is not stream:
+            stream.wait_stream(sa)
         self._before_epilogue(previous_event_before_epilogue)
         sb = stream_b if pipelined else stream
         if pipelined and previous_event_before_epilogue is not None:

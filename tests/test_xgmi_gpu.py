@@ -148,6 +148,14 @@ def _worker(rank, world, port, seed, T, H, K, queue, empty_rank=-1, chunks=0):
                         failures.append(f'{transport} combined_x (bias {nb}, call {it})')
                     if not np.array_equal(out_w.cpu().numpy(), expect[rank][1]):
                         failures.append(f'{transport} combined_topk_weights (bias {nb}, call {it})')
+        # phase A on a 64-CU budget stream (DEEPEP_PHASE_A_CUS): same bits
+        bufs['xgmi'].phase_a_cus = 64
+        out, out_w, _ = bufs['xgmi'].combine(_bf16(x_exp_all[rank], dev), handle, topk_weights=ex_w,
+                                             bias=_bf16(b_all[rank], dev))
+        torch.cuda.synchronize()
+        if not (np.array_equal(_u16(out), expect[rank][0]) and np.array_equal(out_w.cpu().numpy(), expect[rank][1])):
+            failures.append('xgmi combine with a phase-A CU budget')
+        bufs['xgmi'].phase_a_cus = 0
         # HIP graph: the whole xGMI combine (device barrier, phase A stores into the peers' windows,
         # split signal / wait, phase B) captured once and replayed; the barrier epochs are counted on
         # the device, so every replay -- and eager calls in between -- synchronise correctly

@@ -69,22 +69,32 @@ class ExchangeMixin:
                 self._stream_b = torch.cuda.Stream(device=self.device)
             stream_b = self._stream_b
             stream_b.wait_stream(stream)                  # bias / outputs were produced before this call
+        # Optional CU budget for phase A (DEEPEP_PHASE_A_CUS, as in _combine_xgmi): the CUs it leaves
+        # free go to RCCL's kernels and to phase B of the earlier chunks.  Phase A and the exchange
+        # it feeds are then issued from the budget stream (RCCL orders after the current stream).
+        sa = self._cu_budget_stream(self.phase_a_cus) if pipelined and self.phase_a_cus else None
+        sa = stream if sa is None else sa
+        if sa is not stream:
+            sa.wait_stream(stream)
         in_flight = []
         for ch in plan.chunks:
-            n_send = sum(ch.send_counts)
-            packed = torch.empty((n_send, row_elems), dtype=x.dtype, device=x.device)
-            partial_w = packed[:, hidden:].view(torch.float32)[:, :K] if w_elems else None
-            self._mark(stream)
-            kern.combine_reduce(MODE_LOCAL, x, packed[:, :hidden], n_send, table=ch.table_a, row_weights=row_w,
-                                wtable=ch.wtable_a, wsrc=wsrc, out_weights=partial_w, stream=stream)
-            self._mark(stream)
-            recv = torch.empty((sum(ch.back_counts), row_elems), dtype=x.dtype, device=x.device)
-            if pipelined:
-                work = self._a2a_async(recv, packed, ch.back_counts, ch.send_counts)
-            else:
-                self._all_to_all(recv, packed, ch.back_counts, ch.send_counts)
-                work = None
+            with (torch.cuda.stream(sa) if sa is not stream else self._null_ctx()):
+                n_send = sum(ch.send_counts)
+                packed = torch.empty((n_send, row_elems), dtype=x.dtype, device=x.device)
+                partial_w = packed[:, hidden:].view(torch.float32)[:, :K] if w_elems else None
+                self._mark(sa)
+                kern.combine_reduce(MODE_LOCAL, x, packed[:, :hidden], n_send, table=ch.table_a, row_weights=row_w,
+                                    wtable=ch.wtable_a, wsrc=wsrc, out_weights=partial_w, stream=sa)
+                self._mark(sa)
+                recv = torch.empty((sum(ch.back_counts), row_elems), dtype=x.dtype, device=x.device)
+                if pipelined:
+                    work = self._a2a_async(recv, packed, ch.back_counts, ch.send_counts)
+                else:
+                    self._all_to_all(recv, packed, ch.back_counts, ch.send_counts)
+                    work = None
             in_flight.append((ch, recv, packed, work))
+        if sa is not stream:
+            stream.wait_stream(sa)
         self._before_epilogue(previous_event_before_epilogue)
         if pipelined and previous_event_before_epilogue is not None:
             previous_event_before_epilogue.stream_wait(stream_b)

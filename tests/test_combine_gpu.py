@@ -328,17 +328,19 @@ def _buffer_case(rank, world, fixture, comm, results):
         comm.bar.abort() if comm is not None else None
 
 
-@pytest.mark.parametrize('fixture,world,chunks', [
-    ('f1_ep1_t128_h1024_k2.npz', 1, 0),
-    ('f4_ep4_t96_h256_k2.npz', 4, 0),
-    ('f2_ep8_t64_h256_k8.npz', 8, 0),
-    ('f3_ep8_skew_t128_h64_k8.npz', 8, 0),
-    ('f4_ep4_t96_h256_k2.npz', 4, 3),        # pipelined: phase B of each chunk on the second stream
-    ('f3_ep8_skew_t128_h64_k8.npz', 8, 5),
+@pytest.mark.parametrize('fixture,world,chunks,phase_a_cus', [
+    ('f1_ep1_t128_h1024_k2.npz', 1, 0, 0),
+    ('f4_ep4_t96_h256_k2.npz', 4, 0, 0),
+    ('f2_ep8_t64_h256_k8.npz', 8, 0, 0),
+    ('f3_ep8_skew_t128_h64_k8.npz', 8, 0, 0),
+    ('f4_ep4_t96_h256_k2.npz', 4, 3, 0),        # pipelined: phase B of each chunk on the second stream
+    ('f3_ep8_skew_t128_h64_k8.npz', 8, 5, 0),
+    ('f2_ep8_t64_h256_k8.npz', 8, 4, 64),       # pipelined, phase A on a 64-CU budget stream
 ])
-def test_elastic_buffer_golden_on_gpu(fixture, world, chunks, monkeypatch):
+def test_elastic_buffer_golden_on_gpu(fixture, world, chunks, phase_a_cus, monkeypatch):
     if chunks:
         monkeypatch.setenv('DEEPEP_COMBINE_CHUNKS', str(chunks))
+    monkeypatch.setenv('DEEPEP_PHASE_A_CUS', str(phase_a_cus))
     comm = _ThreadComm(world) if world > 1 else None
     results = {}
     threads = [threading.Thread(target=_buffer_case, args=(r, world, fixture, comm, results)) for r in range(world)]

@@ -295,3 +295,37 @@ def test_xgmi_transport_matches_oracle(world, T, H, K, empty_rank, chunks):
         # the root cause is usually one rank's exception; its peers then fail with a closed connection
         tails = {r: [f[-1500:] for f in fl] for r, fl in results.items()}
         pytest.fail(f'{len(results)}/{world} ranks reported; failures: {tails}', pytrace=False)
+
+
+def test_lost_peer_times_out_instead_of_hanging():
+    """Failure detection (comm.cuh:30-54, num_gpu_timeout_secs): rank 0 of a 2-rank window whose
+    peer never arrives.  The device barrier and the split-barrier wait give up after the timeout,
+    set the error flag and let the stream continue; check() raises.  (The reference traps.)"""
+    import ctypes
+    import time
+    sys.path.insert(0, ROOT)
+    from deepep_amd import _lib
+    from deepep_amd.symmetric import HEADER_BYTES, SymmetricBuffer
+    torch.cuda.set_device(0)
+    lib = _lib.load()
+    dead = ctypes.c_void_p()                    # the lost peer's window: allocated, never served
+    _lib.check(lib.deepep_sym_alloc(HEADER_BYTES + 4096, ctypes.byref(dead)), 'sym_alloc')
+    sym = SymmetricBuffer(None, 0, 2, 4096, torch.device('cuda', 0),
+                          exchange=lambda base: [base, int(dead.value)], timeout_s=0.3)
+    try:
+        s = torch.cuda.current_stream()
+        t0 = time.perf_counter()
+        sym.barrier(s)
+        torch.cuda.synchronize()
+        assert int(sym.error_flag.item()) & 2, 'barrier did not report the timeout'
+        with pytest.raises(RuntimeError, match='barrier timeout'):
+            sym.check()
+        sym.error_flag.zero_()
+        sym.signal(1, s)                        # our own signal lands; the peer's never does
+        sym.wait(1, s)
+        torch.cuda.synchronize()
+        assert int(sym.error_flag.item()) & 2, 'split-barrier wait did not report the timeout'
+        assert time.perf_counter() - t0 < 30
+    finally:
+        sym.destroy()
+        _lib.check(lib.deepep_sym_free(dead), 'sym_free')

@@ -144,6 +144,7 @@ class ElasticBuffer(ExchangeMixin):
         # xGMI combine: CUs for phase A while phase B of earlier chunks runs (0 = the whole chip)
         self.phase_a_cus = int(os.environ.get('DEEPEP_PHASE_A_CUS', 0))
         self._sym = None
+        self._capturing = False
         self._sym_exchange = None     # test hook: ranks sharing one process exchange window bases directly
         self._group_barrier()
 
@@ -255,6 +256,12 @@ class ElasticBuffer(ExchangeMixin):
         hops (~25 us per call measured on MI355X)."""
         return (not async_with_compute_stream and previous_event is None and
                 previous_event_before_epilogue is None and not allocate_on_comm_stream)
+
+    def _note_capture(self) -> None:
+        """Whether this call is being captured into a HIP graph (read on the caller's stream,
+        before any stream switch): the host-side error-flag polling of the xGMI windows is skipped
+        then (graph replays still count their barrier epochs on the device)."""
+        self._capturing = self.use_cuda and torch.cuda.is_current_stream_capturing()
 
     def _prologue(self, previous_event: Optional[EventHandle], allocate_on_comm_stream: bool):
         if not self.use_cuda:
@@ -380,6 +387,7 @@ class ElasticBuffer(ExchangeMixin):
                     'topk_weights must be float32 [num_tokens, num_topk]')
         K = num_topk
         epr = num_experts // R
+        self._note_capture()
         compute_stream = self._prologue(previous_event, allocate_on_comm_stream)
         kern = self.kernels
         with self._stream_ctx():
@@ -448,6 +456,8 @@ class ElasticBuffer(ExchangeMixin):
                 kern.dispatch_pack(x_bytes, sf_bytes, idx64, w, r * num_max_tokens_per_rank, dst_slot,
                                    peer_offsets, None, layout, dest_bases=sym.data_bases_dev, stream=stream)
                 sym.barrier(stream)                               # every row landed
+                if not self._capturing:
+                    sym.publish(stream)
                 recv_packed = sym.data[:N * layout.row_bytes].view(N, layout.row_bytes)
             else:
                 packed = torch.empty((sum(send_counts_l), layout.row_bytes), dtype=torch.uint8, device=dev)
@@ -722,6 +732,7 @@ class ElasticBuffer(ExchangeMixin):
 
         kern = self.kernels
         R = self.num_ranks
+        self._note_capture()
         sync_mode = self._sync_mode(previous_event, previous_event_before_epilogue, async_with_compute_stream,
                                     allocate_on_comm_stream) and not force_comm_stream
         if sync_mode:

@@ -183,6 +183,8 @@ class ExchangeMixin:
         slots = self._window_slots if slots is None else slots
         need = slots * (rows_per_slot or self.num_max_tokens_per_rank) * row_bytes
         if self._sym is not None and self._sym.data_bytes >= need:
+            if not self._capturing:
+                self._sym.poll()                  # an earlier call's barrier timed out: raise now
             return self._sym
         from .symmetric import SymmetricBuffer
         old = self._sym
@@ -316,6 +318,8 @@ class ExchangeMixin:
             self._mark(sb)
         if pipelined:
             stream.wait_stream(stream_b)
+        if not self._capturing:
+            sym.publish(stream)
 
     def _combine_xgmi_single(self, handle, x, row_w, wsrc, K, hidden, bias_0, bias_1, topk_weights,
                              combined_x, combined_w, previous_event_before_epilogue, stream) -> None:
@@ -410,3 +414,5 @@ class ExchangeMixin:
             stream.wait_stream(stream_b)
             if recv_w is not None:
                 recv_w.record_stream(stream_b)
+        if not self._capturing:
+            sym.publish(stream)

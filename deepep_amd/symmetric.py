@@ -102,6 +102,27 @@ class SymmetricBuffer:
         _lib.check(self.lib.deepep_sym_wait(self.bases_dev.data_ptr(), self.rank, self.num_ranks, slot, 0,
                                             self.timeout_us, self.error_flag.data_ptr(), handle), 'sym_wait')
 
+    def publish(self, stream) -> None:
+        """Queue a copy of the error flag to pinned host memory behind `stream`'s work (no host
+        sync); poll() reads it once it has landed.  Not for use inside a HIP-graph capture."""
+        with torch.cuda.stream(stream):
+            if getattr(self, '_flag_host', None) is None:
+                self._flag_host = torch.zeros((1,), dtype=torch.int32, pin_memory=True)
+            self._flag_host.copy_(self.error_flag, non_blocking=True)
+            self._flag_event = torch.cuda.Event()
+            self._flag_event.record(stream)
+
+    def poll(self) -> None:
+        """Raise if an earlier call's published flag shows a barrier timeout (no host sync: a copy
+        that has not landed yet is checked at a later call) -- the reference traps instead."""
+        ev = getattr(self, '_flag_event', None)
+        if ev is not None and ev.query():
+            self._flag_event = None
+            v = int(self._flag_host[0])
+            if v:
+                raise RuntimeError(f'deepep_amd: symmetric buffer error flag {v} (2 = barrier timeout): a peer '
+                                   f'did not arrive within num_gpu_timeout_secs; the last results are invalid')
+
     def check(self) -> None:
         """Raise if a barrier timed out (host sync)."""
         v = int(self.error_flag.item())

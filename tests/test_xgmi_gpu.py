@@ -326,6 +326,12 @@ def test_lost_peer_times_out_instead_of_hanging():
         torch.cuda.synchronize()
         assert int(sym.error_flag.item()) & 2, 'split-barrier wait did not report the timeout'
         assert time.perf_counter() - t0 < 30
+        # what ElasticBuffer does around every xGMI call: publish the flag (no sync), poll it at
+        # the next call -> RuntimeError there
+        sym.publish(s)
+        torch.cuda.synchronize()
+        with pytest.raises(RuntimeError, match='did not arrive'):
+            sym.poll()
     finally:
         sym.destroy()
         _lib.check(lib.deepep_sym_free(dead), 'sym_free')

@@ -397,7 +397,8 @@ class ElasticBuffer(ExchangeMixin):
             idx64 = idx64.contiguous()
             w = topk_weights.contiguous() if topk_weights is not None else None
             # A cached handle already holds the routing (slots, counts, metadata, expert layout): the
-            # dispatch is then pack -> exchange -> copy, with no host sync (graph-capturable at EP = 1),
+            # dispatch is then pack -> exchange -> copy, with no host sync (graph-capturable at EP = 1
+            # and, over xGMI, at EP > 1),
             # as the reference's cached mode skips its notify phase (elastic.py:855-1033).
             cached = handle if handle is not None and handle._send_counts is not None else None
             # EP > 1 over xGMI: the pack kernel stores every row straight into its destination's

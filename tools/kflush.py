@@ -40,7 +40,7 @@ def main():
         buf.kernels.combine_reduce(MODE_FUSED, y, out, T, table=plan.local_table, row_weights=ex_w,
                                    wtable=plan.local_table, wsrc=ex_w, out_weights=out_w, stream=s)
 
-    def series(before, n=60):
+    def series(before, n=60):  # noqa: E306
         evs = []
         for _ in range(n):
             before()
@@ -53,8 +53,18 @@ def main():
         v = sorted(a.elapsed_time(b) * 1e3 for a, b in evs)
         return dict(median=round(v[len(v) // 2], 1), p10=round(v[len(v) // 10], 1), p90=round(v[9 * len(v) // 10], 1))
 
+    lib = buf.kernels.lib
     for _ in range(10):
         launch()
+    # output store policy under the write flush (0 plain, 1 nt, 2 sc1 = the default)
+    by_store = {}
+    for pol in (0, 1, 2):
+        assert lib.deepep_set_launch_config(0, -1, pol, 0) == 0
+        for _ in range(5):
+            launch()
+        by_store[pol] = {'none': series(lambda: None, 30), 'write_flush': series(lambda: flush.zero_(), 30)}
+    assert lib.deepep_set_launch_config(0, -1, -1, 0) == 0
+    print(json.dumps({'store_policy': by_store}))
     res = {
         'none': series(lambda: None),
         'write_flush': series(lambda: flush.zero_()),

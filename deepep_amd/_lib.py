@@ -11,7 +11,7 @@ from typing import Optional
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('DEEPEP_AMD_LIB', os.path.join(_HERE, 'libdeepep_amd.so'))
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 MODE_LOCAL, MODE_EPILOGUE, MODE_FUSED = 0, 1, 2
 
@@ -40,6 +40,8 @@ SIGNATURES = {
                                    _P]),
     'deepep_build_local_plan': (_I, [_P, _I, _I, _I, _I, _P, _I, _I, _P, _P, _P]),
     'deepep_set_launch_config': (_I, [_I, _I, _I, _I]),
+    'deepep_set_kernel_choice': (_I, [_I]),
+    'deepep_last_kernel_choice': (_I, []),
     'deepep_combine_buffer_size': (_I64, [_I, _I, _I, _I, _I]),
     'deepep_dispatch_route': (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P]),
     'deepep_dispatch_expert_counts': (_I, [_P, _I, _I, _I, _P, _P]),

@@ -25,6 +25,9 @@
 #include <stdarg.h>
 
 #include <algorithm>
+#include <map>
+#include <mutex>
+#include <tuple>
 
 #include "../../include/deepep_amd.h"
 
@@ -318,6 +321,147 @@ combine_rows_kernel(const Params p) {
         __builtin_amdgcn_raw_buffer_store_b128(result[v], orow, vidx[v] * 16, 0, kStoreAux);
 }
 
+// Streaming variant: one wave owns a whole unit (all of its column chunks), for slot tables of at
+// most kStreamWidth entries and hidden sizes that are a whole number of chunks.  The unit's slots,
+// weights and weight pass-through are handled once; then the chunks are walked in order with the
+// loads of chunk c + 1 (every valid row, kVPT x 16 B per lane) issued before chunk c is summed and
+// stored, so each wave keeps its rows streaming and writes its output row front to back.  The
+// arithmetic per chunk is exactly combine_rows_kernel's (same init, order, rounding), so the two
+// kernels give identical bits; measured on config 2: 161.3 us vs 171.3 us on one box
+// (tools/probe_tok.py).
+constexpr int kStreamWidth = 8;
+
+template <int kMode, bool kWeighted, int kVPT, int kStoreAux>
+__global__ void __launch_bounds__(256)
+combine_stream_kernel(const Params p) {
+    constexpr int kChunkVecs = 64 * kVPT;
+    const int lane = static_cast<int>(threadIdx.x) & 63;
+    const int64_t u = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+    if (u >= p.num_units) return;
+    const int nchunks = (p.hidden >> 3) / kChunkVecs;
+    const int width = p.table == nullptr ? 1 : p.table_width;
+
+    int32_t my_slot = -1;
+    float my_w = 0.0f;
+    if (lane < width) {
+        my_slot = p.table == nullptr ? static_cast<int32_t>(u) : p.table[u * p.table_stride + lane];
+        if (my_slot >= p.num_src_rows) {                     // never dereference a bad slot
+            if (p.error_flag != nullptr) atomicOr(p.error_flag, 1);
+            my_slot = -1;
+        }
+        if constexpr (kWeighted) my_w = my_slot >= 0 ? p.row_weights[my_slot] : 0.0f;
+    }
+    const uint64_t valid = __ballot(my_slot >= 0);
+    const int n = __popcll(valid);
+
+    uint16_t* const out_row = p.out_rows != nullptr ? reinterpret_cast<uint16_t*>(p.out_rows[u])
+                                                     : p.out + u * p.out_stride;
+    if (p.num_weights > 0 && lane < p.num_weights) {           // top-k weight pass-through, once per unit
+        const int64_t i = p.wtable == nullptr ? u * p.num_weights + lane
+                                              : static_cast<int64_t>(p.wtable[u * p.wtable_stride + lane]);
+        float* const ow = p.out_rows != nullptr
+                              ? reinterpret_cast<float*>(reinterpret_cast<char*>(out_row) + p.weights_offset)
+                              : p.out_weights + u * p.out_weights_stride;
+        const float v = i >= 0 ? p.wsrc[i] : 0.0f;
+        if (p.out_rows != nullptr)
+            __hip_atomic_store(ow + lane, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        else
+            ow[lane] = v;
+    }
+
+    // the valid lanes in ascending order (n <= kStreamWidth) with their row pointers and weights
+    const u32x4* rows[kStreamWidth];
+    float wj[kStreamWidth];
+    {
+        uint64_t rem = valid;
+#pragma unroll
+        for (int j = 0; j < kStreamWidth; ++j) {
+            const int l = rem != 0ull ? static_cast<int>(__builtin_ctzll(rem)) : 0;
+            const int32_t sj = __builtin_amdgcn_readlane(my_slot, l);
+            rows[j] = reinterpret_cast<const u32x4*>(p.src + static_cast<int64_t>(sj < 0 ? 0 : sj) * p.src_stride);
+            wj[j] = kWeighted ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_w), l)) : 0.0f;
+            rem &= rem - 1ull;
+        }
+    }
+    const bool has_bias0 = p.bias0 != nullptr, has_bias1 = p.bias1 != nullptr;
+    const bool has_bias = has_bias0 || has_bias1;
+    bool copy_row = false;
+    float init;
+    if constexpr (kMode == DEEPEP_MODE_LOCAL || kMode == DEEPEP_MODE_FUSED) {
+        copy_row = !kWeighted && n == 1;
+        init = (!kWeighted && n == 2) ? -0.0f : 0.0f;
+    } else {
+        init = (!kWeighted && !has_bias && n == 2) ? -0.0f : 0.0f;
+    }
+    const __amdgpu_buffer_rsrc_t orow = row_rsrc(out_row, p.hidden * 2);
+
+    auto issue = [&](int c, u32x4 (&v)[kStreamWidth][kVPT]) {
+#pragma unroll
+        for (int j = 0; j < kStreamWidth; ++j)
+            if (j < n) {
+#pragma unroll
+                for (int q = 0; q < kVPT; ++q) v[j][q] = load16<true>(rows[j] + c * kChunkVecs + q * 64 + lane);
+            }
+    };
+    auto finish = [&](int c, u32x4 (&v)[kStreamWidth][kVPT]) {
+        u32x4 result[kVPT];
+#pragma unroll
+        for (int q = 0; q < kVPT; ++q) {
+            const int vi = c * kChunkVecs + q * 64 + lane;
+            float acc[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc[e] = init;
+            if constexpr (kMode == DEEPEP_MODE_EPILOGUE) {     // bias0 then bias1 before the partials
+                if (has_bias0) acc_add(acc, *(reinterpret_cast<const u32x4*>(p.bias0 + u * p.hidden) + vi));
+                if (has_bias1) acc_add(acc, *(reinterpret_cast<const u32x4*>(p.bias1 + u * p.hidden) + vi));
+            }
+            if (copy_row) {
+                result[q] = v[0][q];
+            } else {
+#pragma unroll
+                for (int j = 0; j < kStreamWidth; ++j)
+                    if (j < n) {
+                        if constexpr (kWeighted) acc_fma(acc, v[j][q], wj[j]);
+                        else acc_add(acc, v[j][q]);
+                    }
+                result[q] = acc_pack(acc);
+            }
+            if constexpr (kMode == DEEPEP_MODE_FUSED) {
+                float a[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) a[e] = 0.0f;
+                if (has_bias0) acc_add(a, *(reinterpret_cast<const u32x4*>(p.bias0 + u * p.hidden) + vi));
+                if (has_bias1) acc_add(a, *(reinterpret_cast<const u32x4*>(p.bias1 + u * p.hidden) + vi));
+                if (n > 0) acc_add(a, result[q]);
+                result[q] = acc_pack(a);
+            }
+            __builtin_amdgcn_raw_buffer_store_b128(result[q], orow, vi * 16, 0, kStoreAux);
+        }
+    };
+    u32x4 va[kStreamWidth][kVPT], vb[kStreamWidth][kVPT];
+    issue(0, va);
+    for (int c = 0; c < nchunks; c += 2) {
+        if (c + 1 < nchunks) issue(c + 1, vb);
+        finish(c, va);
+        if (c + 1 >= nchunks) break;
+        if (c + 2 < nchunks) issue(c + 2, va);
+        finish(c + 1, vb);
+    }
+}
+
+template <int kMode, bool kWeighted, int kVPT>
+void launch_stream(const Params& p, int policy, hipStream_t stream) {
+    const dim3 grid(static_cast<unsigned>((p.num_units + 3) / 4)), block(256);
+    if (policy == 0)
+        hipLaunchKernelGGL((combine_stream_kernel<kMode, kWeighted, kVPT, 0>), grid, block, 0, stream, p);
+    else if (policy == 1)
+        hipLaunchKernelGGL((combine_stream_kernel<kMode, kWeighted, kVPT, kAuxNT>), grid, block, 0, stream, p);
+    else if (policy == 3)
+        hipLaunchKernelGGL((combine_stream_kernel<kMode, kWeighted, kVPT, kAuxSys>), grid, block, 0, stream, p);
+    else
+        hipLaunchKernelGGL((combine_stream_kernel<kMode, kWeighted, kVPT, kAuxSC1>), grid, block, 0, stream, p);
+}
+
 struct LaunchConfig {
     int vec_per_lane = 0;        // 0: auto (16-byte vectors per lane per source row and item)
     int stage_lds = -1;          // -1: auto (1 = LDS staging per workgroup, 0 = per-wave registers)
@@ -325,6 +469,17 @@ struct LaunchConfig {
     int rows_in_flight = 0;      // 0: auto (source rows loaded per lane before accumulating: 2, 4 or 8)
 };
 LaunchConfig g_config;
+
+// Item kernel vs streaming kernel.  Both give identical bits, but which is faster depends on the
+// machine: on config 2 the streaming kernel ran 161 us against 171 us on one MI355X box and
+// 187-196 us against 175 us on another (tools/probe_tok.py, interleaved in one process).  So by
+// default the first large launch of each shape times both on the caller's stream (three launches
+// each, same arguments: the kernels are pure functions of their inputs) and keeps the faster; a
+// launch being captured into a graph, or a small one, takes the item kernel without tuning.
+int g_kernel_choice = -1;        // -1 autotune, 0 item kernel, 1 streaming kernel
+int g_last_choice = 0;
+std::mutex g_tune_mutex;
+std::map<std::tuple<int, int, int, int, int, int, int>, int> g_tuned;
 
 template <int kMode, bool kWeighted, int kVPT, bool kFull, int kAux, bool kLDS, int kWaves, int kGroup>
 void launch_shape(const Params& p, int64_t items, hipStream_t stream) {
@@ -561,16 +716,81 @@ int launch_combine(int mode, int weighted, const Params& p, deepep_stream_t stre
     sh.waves = p.units_per_block == 4 ? 4 : (p.units_per_block == 8 ? 8 : (mode == DEEPEP_MODE_LOCAL ? 4 : 8));
     sh.group = g_config.rows_in_flight > 0 ? g_config.rows_in_flight : 8;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    if (mode == DEEPEP_MODE_LOCAL) {
-        if (weighted) launch_vpt<DEEPEP_MODE_LOCAL, true>(p, sh, s);
-        else launch_vpt<DEEPEP_MODE_LOCAL, false>(p, sh, s);
-    } else if (mode == DEEPEP_MODE_EPILOGUE) {
-        if (weighted) launch_vpt<DEEPEP_MODE_EPILOGUE, true>(p, sh, s);
-        else launch_vpt<DEEPEP_MODE_EPILOGUE, false>(p, sh, s);
-    } else {
-        if (weighted) launch_vpt<DEEPEP_MODE_FUSED, true>(p, sh, s);
-        else launch_vpt<DEEPEP_MODE_FUSED, false>(p, sh, s);
+    // The streaming kernel (one wave per unit, chunks pipelined) whenever it applies and the shape
+    // is automatic: an explicit units_per_block / LDS / rows-in-flight setting selects the item
+    // kernel (which also serves tables wider than kStreamWidth and ragged hidden sizes).
+    const bool stream_ok = (p.table == nullptr || p.table_width <= kStreamWidth) && nvec % (64 * sh.vpt) == 0 &&
+                           p.units_per_block == 0 && g_config.stage_lds < 0 && g_config.rows_in_flight == 0;
+    auto launch_items = [&]() {
+        if (mode == DEEPEP_MODE_LOCAL) {
+            if (weighted) launch_vpt<DEEPEP_MODE_LOCAL, true>(p, sh, s);
+            else launch_vpt<DEEPEP_MODE_LOCAL, false>(p, sh, s);
+        } else if (mode == DEEPEP_MODE_EPILOGUE) {
+            if (weighted) launch_vpt<DEEPEP_MODE_EPILOGUE, true>(p, sh, s);
+            else launch_vpt<DEEPEP_MODE_EPILOGUE, false>(p, sh, s);
+        } else {
+            if (weighted) launch_vpt<DEEPEP_MODE_FUSED, true>(p, sh, s);
+            else launch_vpt<DEEPEP_MODE_FUSED, false>(p, sh, s);
+        }
+    };
+    auto launch_streaming = [&]() {
+#define DEEPEP_STREAM(M, W) \
+        (sh.vpt == 1 ? launch_stream<M, W, 1>(p, sh.policy, s) : launch_stream<M, W, 2>(p, sh.policy, s))
+        if (mode == DEEPEP_MODE_LOCAL) {
+            if (weighted) DEEPEP_STREAM(DEEPEP_MODE_LOCAL, true); else DEEPEP_STREAM(DEEPEP_MODE_LOCAL, false);
+        } else if (mode == DEEPEP_MODE_EPILOGUE) {
+            if (weighted) DEEPEP_STREAM(DEEPEP_MODE_EPILOGUE, true); else DEEPEP_STREAM(DEEPEP_MODE_EPILOGUE, false);
+        } else {
+            if (weighted) DEEPEP_STREAM(DEEPEP_MODE_FUSED, true); else DEEPEP_STREAM(DEEPEP_MODE_FUSED, false);
+        }
+#undef DEEPEP_STREAM
+    };
+    int choice = 0;
+    if (stream_ok) {
+        if (g_kernel_choice >= 0) {
+            choice = g_kernel_choice;
+        } else if (static_cast<int64_t>(p.num_units) * nvec >= (int64_t(1) << 20)) {   // >= 16 MiB written
+            int units_log2 = 0;
+            while ((int64_t(1) << (units_log2 + 1)) <= p.num_units) ++units_log2;
+            const auto key = std::make_tuple(mode, weighted, sh.vpt, sh.policy, p.table == nullptr ? 1 : p.table_width,
+                                             p.hidden, units_log2);
+            std::lock_guard<std::mutex> lock(g_tune_mutex);
+            const auto it = g_tuned.find(key);
+            if (it != g_tuned.end()) {
+                choice = it->second;
+            } else {
+                hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+                if (hipStreamIsCapturing(s, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone) {
+                    hipEvent_t e[3] = {nullptr, nullptr, nullptr};
+                    bool ok = true;
+                    for (auto& ev : e) ok = ok && hipEventCreate(&ev) == hipSuccess;
+                    if (ok) {
+                        launch_items();
+                        launch_streaming();                       // warm both
+                        ok = hipEventRecord(e[0], s) == hipSuccess;
+                        for (int r = 0; r < 3; ++r) launch_items();
+                        ok = ok && hipEventRecord(e[1], s) == hipSuccess;
+                        for (int r = 0; r < 3; ++r) launch_streaming();
+                        ok = ok && hipEventRecord(e[2], s) == hipSuccess;
+                        float t_items = 0.0f, t_stream = 0.0f;
+                        ok = ok && hipEventSynchronize(e[2]) == hipSuccess &&
+                             hipEventElapsedTime(&t_items, e[0], e[1]) == hipSuccess &&
+                             hipEventElapsedTime(&t_stream, e[1], e[2]) == hipSuccess;
+                        if (ok) {
+                            choice = t_stream < t_items ? 1 : 0;
+                            g_tuned[key] = choice;
+                        }
+                    }
+                    for (auto& ev : e)
+                        if (ev != nullptr) (void)hipEventDestroy(ev);
+                    (void)hipGetLastError();
+                }
+            }
+        }
     }
+    g_last_choice = choice;
+    if (choice == 1) launch_streaming();
+    else launch_items();
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess)
         return set_error(DEEPEP_ERR_HIP, "combine launch failed: %s", hipGetErrorString(err));
@@ -613,6 +833,16 @@ int deepep_build_local_plan(const int32_t* src_metadata, int num_recv_tokens, in
         return set_error(DEEPEP_ERR_HIP, "plan launch failed: %s", hipGetErrorString(err));
     return DEEPEP_OK;
 }
+
+int deepep_set_kernel_choice(int choice) {
+    if (choice < -1 || choice > 1) return set_error(DEEPEP_ERR_INVALID_ARG, "kernel choice must be -1, 0 or 1");
+    std::lock_guard<std::mutex> lock(g_tune_mutex);
+    g_kernel_choice = choice;
+    if (choice == -1) g_tuned.clear();
+    return DEEPEP_OK;
+}
+
+int deepep_last_kernel_choice(void) { return g_last_choice; }
 
 int deepep_set_launch_config(int vec_per_lane, int stage_lds, int store_policy, int rows_in_flight) {
     if (vec_per_lane < 0 || vec_per_lane > 2 || stage_lds < -1 || stage_lds > 1 || store_policy < -1 ||

@@ -45,7 +45,7 @@ extern "C" {
 
 typedef struct ihipStream_t* deepep_stream_t;   /* == hipStream_t */
 
-#define DEEPEP_AMD_ABI_VERSION 8
+#define DEEPEP_AMD_ABI_VERSION 9
 
 #define DEEPEP_OK               0
 #define DEEPEP_ERR_INVALID_ARG  (-1)
@@ -124,6 +124,21 @@ int deepep_build_local_plan(const int32_t* src_metadata, int num_recv_tokens, in
  * The results are identical for every configuration; only the speed changes.
  */
 int deepep_set_launch_config(int vec_per_lane, int stage_lds, int store_policy, int rows_in_flight);
+
+/*
+ * Kernel for deepep_combine_reduce / _scatter when the shape is automatic (units_per_block 0, default
+ * launch config), the slot table is at most 8 wide and hidden is a whole number of column chunks:
+ *   0  the item kernel (one wave per (unit, column chunk));
+ *   1  the streaming kernel (one wave per unit, the next chunk's rows loading while the current one
+ *      is summed);
+ *  -1  (default) autotune: the first launch of each shape that writes >= 16 MiB times both kernels
+ *      on the caller's stream (3 launches each, one host sync) and keeps the faster; launches that
+ *      are being captured into a graph, or smaller, use the item kernel.  Setting -1 forgets earlier
+ *      choices.
+ * Both kernels produce identical bits.  deepep_last_kernel_choice() says which one the last launch used.
+ */
+int deepep_set_kernel_choice(int choice);
+int deepep_last_kernel_choice(void);
 
 /* ------------------------------------------------------------------ dispatch
  * Packed token row exchanged between ranks (byte offsets, all 16-byte aligned except as noted):

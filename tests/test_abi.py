@@ -33,7 +33,7 @@ def test_exports_every_declared_symbol(lib):
 
 
 def test_abi_version(lib):
-    assert lib.deepep_amd_abi_version() == 8
+    assert lib.deepep_amd_abi_version() == 9
 
 
 def test_invalid_arguments_are_rejected_without_a_gpu(lib):

@@ -377,15 +377,23 @@ def test_config2_full_size_bitwise(weighted, T, skew):
     x = torch.zeros((T, H), dtype=torch.bfloat16, device='cuda')
     _, _, ex_w, handle, _ = buf.dispatch(x, topk_idx=idx, topk_weights=w, num_experts=E, do_expand=True)
     y = torch.randn((handle.num_expanded_tokens, H), device='cuda', generator=g).to(torch.bfloat16)
-    out, out_w, _ = buf.combine(y, handle, topk_weights=ex_w, apply_topk_weights=weighted)
-    torch.cuda.synchronize()
     meta = handle.recv_src_metadata.cpu().numpy()
     part, _ = oracle.phase_a(_u16(y), meta, K, True, ex_w.cpu().numpy(), weighted=weighted)
     recv = np.zeros((1, T, H), np.uint16)
     recv[0, meta[:, 0] % T] = part
     ref, _ = oracle.phase_b(recv, None, idx.cpu().numpy(), E, 1, True, True)
-    assert np.array_equal(_u16(out), ref)
-    assert torch.equal(out_w, w)
+    lib = buf.kernels.lib
+    try:
+        # the item kernel, the streaming kernel, and the autotuned choice between them
+        for choice in (0, 1, -1):
+            assert lib.deepep_set_kernel_choice(choice) == 0
+            out, out_w, _ = buf.combine(y, handle, topk_weights=ex_w, apply_topk_weights=weighted)
+            torch.cuda.synchronize()
+            assert lib.deepep_last_kernel_choice() in ((choice,) if choice >= 0 else (0, 1))
+            assert np.array_equal(_u16(out), ref), f'kernel choice {choice}'
+            assert torch.equal(out_w, w)
+    finally:
+        lib.deepep_set_kernel_choice(-1)
     if weighted:
         # and within the reference's weighted tolerance of the exact sum (test_low_latency.py:178-181)
         yd = y.double()

@@ -36,6 +36,16 @@ def _case(seed: int):
     return rng, T, H, K, E, masked
 
 
+@pytest.fixture(params=[0, 1], ids=['item', 'stream'])
+def kernel_choice(request):
+    """Both combine kernels (deepep_set_kernel_choice): the item kernel and the streaming kernel."""
+    from deepep_amd import _lib
+    lib = _lib.load()
+    assert lib.deepep_set_kernel_choice(request.param) == 0
+    yield request.param
+    lib.deepep_set_kernel_choice(-1)
+
+
 @pytest.fixture(scope='module')
 def group():
     import torch.distributed as dist
@@ -47,7 +57,7 @@ def group():
 
 
 @pytest.mark.parametrize('seed', range(32))
-def test_random_shapes_ep1(group, seed):
+def test_random_shapes_ep1(group, seed, kernel_choice):
     from deepep_amd import ElasticBuffer
     rng, T, H, K, E, masked = _case(seed)
     idx = np.array([rng.permutation(E)[:K] for _ in range(T)], dtype=np.int64).reshape(T, K)
@@ -192,7 +202,7 @@ def _ep_thread(rank, world, seed, comm, results):
 
 
 @pytest.mark.parametrize('case', range(16))
-def test_random_shapes_ep_sim(case, monkeypatch):
+def test_random_shapes_ep_sim(case, monkeypatch, kernel_choice):
     """Random EP = 2..8 cases (ragged per-rank batches incl. empty ranks, top-k 1..8, R > K and
     R <= K layouts, chunked and one-shot exchange), all ranks simulated by threads on the GPU."""
     import threading

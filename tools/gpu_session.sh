@@ -34,6 +34,7 @@ for step in "$@"; do
         kvar)   run kvar 300 python tools/kvar.py ;;
         kflush) run kflush 300 python tools/kflush.py ;;
         probetok) run probetok 300 python tools/probe_tok.py ;;
+        kplace) run kplace 300 python tools/kplace.py ;;
         kphase) run kphase 300 python tools/kphase.py ;;
         kcu)    run kcu 300 python tools/kcu.py ;;
         cumask) run cumask 120 python tools/probe_cumask.py ;;

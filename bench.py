@@ -539,8 +539,9 @@ def main():
         workload = f'combine_fused_{"weighted" if weighted else "plain"}_t{T}_h{H}_k{K}'
         roofline = dict(bound='hbm', achieved=round(achieved, 1), peak=HBM_PEAK_GBPS, unit='GB/s',
                         frac=round(achieved / HBM_PEAK_GBPS, 4), traffic=_pmc_traffic(workload),
-                        kernel=('combine_stream_kernel<FUSED>' if kern.lib.deepep_last_kernel_choice() == 1
-                                else 'combine_rows_kernel<FUSED>'), kernel_us=round(kern_us, 2),
+                        kernel=('combine_rows_kernel<FUSED>', 'combine_stream_kernel<FUSED, 2 vectors/lane>',
+                                'combine_stream_kernel<FUSED, 1 vector/lane>')[kern.lib.deepep_last_kernel_choice()],
+                        kernel_us=round(kern_us, 2),
                         kernel_us_flushed_median=None if kern_us_flushed is None else round(kern_us_flushed, 2),
                         kernel_us_read_flushed_median=(None if kern_us_read_flushed is None
                                                        else round(kern_us_read_flushed, 2)),

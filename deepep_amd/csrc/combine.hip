@@ -476,7 +476,7 @@ LaunchConfig g_config;
 // default the first large launch of each shape times both on the caller's stream (three launches
 // each, same arguments: the kernels are pure functions of their inputs) and keeps the faster; a
 // launch being captured into a graph, or a small one, takes the item kernel without tuning.
-int g_kernel_choice = -1;        // -1 autotune, 0 item kernel, 1 streaming kernel
+int g_kernel_choice = -1;        // -1 autotune, 0 item kernel, 1 streaming kernel, 2 streaming, 1 vector/lane
 int g_last_choice = 0;
 std::mutex g_tune_mutex;
 std::map<std::tuple<int, int, int, int, int, int, int>, int> g_tuned;
@@ -733,9 +733,9 @@ int launch_combine(int mode, int weighted, const Params& p, deepep_stream_t stre
             else launch_vpt<DEEPEP_MODE_FUSED, false>(p, sh, s);
         }
     };
-    auto launch_streaming = [&]() {
+    auto launch_streaming = [&](int vpt) {
 #define DEEPEP_STREAM(M, W) \
-        (sh.vpt == 1 ? launch_stream<M, W, 1>(p, sh.policy, s) : launch_stream<M, W, 2>(p, sh.policy, s))
+        (vpt == 1 ? launch_stream<M, W, 1>(p, sh.policy, s) : launch_stream<M, W, 2>(p, sh.policy, s))
         if (mode == DEEPEP_MODE_LOCAL) {
             if (weighted) DEEPEP_STREAM(DEEPEP_MODE_LOCAL, true); else DEEPEP_STREAM(DEEPEP_MODE_LOCAL, false);
         } else if (mode == DEEPEP_MODE_EPILOGUE) {
@@ -745,6 +745,13 @@ int launch_combine(int mode, int weighted, const Params& p, deepep_stream_t stre
         }
 #undef DEEPEP_STREAM
     };
+    // candidates: 0 item kernel, 1 streaming kernel (sh.vpt vectors per lane), 2 streaming kernel with
+    // 1 vector per lane (half the registers, more waves per SIMD)
+    auto launch_choice = [&](int c) {
+        if (c == 0) launch_items();
+        else launch_streaming(c == 2 ? 1 : sh.vpt);
+    };
+    constexpr int kCandidates = 3;
     int choice = 0;
     if (stream_ok) {
         if (g_kernel_choice >= 0) {
@@ -761,25 +768,25 @@ int launch_combine(int mode, int weighted, const Params& p, deepep_stream_t stre
             } else {
                 hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
                 if (hipStreamIsCapturing(s, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone) {
-                    hipEvent_t e[3] = {nullptr, nullptr, nullptr};
+                    hipEvent_t e[kCandidates + 1] = {};
                     bool ok = true;
                     for (auto& ev : e) ok = ok && hipEventCreate(&ev) == hipSuccess;
                     if (ok) {
-                        launch_items();
-                        launch_streaming();                       // warm both
+                        for (int c = 0; c < kCandidates; ++c) launch_choice(c);          // warm every candidate
                         ok = hipEventRecord(e[0], s) == hipSuccess;
-                        for (int r = 0; r < 3; ++r) launch_items();
-                        ok = ok && hipEventRecord(e[1], s) == hipSuccess;
-                        for (int r = 0; r < 3; ++r) launch_streaming();
-                        ok = ok && hipEventRecord(e[2], s) == hipSuccess;
-                        float t_items = 0.0f, t_stream = 0.0f;
-                        ok = ok && hipEventSynchronize(e[2]) == hipSuccess &&
-                             hipEventElapsedTime(&t_items, e[0], e[1]) == hipSuccess &&
-                             hipEventElapsedTime(&t_stream, e[1], e[2]) == hipSuccess;
-                        if (ok) {
-                            choice = t_stream < t_items ? 1 : 0;
-                            g_tuned[key] = choice;
+                        for (int c = 0; c < kCandidates; ++c) {
+                            for (int r = 0; r < 3; ++r) launch_choice(c);
+                            ok = ok && hipEventRecord(e[c + 1], s) == hipSuccess;
                         }
+                        ok = ok && hipEventSynchronize(e[kCandidates]) == hipSuccess;
+                        float best = 0.0f;
+                        for (int c = 0; ok && c < kCandidates; ++c) {
+                            float t = 0.0f;
+                            ok = hipEventElapsedTime(&t, e[c], e[c + 1]) == hipSuccess;
+                            if (ok && (c == 0 || t < best)) best = t, choice = c;
+                        }
+                        if (ok) g_tuned[key] = choice;
+                        else choice = 0;
                     }
                     for (auto& ev : e)
                         if (ev != nullptr) (void)hipEventDestroy(ev);
@@ -789,8 +796,7 @@ int launch_combine(int mode, int weighted, const Params& p, deepep_stream_t stre
         }
     }
     g_last_choice = choice;
-    if (choice == 1) launch_streaming();
-    else launch_items();
+    launch_choice(choice);
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess)
         return set_error(DEEPEP_ERR_HIP, "combine launch failed: %s", hipGetErrorString(err));
@@ -835,7 +841,7 @@ int deepep_build_local_plan(const int32_t* src_metadata, int num_recv_tokens, in
 }
 
 int deepep_set_kernel_choice(int choice) {
-    if (choice < -1 || choice > 1) return set_error(DEEPEP_ERR_INVALID_ARG, "kernel choice must be -1, 0 or 1");
+    if (choice < -1 || choice > 2) return set_error(DEEPEP_ERR_INVALID_ARG, "kernel choice must be -1, 0, 1 or 2");
     std::lock_guard<std::mutex> lock(g_tune_mutex);
     g_kernel_choice = choice;
     if (choice == -1) g_tuned.clear();

@@ -130,12 +130,13 @@ int deepep_set_launch_config(int vec_per_lane, int stage_lds, int store_policy, 
  * launch config), the slot table is at most 8 wide and hidden is a whole number of column chunks:
  *   0  the item kernel (one wave per (unit, column chunk));
  *   1  the streaming kernel (one wave per unit, the next chunk's rows loading while the current one
- *      is summed);
- *  -1  (default) autotune: the first launch of each shape that writes >= 16 MiB times both kernels
- *      on the caller's stream (3 launches each, one host sync) and keeps the faster; launches that
+ *      is summed), 2 x 16 B per lane and row when hidden allows;
+ *   2  the streaming kernel with 16 B per lane and row (half the registers, more waves per SIMD);
+ *  -1  (default) autotune: the first launch of each shape that writes >= 16 MiB times the three
+ *      on the caller's stream (3 launches each, one host sync) and keeps the fastest; launches that
  *      are being captured into a graph, or smaller, use the item kernel.  Setting -1 forgets earlier
  *      choices.
- * Both kernels produce identical bits.  deepep_last_kernel_choice() says which one the last launch used.
+ * All of them produce identical bits.  deepep_last_kernel_choice() says which one the last launch used.
  */
 int deepep_set_kernel_choice(int choice);
 int deepep_last_kernel_choice(void);

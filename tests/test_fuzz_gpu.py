@@ -36,9 +36,10 @@ def _case(seed: int):
     return rng, T, H, K, E, masked
 
 
-@pytest.fixture(params=[0, 1], ids=['item', 'stream'])
+@pytest.fixture(params=[0, 1, 2], ids=['item', 'stream', 'stream_vpt1'])
 def kernel_choice(request):
-    """Both combine kernels (deepep_set_kernel_choice): the item kernel and the streaming kernel."""
+    """Every combine kernel (deepep_set_kernel_choice): the item kernel and the streaming kernel at 2 and 1
+    vectors per lane."""
     from deepep_amd import _lib
     lib = _lib.load()
     assert lib.deepep_set_kernel_choice(request.param) == 0

@@ -54,8 +54,10 @@ def main():
     # as in bench.py and plain, interleaved rounds
     for rnd in range(3):
         for weighted in (True, False):
-            for upb, name in ((8, 'item'), (0, 'stream')):
-                res[f'ab r{rnd} {"w" if weighted else "p"} {name}'] = round(timeit(lib_kernel(upb, weighted), 50, 5), 1)
+            for choice, name in ((0, 'item'), (1, 'stream'), (2, 'stream_vpt1')):
+                assert buf.kernels.lib.deepep_set_kernel_choice(choice) == 0
+                res[f'ab r{rnd} {"w" if weighted else "p"} {name}'] = round(timeit(lib_kernel(0, weighted), 50, 5), 1)
+    buf.kernels.lib.deepep_set_kernel_choice(-1)
     for rnd in range(2):
         for vpt in (1, 2):
             for aux in (16, 2):

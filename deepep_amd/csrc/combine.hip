@@ -336,11 +336,11 @@ __global__ void __launch_bounds__(256)
 combine_stream_kernel(const Params p) {
     constexpr int kChunkVecs = 64 * kVPT;
     const int lane = static_cast<int>(threadIdx.x) & 63;
-    const int64_t u = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
-    if (u >= p.num_units) return;
     const int nchunks = (p.hidden >> 3) / kChunkVecs;
     const int width = p.table == nullptr ? 1 : p.table_width;
-
+    // one unit per wave, or (a grid capped at the resident capacity) units strided over the waves
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * 4;
+    for (int64_t u = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6); u < p.num_units; u += stride) {
     int32_t my_slot = -1;
     float my_w = 0.0f;
     if (lane < width) {
@@ -447,19 +447,37 @@ combine_stream_kernel(const Params p) {
         if (c + 2 < nchunks) issue(c + 2, va);
         finish(c + 1, vb);
     }
+    }
+}
+
+// persistent: the grid is capped at the workgroups the chip holds at once (occupancy x CUs), so
+// there is no partial last round of long-lived waves; otherwise one unit per wave
+template <int kMode, bool kWeighted, int kVPT, int kAux>
+void launch_stream_policy(const Params& p, bool persistent, hipStream_t stream) {
+    const auto kernel = combine_stream_kernel<kMode, kWeighted, kVPT, kAux>;
+    int64_t blocks = (p.num_units + 3) / 4;
+    if (persistent) {
+        static int cap = 0;                       // per template instance
+        if (cap == 0) {
+            int per_cu = 0, dev = 0, cus = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) == hipSuccess &&
+                hipGetDevice(&dev) == hipSuccess &&
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+                cap = std::max(1, per_cu * cus);
+            else
+                cap = 1 << 30;
+        }
+        blocks = std::min<int64_t>(blocks, cap);
+    }
+    hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream, p);
 }
 
 template <int kMode, bool kWeighted, int kVPT>
-void launch_stream(const Params& p, int policy, hipStream_t stream) {
-    const dim3 grid(static_cast<unsigned>((p.num_units + 3) / 4)), block(256);
-    if (policy == 0)
-        hipLaunchKernelGGL((combine_stream_kernel<kMode, kWeighted, kVPT, 0>), grid, block, 0, stream, p);
-    else if (policy == 1)
-        hipLaunchKernelGGL((combine_stream_kernel<kMode, kWeighted, kVPT, kAuxNT>), grid, block, 0, stream, p);
-    else if (policy == 3)
-        hipLaunchKernelGGL((combine_stream_kernel<kMode, kWeighted, kVPT, kAuxSys>), grid, block, 0, stream, p);
-    else
-        hipLaunchKernelGGL((combine_stream_kernel<kMode, kWeighted, kVPT, kAuxSC1>), grid, block, 0, stream, p);
+void launch_stream(const Params& p, int policy, bool persistent, hipStream_t stream) {
+    if (policy == 0) launch_stream_policy<kMode, kWeighted, kVPT, 0>(p, persistent, stream);
+    else if (policy == 1) launch_stream_policy<kMode, kWeighted, kVPT, kAuxNT>(p, persistent, stream);
+    else if (policy == 3) launch_stream_policy<kMode, kWeighted, kVPT, kAuxSys>(p, persistent, stream);
+    else launch_stream_policy<kMode, kWeighted, kVPT, kAuxSC1>(p, persistent, stream);
 }
 
 struct LaunchConfig {
@@ -476,7 +494,7 @@ LaunchConfig g_config;
 // default the first large launch of each shape times both on the caller's stream (three launches
 // each, same arguments: the kernels are pure functions of their inputs) and keeps the faster; a
 // launch being captured into a graph, or a small one, takes the item kernel without tuning.
-int g_kernel_choice = -1;        // -1 autotune, 0 item kernel, 1 streaming kernel, 2 streaming, 1 vector/lane
+int g_kernel_choice = -1;        // -1 autotune, else a candidate of launch_combine (0 item kernel, 1-3 streaming)
 int g_last_choice = 0;
 std::mutex g_tune_mutex;
 std::map<std::tuple<int, int, int, int, int, int, int>, int> g_tuned;
@@ -733,9 +751,10 @@ int launch_combine(int mode, int weighted, const Params& p, deepep_stream_t stre
             else launch_vpt<DEEPEP_MODE_FUSED, false>(p, sh, s);
         }
     };
-    auto launch_streaming = [&](int vpt) {
+    auto launch_streaming = [&](int vpt, bool persistent) {
 #define DEEPEP_STREAM(M, W) \
-        (vpt == 1 ? launch_stream<M, W, 1>(p, sh.policy, s) : launch_stream<M, W, 2>(p, sh.policy, s))
+        (vpt == 1 ? launch_stream<M, W, 1>(p, sh.policy, persistent, s) \
+                  : launch_stream<M, W, 2>(p, sh.policy, persistent, s))
         if (mode == DEEPEP_MODE_LOCAL) {
             if (weighted) DEEPEP_STREAM(DEEPEP_MODE_LOCAL, true); else DEEPEP_STREAM(DEEPEP_MODE_LOCAL, false);
         } else if (mode == DEEPEP_MODE_EPILOGUE) {
@@ -746,12 +765,13 @@ int launch_combine(int mode, int weighted, const Params& p, deepep_stream_t stre
 #undef DEEPEP_STREAM
     };
     // candidates: 0 item kernel, 1 streaming kernel (sh.vpt vectors per lane), 2 streaming kernel with
-    // 1 vector per lane (half the registers, more waves per SIMD)
+    // 1 vector per lane (half the registers, more waves per SIMD), 3 streaming kernel on a persistent
+    // grid (sh.vpt vectors per lane)
     auto launch_choice = [&](int c) {
         if (c == 0) launch_items();
-        else launch_streaming(c == 2 ? 1 : sh.vpt);
+        else launch_streaming(c == 2 ? 1 : sh.vpt, c == 3);
     };
-    constexpr int kCandidates = 3;
+    constexpr int kCandidates = 4;
     int choice = 0;
     if (stream_ok) {
         if (g_kernel_choice >= 0) {
@@ -841,7 +861,7 @@ int deepep_build_local_plan(const int32_t* src_metadata, int num_recv_tokens, in
 }
 
 int deepep_set_kernel_choice(int choice) {
-    if (choice < -1 || choice > 2) return set_error(DEEPEP_ERR_INVALID_ARG, "kernel choice must be -1, 0, 1 or 2");
+    if (choice < -1 || choice > 3) return set_error(DEEPEP_ERR_INVALID_ARG, "kernel choice must be -1, 0, 1, 2 or 3");
     std::lock_guard<std::mutex> lock(g_tune_mutex);
     g_kernel_choice = choice;
     if (choice == -1) g_tuned.clear();

@@ -132,7 +132,9 @@ int deepep_set_launch_config(int vec_per_lane, int stage_lds, int store_policy, 
  *   1  the streaming kernel (one wave per unit, the next chunk's rows loading while the current one
  *      is summed), 2 x 16 B per lane and row when hidden allows;
  *   2  the streaming kernel with 16 B per lane and row (half the registers, more waves per SIMD);
- *  -1  (default) autotune: the first launch of each shape that writes >= 16 MiB times the three
+ *   3  the streaming kernel (as 1) on a persistent grid: as many workgroups as the chip holds at
+ *      once, units strided over the waves;
+ *  -1  (default) autotune: the first launch of each shape that writes >= 16 MiB times the four
  *      on the caller's stream (3 launches each, one host sync) and keeps the fastest; launches that
  *      are being captured into a graph, or smaller, use the item kernel.  Setting -1 forgets earlier
  *      choices.

@@ -384,12 +384,12 @@ def test_config2_full_size_bitwise(weighted, T, skew):
     ref, _ = oracle.phase_b(recv, None, idx.cpu().numpy(), E, 1, True, True)
     lib = buf.kernels.lib
     try:
-        # the item kernel, the streaming kernel (2 and 1 vectors per lane), and the autotuned choice
-        for choice in (0, 1, 2, -1):
+        # the item kernel, the streaming kernel (2 and 1 vectors per lane, persistent), and the autotuned choice
+        for choice in (0, 1, 2, 3, -1):
             assert lib.deepep_set_kernel_choice(choice) == 0
             out, out_w, _ = buf.combine(y, handle, topk_weights=ex_w, apply_topk_weights=weighted)
             torch.cuda.synchronize()
-            assert lib.deepep_last_kernel_choice() in ((choice,) if choice >= 0 else (0, 1, 2))
+            assert lib.deepep_last_kernel_choice() in ((choice,) if choice >= 0 else (0, 1, 2, 3))
             assert np.array_equal(_u16(out), ref), f'kernel choice {choice}'
             assert torch.equal(out_w, w)
     finally:

@@ -36,10 +36,10 @@ def _case(seed: int):
     return rng, T, H, K, E, masked
 
 
-@pytest.fixture(params=[0, 1, 2], ids=['item', 'stream', 'stream_vpt1'])
+@pytest.fixture(params=[0, 1, 2, 3], ids=['item', 'stream', 'stream_vpt1', 'stream_persistent'])
 def kernel_choice(request):
     """Every combine kernel (deepep_set_kernel_choice): the item kernel and the streaming kernel at 2 and 1
-    vectors per lane."""
+    vectors per lane and on a persistent grid."""
     from deepep_amd import _lib
     lib = _lib.load()
     assert lib.deepep_set_kernel_choice(request.param) == 0

@@ -35,6 +35,9 @@ for step in "$@"; do
         kflush) run kflush 300 python tools/kflush.py ;;
         probetok) run probetok 300 python tools/probe_tok.py ;;
         kplace) run kplace 300 python tools/kplace.py ;;
+        kplacetlb) export KPLACE_ITERS=4 KPLACE_WARM=1 KPLACE_ROUNDS=1
+                run kplacetlb 300 rocprofv3 --kernel-trace --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_STALL_MULTI_MISS_sum -d $OUT/kplacetlb -o pmc --output-format csv -- python3 tools/kplace.py
+                unset KPLACE_ITERS KPLACE_WARM KPLACE_ROUNDS ;;
         kphase) run kphase 300 python tools/kphase.py ;;
         kcu)    run kcu 300 python tools/kcu.py ;;
         cumask) run cumask 120 python tools/probe_cumask.py ;;

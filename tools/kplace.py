@@ -36,13 +36,14 @@ def main():
     ow = torch.empty((T, K), dtype=torch.float32, device='cuda')
     s = torch.cuda.current_stream()
     res = {}
-    for rnd in range(3):
+    iters, warm = int(os.environ.get('KPLACE_ITERS', 30)), int(os.environ.get('KPLACE_WARM', 3))
+    for rnd in range(int(os.environ.get('KPLACE_ROUNDS', 3))):
         for i, y in enumerate(copies):
             for j, out in enumerate(outs):
                 def f():
                     buf.kernels.combine_reduce(MODE_FUSED, y, out, T, table=table, row_weights=ex_w, wtable=table,
                                                wsrc=ex_w, out_weights=ow, stream=s)
-                res[f'r{rnd} rows{i} out{j}'] = round(timeit(f, 30, 3), 1)
+                res[f'r{rnd} rows{i} out{j}'] = round(timeit(f, iters, warm), 1)
     lib.deepep_set_kernel_choice(-1)
     print(json.dumps(res))
     dist.destroy_process_group()

@@ -36,7 +36,8 @@ for step in "$@"; do
         probetok) run probetok 300 python tools/probe_tok.py ;;
         kplace) run kplace 300 python tools/kplace.py ;;
         kplacetlb) export KPLACE_ITERS=4 KPLACE_WARM=1 KPLACE_ROUNDS=1
-                run kplacetlb 300 rocprofv3 --kernel-trace --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_STALL_MULTI_MISS_sum -d $OUT/kplacetlb -o pmc --output-format csv -- python3 tools/kplace.py
+                run kplacetlb 300 rocprofv3 --kernel-trace --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum GRBM_UTCL2_BUSY GRBM_GUI_ACTIVE -d $OUT/kplacetlb -o pmc --output-format csv -- python3 tools/kplace.py
+                run kplacetlb2 300 rocprofv3 --kernel-trace --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum GRBM_UTCL2_BUSY GRBM_GUI_ACTIVE -d $OUT/kplacetlb2 -o pmc --output-format csv -- python3 tools/kplace.py
                 unset KPLACE_ITERS KPLACE_WARM KPLACE_ROUNDS ;;
         kphase) run kphase 300 python tools/kphase.py ;;
         kcu)    run kcu 300 python tools/kcu.py ;;

@@ -541,7 +541,8 @@ def main():
                         frac=round(achieved / HBM_PEAK_GBPS, 4), traffic=_pmc_traffic(workload),
                         kernel=('combine_rows_kernel<FUSED>', 'combine_stream_kernel<FUSED, 2 vectors/lane>',
                                 'combine_stream_kernel<FUSED, 1 vector/lane>',
-                                'combine_stream_kernel<FUSED, persistent grid>')[kern.lib.deepep_last_kernel_choice()],
+                                'combine_stream_kernel<FUSED, persistent grid>',
+                                'combine_rows_kernel<FUSED, XCD-contiguous>')[kern.lib.deepep_last_kernel_choice()],
                         kernel_us=round(kern_us, 2),
                         kernel_us_flushed_median=None if kern_us_flushed is None else round(kern_us_flushed, 2),
                         kernel_us_read_flushed_median=(None if kern_us_read_flushed is None

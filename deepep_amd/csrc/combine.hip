@@ -98,7 +98,17 @@ struct Params {
     int32_t* error_flag;
     const uint64_t* out_rows;    // scatter (phase A over xGMI): byte address of unit u's output row, or NULL
     int64_t weights_offset;      // scatter: byte offset of the weights inside the output row
+    int xcd_blocks;              // item kernel: 1 = XCD-contiguous workgroup order (see xcd_block)
 };
+
+// Workgroups are dealt round-robin to the 8 XCDs (workgroup b runs on XCD b % 8).  With
+// xcd_blocks, workgroup b takes block xcd_block(b) instead, so each XCD works through one
+// contiguous eighth of the items (its L2 and its share of the memory traffic stay on neighbouring
+// tokens) -- a bijection on [0, n) for any n.
+__device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t n) {
+    const int64_t per = n / 8, rem = n % 8, xcd = b % 8, idx = b / 8;
+    return xcd * per + (xcd < rem ? xcd : rem) + idx;
+}
 
 // acc[8*v + e] += element e of the 16-byte vector (8 bf16)
 __device__ __forceinline__ void acc_add(float* acc, const u32x4& v) {
@@ -153,7 +163,8 @@ combine_rows_kernel(const Params p) {
     const int nvec = p.hidden >> 3;                          // 16-byte vectors per row
     const int nchunks = (nvec + kChunkVecs - 1) / kChunkVecs;
     const int64_t items = static_cast<int64_t>(p.num_units) * nchunks;
-    const int64_t it0 = static_cast<int64_t>(blockIdx.x) * kWaves;
+    const int64_t blk = p.xcd_blocks ? xcd_block(blockIdx.x, gridDim.x) : static_cast<int64_t>(blockIdx.x);
+    const int64_t it0 = blk * kWaves;
     const int64_t it = it0 + wave;
     const int width = p.table == nullptr ? 1 : p.table_width;
 
@@ -494,7 +505,7 @@ LaunchConfig g_config;
 // default the first large launch of each shape times both on the caller's stream (three launches
 // each, same arguments: the kernels are pure functions of their inputs) and keeps the faster; a
 // launch being captured into a graph, or a small one, takes the item kernel without tuning.
-int g_kernel_choice = -1;        // -1 autotune, else a candidate of launch_combine (0 item kernel, 1-3 streaming)
+int g_kernel_choice = -1;        // -1 autotune, else a candidate of launch_combine (0/4 item kernel, 1-3 streaming)
 int g_last_choice = 0;
 std::mutex g_tune_mutex;
 std::map<std::tuple<int, int, int, int, int, int, int>, int> g_tuned;
@@ -662,6 +673,7 @@ int deepep_combine_reduce(int mode, int weighted,
     p.error_flag = error_flag;
     p.out_rows = nullptr;
     p.weights_offset = 0;
+    p.xcd_blocks = 0;
 
     return launch_combine(mode, weighted, p, stream);
 }
@@ -714,6 +726,7 @@ int deepep_combine_reduce_scatter(int weighted,
     p.error_flag = error_flag;
     p.out_rows = out_rows;
     p.weights_offset = weights_offset;
+    p.xcd_blocks = 0;
     return launch_combine(DEEPEP_MODE_LOCAL, weighted, p, stream);
 }
 
@@ -721,7 +734,8 @@ int deepep_combine_reduce_scatter(int weighted,
 
 namespace {
 
-int launch_combine(int mode, int weighted, const Params& p, deepep_stream_t stream) {
+int launch_combine(int mode, int weighted, const Params& p_in, deepep_stream_t stream) {
+    Params p = p_in;
     // Launch shape: one wave per (unit, 64 x vpt x 16-byte column chunk) item; at hidden 7168 a
     // token is 7 items of 2 KiB per source row.
     const int nvec = p.hidden / 8;
@@ -767,8 +781,12 @@ int launch_combine(int mode, int weighted, const Params& p, deepep_stream_t stre
     // candidates: 0 item kernel, 1 streaming kernel (sh.vpt vectors per lane), 2 streaming kernel with
     // 1 vector per lane (half the registers, more waves per SIMD), 3 streaming kernel on a persistent
     // grid (sh.vpt vectors per lane)
+    // 4: the item kernel with XCD-contiguous workgroup order -- forced only, never autotuned: it lost
+    // on every measurement (config 2 188.4 vs 175.3 us, EP = 8 phase A 318 vs 301, phase B 126 vs
+    // 115): neighbouring items spread over all XCDs stream better
     auto launch_choice = [&](int c) {
-        if (c == 0) launch_items();
+        p.xcd_blocks = c == 4 ? 1 : 0;
+        if (c == 0 || c == 4) launch_items();
         else launch_streaming(c == 2 ? 1 : sh.vpt, c == 3);
     };
     constexpr int kCandidates = 4;
@@ -861,7 +879,7 @@ int deepep_build_local_plan(const int32_t* src_metadata, int num_recv_tokens, in
 }
 
 int deepep_set_kernel_choice(int choice) {
-    if (choice < -1 || choice > 3) return set_error(DEEPEP_ERR_INVALID_ARG, "kernel choice must be -1, 0, 1, 2 or 3");
+    if (choice < -1 || choice > 4) return set_error(DEEPEP_ERR_INVALID_ARG, "kernel choice must be -1 or 0..4");
     std::lock_guard<std::mutex> lock(g_tune_mutex);
     g_kernel_choice = choice;
     if (choice == -1) g_tuned.clear();

@@ -134,7 +134,9 @@ int deepep_set_launch_config(int vec_per_lane, int stage_lds, int store_policy, 
  *   2  the streaming kernel with 16 B per lane and row (half the registers, more waves per SIMD);
  *   3  the streaming kernel (as 1) on a persistent grid: as many workgroups as the chip holds at
  *      once, units strided over the waves;
- *  -1  (default) autotune: the first launch of each shape that writes >= 16 MiB times the four
+ *   4  the item kernel with XCD-contiguous workgroup order (each of the 8 XCDs takes one
+ *      contiguous eighth of the items; measured slower, so only when forced);
+ *  -1  (default) autotune: the first launch of each shape that writes >= 16 MiB times 0-3
  *      on the caller's stream (3 launches each, one host sync) and keeps the fastest; launches that
  *      are being captured into a graph, or smaller, use the item kernel.  Setting -1 forgets earlier
  *      choices.

@@ -385,7 +385,7 @@ def test_config2_full_size_bitwise(weighted, T, skew):
     lib = buf.kernels.lib
     try:
         # the item kernel, the streaming kernel (2 and 1 vectors per lane, persistent), and the autotuned choice
-        for choice in (0, 1, 2, 3, -1):
+        for choice in (0, 1, 2, 3, 4, -1):
             assert lib.deepep_set_kernel_choice(choice) == 0
             out, out_w, _ = buf.combine(y, handle, topk_weights=ex_w, apply_topk_weights=weighted)
             torch.cuda.synchronize()

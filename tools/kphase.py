@@ -55,11 +55,11 @@ def main():
     kern.lib.deepep_set_launch_config(0, -1, -1, 0)
     # the library's kernels on the automatic shape, forced (0 item, 1 streaming, 2 streaming 1 vector/lane)
     for rnd in range(2):
-        for choice in (0, 1, 2, 3):
+        for choice in (0, 1, 2, 3, 4):
             assert kern.lib.deepep_set_kernel_choice(choice) == 0
             us = timeit(lambda: kern.combine_reduce(MODE_LOCAL, y, packed[:, :H], n_recv, table=table_a, row_weights=w,
                                                     wtable=table_a, wsrc=w, out_weights=pw, stream=s), s)
-            print(json.dumps(dict(phase='A', kernel=('item', 'stream', 'stream_vpt1', 'stream_persistent')[choice], round=rnd, us=round(us, 1),
+            print(json.dumps(dict(phase='A', kernel=('item', 'stream', 'stream_vpt1', 'stream_persistent', 'item_xcd')[choice], round=rnd, us=round(us, 1),
                                   gbps=round(bytes_a / us / 1e3, 1))), flush=True)
     kern.lib.deepep_set_kernel_choice(-1)
     # same bytes, rows in a random order (no expert grouping): the scatter's cost
@@ -90,10 +90,10 @@ def main():
                                   gbps=round(bytes_b / us / 1e3, 1))), flush=True)
     kern.lib.deepep_set_launch_config(0, -1, -1, 0)
     for rnd in range(2):
-        for choice in (0, 1, 2, 3):
+        for choice in (0, 1, 2, 3, 4):
             assert kern.lib.deepep_set_kernel_choice(choice) == 0
             us = timeit(lambda: kern.combine_reduce(MODE_EPILOGUE, recv[:, :H], out, T, table=table_b, stream=s), s)
-            print(json.dumps(dict(phase='B', kernel=('item', 'stream', 'stream_vpt1', 'stream_persistent')[choice], round=rnd, us=round(us, 1),
+            print(json.dumps(dict(phase='B', kernel=('item', 'stream', 'stream_vpt1', 'stream_persistent', 'item_xcd')[choice], round=rnd, us=round(us, 1),
                                   gbps=round(bytes_b / us / 1e3, 1))), flush=True)
     kern.lib.deepep_set_kernel_choice(-1)
     # EP = 1 fused kernel, config 2 (8 rows per token, 65536 random expanded rows)

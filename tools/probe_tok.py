@@ -54,7 +54,8 @@ def main():
     # as in bench.py and plain, interleaved rounds
     for rnd in range(3):
         for weighted in (True, False):
-            for choice, name in ((0, 'item'), (1, 'stream'), (2, 'stream_vpt1'), (3, 'stream_persistent')):
+            for choice, name in ((0, 'item'), (1, 'stream'), (2, 'stream_vpt1'), (3, 'stream_persistent'),
+                                 (4, 'item_xcd')):
                 assert buf.kernels.lib.deepep_set_kernel_choice(choice) == 0
                 res[f'ab r{rnd} {"w" if weighted else "p"} {name}'] = round(timeit(lib_kernel(0, weighted), 50, 5), 1)
     buf.kernels.lib.deepep_set_kernel_choice(-1)

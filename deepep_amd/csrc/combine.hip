@@ -806,23 +806,29 @@ int launch_combine(int mode, int weighted, const Params& p_in, deepep_stream_t s
             } else {
                 hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
                 if (hipStreamIsCapturing(s, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone) {
-                    hipEvent_t e[kCandidates + 1] = {};
+                    // two passes, forward then reverse candidate order, so a clock drift during
+                    // tuning does not favour the candidates timed last
+                    constexpr int kSeg = 2 * kCandidates;
+                    hipEvent_t e[kSeg + 1] = {};
                     bool ok = true;
                     for (auto& ev : e) ok = ok && hipEventCreate(&ev) == hipSuccess;
                     if (ok) {
                         for (int c = 0; c < kCandidates; ++c) launch_choice(c);          // warm every candidate
                         ok = hipEventRecord(e[0], s) == hipSuccess;
-                        for (int c = 0; c < kCandidates; ++c) {
-                            for (int r = 0; r < 3; ++r) launch_choice(c);
-                            ok = ok && hipEventRecord(e[c + 1], s) == hipSuccess;
+                        for (int g = 0; g < kSeg; ++g) {
+                            const int c = g < kCandidates ? g : kSeg - 1 - g;
+                            for (int r = 0; r < 2; ++r) launch_choice(c);
+                            ok = ok && hipEventRecord(e[g + 1], s) == hipSuccess;
                         }
-                        ok = ok && hipEventSynchronize(e[kCandidates]) == hipSuccess;
-                        float best = 0.0f;
-                        for (int c = 0; ok && c < kCandidates; ++c) {
-                            float t = 0.0f;
-                            ok = hipEventElapsedTime(&t, e[c], e[c + 1]) == hipSuccess;
-                            if (ok && (c == 0 || t < best)) best = t, choice = c;
+                        ok = ok && hipEventSynchronize(e[kSeg]) == hipSuccess;
+                        float t[kCandidates] = {};
+                        for (int g = 0; ok && g < kSeg; ++g) {
+                            float dt = 0.0f;
+                            ok = hipEventElapsedTime(&dt, e[g], e[g + 1]) == hipSuccess;
+                            t[g < kCandidates ? g : kSeg - 1 - g] += dt;
                         }
+                        for (int c = 1; ok && c < kCandidates; ++c)
+                            if (t[c] < t[choice]) choice = c;
                         if (ok) g_tuned[key] = choice;
                         else choice = 0;
                     }

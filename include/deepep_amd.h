@@ -137,7 +137,8 @@ int deepep_set_launch_config(int vec_per_lane, int stage_lds, int store_policy, 
  *   4  the item kernel with XCD-contiguous workgroup order (each of the 8 XCDs takes one
  *      contiguous eighth of the items; measured slower, so only when forced);
  *  -1  (default) autotune: the first launch of each shape that writes >= 16 MiB times 0-3
- *      on the caller's stream (3 launches each, one host sync) and keeps the fastest; launches that
+ *      on the caller's stream (2 + 2 launches each, in forward then reverse order, one host sync)
+ *      and keeps the fastest; launches that
  *      are being captured into a graph, or smaller, use the item kernel.  Setting -1 forgets earlier
  *      choices.
  * All of them produce identical bits.  deepep_last_kernel_choice() says which one the last launch used.

@@ -5,15 +5,46 @@ There is no fallback: if the library is missing or a call fails, the error is ra
 (RuntimeError, as the reference's EP_HOST_ASSERT -> EPException does).
 """
 import ctypes
+import hashlib
 import os
 import threading
 from typing import Optional
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('DEEPEP_AMD_LIB', os.path.join(_HERE, 'libdeepep_amd.so'))
-ABI_VERSION = 9
+SOURCES = [os.path.join(_HERE, 'csrc', f) for f in ('combine.hip', 'dispatch.hip', 'symmetric.hip', 'plan.hip')]
+HEADER = os.path.join(os.path.dirname(_HERE), 'include', 'deepep_amd.h')
+HIPCC_FLAGS = ['--offload-arch=gfx950', '-O3', '-fPIC', '-std=c++17', '-Wall']
+
+
+def source_build_id() -> Optional[str]:
+    """sha256 (16 hex digits) of the library's sources, header and compile flags; None when the
+    sources are not next to the package."""
+    if not all(os.path.exists(p) for p in SOURCES + [HEADER]):
+        return None
+    h = hashlib.sha256(' '.join(HIPCC_FLAGS).encode())
+    for p in SOURCES + [HEADER]:
+        h.update(os.path.basename(p).encode())
+        with open(p, 'rb') as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def binary_build_id(path: str) -> Optional[str]:
+    """The build id compiled into a library file (read from its bytes, nothing is loaded)."""
+    if not os.path.exists(path):
+        return None
+    with open(path, 'rb') as f:
+        data = f.read()
+    i = data.find(b'DEEPEP_BUILD_ID=')
+    return data[i + 16:i + 32].decode(errors='replace') if i >= 0 else None
+ABI_VERSION = 10
 
 MODE_LOCAL, MODE_EPILOGUE, MODE_FUSED = 0, 1, 2
+
+# deepep_plan_* (include/deepep_amd.h)
+PLAN_BLOCK_TOKENS = 64
+PLAN_EXPANDED, PLAN_SINGLE, PLAN_INTERLEAVE, PLAN_RANK_LAYOUT, PLAN_WINDOW = 1, 2, 4, 8, 16
 
 _lib = None
 _lock = threading.Lock()
@@ -26,6 +57,7 @@ _I64 = ctypes.c_int64
 SIGNATURES = {
     'deepep_amd_abi_version': (_I, []),
     'deepep_amd_last_error': (ctypes.c_char_p, []),
+    'deepep_amd_build_id': (ctypes.c_char_p, []),
     'deepep_combine_reduce': (_I, [_I, _I,
                                    _P, _I64, _I64,
                                    _P, _I64, _I,
@@ -46,12 +78,15 @@ SIGNATURES = {
     'deepep_dispatch_route': (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P]),
     'deepep_dispatch_expert_counts': (_I, [_P, _I, _I, _I, _P, _P]),
     'deepep_dispatch_pack': (_I, [_P, _I64, _I, _P, _I64, _I, _P, _P, _I, _I, _I, _P, _P, _I,
-                                  _P, _P, _I64, _I, _I, _I, _I, _P]),
+                                  _P, _P, _I64, _I, _I, _I, _I, _P, _P]),
     'deepep_dispatch_count': (_I, [_P, _I64, _I, _I, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P]),
     'deepep_dispatch_scan': (_I, [_P, _I, _I, _I, _I, _P, _P, _P]),
     'deepep_dispatch_slots': (_I, [_P, _I64, _I, _I, _I, _I, _I, _P, _P, _P]),
     'deepep_dispatch_copy': (_I, [_P, _I64, _I, _I, _I, _I, _I, _I, _P, _I, _P, _I64, _P, _I64, _I,
-                                  _P, _P, _P, _P]),
+                                  _P, _P, _P, _I64, _P, _P]),
+    'deepep_route_block_counts': (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P]),
+    'deepep_plan_expert': (_I, [_P, _I, _I, _I, _I, _P, _P, _I, _I, _I, _P, _P, _P, _I64, _P, _P]),
+    'deepep_plan_source': (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I64, _I64, _P, _I, _P, _P]),
     'deepep_sym_alloc': (_I, [_I64, ctypes.POINTER(ctypes.c_void_p)]),
     'deepep_sym_free': (_I, [_P]),
     'deepep_sym_export': (_I, [_P, _P]),
@@ -80,6 +115,10 @@ def load(path: Optional[str] = None):
         p = path or LIB_PATH
         if not os.path.exists(p):
             raise LibraryMissing(f'deepep_amd: HIP library not found at {p}; run __graft_entry__.build()')
+        want = source_build_id() if path is None and 'DEEPEP_AMD_LIB' not in os.environ else None
+        if want is not None and binary_build_id(p) != want:
+            raise RuntimeError(f'deepep_amd: {p} was built from other sources (build id {binary_build_id(p)}, '
+                               f'sources {want}); run __graft_entry__.build()')
         lib = ctypes.CDLL(p)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(lib, name)

@@ -26,13 +26,16 @@ import torch.distributed as dist
 
 from .event import EventHandle, EventOverlap
 from .exchange import ExchangeMixin
-from .handle import CombinePlan, EPHandle, chunk_plans, single_chunk_plans, single_reduction_tables
+from .handle import BlockCounts, CombinePlan, EPHandle, build_ep_plan, chunk_geometry
 from .kernels import MODE_EPILOGUE, MODE_FUSED, MODE_LOCAL, RowLayout
 from .utils import align, ceil_div, value_or
 
 topk_idx_t = torch.int32 if int(os.environ.get('EP_NUM_TOPK_IDX_BITS', 64)) == 32 else torch.int64
 
 BUFFER_ALIGNMENT = 2 * 1024 * 1024          # symmetric::kNumAlignmentBytes (symmetric.hpp:16)
+# CU-budget streams (deepep_stream_create_cu_budget), keyed by (device, CUs); they live for the whole
+# process, so tensors whose allocator records them stay valid after their buffer is destroyed
+_BUDGET_STREAMS = {}
 _TOKEN_ALIGN = 32                           # ptx::kNumTMAAlignBytes (ptx.cuh:16)
 
 
@@ -61,16 +64,19 @@ def calculate_buffer_size(num_ranks: int, num_max_tokens_per_rank: int, hidden: 
     return align(max(dispatch_bytes, combine_bytes), BUFFER_ALIGNMENT)
 
 
-def notify_layout(notify: List[int], num_ranks: int, rank: int, experts_per_rank: int, all_gathered: bool):
+def notify_layout(notify: List[int], num_ranks: int, rank: int, experts_per_rank: int, all_gathered: bool,
+                  num_blocks: int = 0):
     """Host view of the dispatch notify (dispatch.cuh:79-258; buffer.hpp:1017-1064's CPU wait).
-    Each record is [tokens | tokens per local expert] (1 + experts_per_rank ints) from a source to a
-    destination.  `notify` holds the records this rank received, one per source (all_gathered
-    False), or every rank's records to every destination, [source][destination] (all_gathered True:
-    the xGMI push needs them).  Returns (tokens this rank sends per destination -- only when
-    all_gathered, else None -- tokens received per source, rows received per local expert, and,
-    when all_gathered, the row offset of this rank's rows inside every destination's receive window:
-    the rows the lower source ranks send there come first)."""
-    R, r, w = num_ranks, rank, 1 + experts_per_rank
+    Each record is [tokens | tokens per local expert | tokens per 64-token block | (token, lane) pairs
+    per block] (1 + experts_per_rank + 2 * num_blocks ints) from a source to a destination; the block
+    counts size the pipeline chunks of the EP > 1 combine (handle.BlockCounts).  `notify` holds the
+    records this rank received, one per source (all_gathered False), or every rank's records to every
+    destination, [source][destination] (all_gathered True: the xGMI push needs them).  Returns (tokens
+    this rank sends per destination -- only when all_gathered, else None -- tokens received per
+    source, rows received per local expert, when all_gathered the row offset of this rank's rows
+    inside every destination's receive window (the rows the lower source ranks send there come
+    first), and the block counts received from every source, [source][2 * num_blocks])."""
+    R, r, w = num_ranks, rank, 1 + experts_per_rank + 2 * num_blocks
     if all_gathered:
         grid = [[notify[(s * R + d) * w:(s * R + d + 1) * w] for d in range(R)] for s in range(R)]
         rows = [grid[s][r] for s in range(R)]
@@ -81,7 +87,8 @@ def notify_layout(notify: List[int], num_ranks: int, rank: int, experts_per_rank
         sends, offsets = None, None
     recv = [row[0] for row in rows]
     experts = [sum(row[1 + e] for row in rows) for e in range(experts_per_rank)]
-    return sends, recv, experts, offsets
+    blocks = [list(row[1 + experts_per_rank:]) for row in rows]
+    return sends, recv, experts, offsets, blocks
 
 
 class ElasticBuffer(ExchangeMixin):
@@ -144,9 +151,17 @@ class ElasticBuffer(ExchangeMixin):
         # xGMI combine: CUs for phase A while phase B of earlier chunks runs (0 = the whole chip)
         self.phase_a_cus = int(os.environ.get('DEEPEP_PHASE_A_CUS', 0))
         self._sym = None
+        self._sym_gen = None
+        self._old_sym_gens = set()
         self._capturing = False
         self._sym_exchange = None     # test hook: ranks sharing one process exchange window bases directly
         self._group_barrier()
+        # The xGMI transport's symmetric window is allocated here, as the reference allocates its
+        # symmetric buffer at construction (buffer.hpp:181-208): a first dispatch / combine then needs
+        # no collective set-up (a window too small for a later call is re-allocated there).
+        if self.transport == 'xgmi' and self.num_ranks > 1 and self.use_cuda and \
+                int(os.environ.get('DEEPEP_EAGER_WINDOW', 1)) and not hasattr(group, 'comm'):
+            self._window(1, slots=1, rows_per_slot=1)
 
     def _group_barrier(self) -> None:
         """torch.cuda.synchronize(); group barrier; synchronize (elastic.py:365-367)."""
@@ -176,8 +191,8 @@ class ElasticBuffer(ExchangeMixin):
                 self._group_barrier()             # no peer still stores into this rank's window
                 self._sym.destroy()
                 self._sym = None
-            for raw, _ in self.__dict__.pop('_budget_streams', {}).values():
-                self.kernels.lib.deepep_stream_destroy(raw)
+            # the CU-budget streams are process-wide and never destroyed: tensors returned by an async
+            # combine may still record events on them after this buffer is gone
             self.runtime = None
 
     @staticmethod
@@ -405,6 +420,7 @@ class ElasticBuffer(ExchangeMixin):
             # symmetric window (dispatch.cuh:373-392's push), no RCCL exchange for the rows
             use_xgmi = R > 1 and self.transport == 'xgmi' and self.use_cuda
             peer_offsets = None
+            counts = cached._counts if cached is not None else None
             if cached is not None:
                 _assert(do_expand == handle.do_expand, 'do_expand must match the cached handle')
                 dst_slot = cached.dst_buffer_slot_idx
@@ -419,26 +435,42 @@ class ElasticBuffer(ExchangeMixin):
                 kern.dispatch_route(idx64, num_experts, R, dst_slot, send_counts, stream=stream)
                 expert_hist = torch.empty((num_experts,), dtype=torch.int32, device=dev)
                 kern.dispatch_expert_counts(idx64, num_experts, expert_hist, stream=stream)
-                # notify (dispatch.cuh:79-258): every destination gets [tokens | tokens per local expert]
-                # from this rank; one exchange and ONE host sync size every receive-side allocation.
+                # per 64-token block and destination: tokens and (token, lane) pairs -- the sizes of
+                # every pipeline chunk of the EP > 1 combine (handle.BlockCounts), so the combine plan
+                # never needs a host sync of its own
+                nb = chunk_geometry(num_max_tokens_per_rank, 1)[0] if R > 1 else 0
+                blk = torch.empty((2, R, nb), dtype=torch.int32, device=dev)
+                if R > 1:
+                    kern.route_block_counts(idx64, num_experts, R, nb, blk[0], blk[1], stream=stream)
+                # notify (dispatch.cuh:79-258): every destination gets [tokens | tokens per local expert |
+                # block counts] from this rank; one exchange and ONE host sync size every receive-side
+                # allocation and every combine exchange.
                 # The xGMI transport pushes rows straight into the peers' windows, so every rank needs
                 # the whole [source, destination] count matrix (its rows' offset in a peer's window is
                 # what the lower source ranks send there): the notify is all-gathered instead.
-                notify = torch.cat([send_counts.view(R, 1), expert_hist.view(R, epr)], dim=1)
+                notify = torch.cat([send_counts.view(R, 1), expert_hist.view(R, epr), blk[0], blk[1]], dim=1)
                 if R == 1:
                     recv_notify = notify
                 elif use_xgmi:
-                    everyone = torch.empty((R * R, 1 + epr), dtype=notify.dtype, device=dev)
+                    everyone = torch.empty((R * R, notify.shape[1]), dtype=notify.dtype, device=dev)
                     self._a2a(everyone, notify.repeat(R, 1))
-                    recv_notify = everyone.view(R, R, 1 + epr)[:, r]
+                    recv_notify = everyone.view(R, R, notify.shape[1])[:, r]
                 else:
                     recv_notify = torch.empty_like(notify)
                     self._a2a(recv_notify, notify)
-                host = [int(v) for v in torch.cat([send_counts, (everyone if R > 1 and use_xgmi else
-                                                                 recv_notify).reshape(-1)]).tolist()]   # host sync
+                host = [int(v) for v in torch.cat([send_counts, blk.view(-1), (everyone if R > 1 and use_xgmi else
+                                                                               recv_notify).reshape(-1)]).tolist()]   # host sync
                 send_counts_l = host[:R]
-                _, recv_counts_l, expert_counts_l, offs = notify_layout(host[R:], R, r, epr,
-                                                                        all_gathered=R > 1 and use_xgmi)
+                own_blk = host[R:R + 2 * R * nb]
+                _, recv_counts_l, expert_counts_l, offs, recv_blk = notify_layout(
+                    host[R + 2 * R * nb:], R, r, epr, all_gathered=R > 1 and use_xgmi, num_blocks=nb)
+                counts = None
+                if R > 1:
+                    rb = recv_notify[:, 1 + epr:].reshape(R, 2, nb).transpose(0, 1)
+                    counts = BlockCounts(nb, [own_blk[d * nb:(d + 1) * nb] for d in range(R)],
+                                         [own_blk[(R + d) * nb:(R + d + 1) * nb] for d in range(R)],
+                                         [b[:nb] for b in recv_blk], [b[nb:] for b in recv_blk],
+                                         torch.cat([blk, rb]).contiguous())
                 if offs is not None:
                     peer_offsets = torch.tensor(offs, dtype=torch.int32).to(dev, non_blocking=True)
                 recv_counts_t = recv_notify[:, 0].contiguous()
@@ -455,7 +487,8 @@ class ElasticBuffer(ExchangeMixin):
                 sym = self._window(layout.row_bytes, slots=R, rows_per_slot=num_max_tokens_per_rank)
                 sym.barrier(stream)                               # peers finished reading their windows
                 kern.dispatch_pack(x_bytes, sf_bytes, idx64, w, r * num_max_tokens_per_rank, dst_slot,
-                                   peer_offsets, None, layout, dest_bases=sym.data_bases_dev, stream=stream)
+                                   peer_offsets, None, layout, dest_bases=sym.data_bases_dev,
+                                   error_flag=sym.error_flag, stream=stream)
                 sym.barrier(stream)                               # every row landed
                 if not self._capturing:
                     sym.publish(stream)
@@ -519,7 +552,7 @@ class ElasticBuffer(ExchangeMixin):
                                out_x.view(torch.uint8), out_sf.view(torch.uint8) if out_sf is not None else None,
                                out_w, x_direct=x_bytes if direct else None,
                                sf_direct=sf_bytes if direct else None, num_max_tokens=num_max_tokens_per_rank,
-                               stream=stream)
+                               error_flag=sym.error_flag if use_xgmi else None, stream=stream)
             recv_idx64 = out_idx
             if out_idx is not None and topk_idx.dtype != torch.int64:
                 out_idx = out_idx.to(topk_idx.dtype)
@@ -551,6 +584,7 @@ class ElasticBuffer(ExchangeMixin):
             handle._send_offsets = send_offsets
             handle._peer_offsets = peer_offsets
             handle._recv_topk_idx = recv_idx64
+            handle._counts = counts
         out_x = (out_x, out_sf) if out_sf is not None else out_x
         return out_x, out_idx, out_w, handle, EventOverlap(event)
 
@@ -575,52 +609,49 @@ class ElasticBuffer(ExchangeMixin):
             return max(1, int(env))
         return 4 if self.use_cuda and handle.num_max_tokens_per_rank >= 1024 else 1
 
-    def _plan(self, handle: EPHandle, single_reduction: bool, num_chunks: int = 1) -> CombinePlan:
-        key = ('single' if single_reduction else 'multi', self.num_ranks) + ((num_chunks,) if num_chunks > 1 else ())
+    def _plan(self, handle: EPHandle, single_reduction: bool, num_chunks: int, hidden: int,
+              window=None) -> CombinePlan:
+        """The handle's combine plan for this buffer's configuration, built on the first use by kernels
+        on the current stream (no host sync: handle.build_ep_plan) and cached on the handle.  A plan
+        built while a HIP graph is being captured belongs to that graph (its kernels run at replay),
+        so it is not cached for eager calls."""
+        R = self.num_ranks
+        if R == 1:
+            key = ('single' if single_reduction else 'multi', 1)
+        elif window is None:
+            key = ('single' if single_reduction else 'multi', R, num_chunks, hidden)
+        else:
+            for k in [k for k in handle._combine_plans if k[0] == 'xgmi' and k[-1] in self._old_sym_gens]:
+                del handle._combine_plans[k]          # plans that address an earlier (freed) window
+            key = ('xgmi', single_reduction, R, num_chunks, hidden, self._sym_gen)
         plan = handle._combine_plans.get(key)
+        stream = torch.cuda.current_stream() if self.use_cuda else None
         if plan is not None:
+            if self.use_cuda and not self._capturing and plan.ready is not None and plan.ready[0] != stream:
+                # built on another stream: order this use after it (once per call, cheap)
+                stream.wait_event(plan.ready[1])
             return plan
         T, K = handle.topk_idx.shape
-        R = self.num_ranks
-        plan = CombinePlan(num_ranks=R, num_tokens=T, num_topk=K, expanded=handle.do_expand)
-        meta = handle.recv_src_metadata
-        recv_counts = handle._recv_counts
-        if recv_counts is None:     # handle built elsewhere: counts from the inclusive prefix sum
-            psum = [0] + [int(v) for v in handle.psum_num_recv_tokens_per_scaleup_rank.tolist()]
-            recv_counts = [psum[i + 1] - psum[i] for i in range(R)]
-        n_recv = sum(recv_counts)
-        plan.recv_counts = recv_counts
         if R == 1:
+            meta = handle.recv_src_metadata
+            n_recv = handle.num_recv_tokens if handle._recv_counts is None else sum(handle._recv_counts)
+            plan = CombinePlan(num_ranks=1, num_tokens=T, num_topk=K, expanded=handle.do_expand)
             width = K if handle.do_expand else 1
             plan.local_table = torch.empty((T, width), dtype=torch.int32, device=meta.device)
             if not handle.do_expand:
                 plan.local_wtable = torch.empty((T, K), dtype=torch.int32, device=meta.device)
             self.kernels.build_local_plan(meta, n_recv, K, handle.num_max_tokens_per_rank, handle.do_expand,
-                                          plan.local_table, T, handle.topk_idx, plan.local_wtable,
-                                          stream=torch.cuda.current_stream() if self.use_cuda else None)
-        elif single_reduction and num_chunks > 1:
-            plan.chunks = single_chunk_plans(meta, recv_counts, handle.topk_idx, handle.num_experts, R,
-                                             handle.num_max_tokens_per_rank, num_chunks)
-        elif single_reduction:
-            plan.table_b1, plan.back_counts1 = single_reduction_tables(handle.topk_idx, handle.num_experts, R)
-            slots = meta[:n_recv, 2:]
-            valid = slots >= 0
-            plan.send_slots1 = slots[valid].view(-1, 1).to(torch.int32).contiguous()
-            per_tok = valid.sum(dim=1)
-            bounds = [0]
-            for c in recv_counts:
-                bounds.append(bounds[-1] + c)
-            csum = torch.cat([per_tok.new_zeros(1), torch.cumsum(per_tok, 0)])
-            cs = csum[torch.tensor(bounds, device=csum.device)].tolist()
-            plan.send_counts1 = [int(cs[i + 1] - cs[i]) for i in range(R)]
+                                          plan.local_table, T, handle.topk_idx, plan.local_wtable, stream=stream)
         else:
-            plan.chunks = chunk_plans(meta, recv_counts, handle.topk_idx, handle.num_experts, R,
-                                      handle.num_max_tokens_per_rank, num_chunks, handle.do_expand)
-            if num_chunks == 1:
-                ch = plan.chunks[0]
-                plan.table_b, plan.row_of_lane, plan.back_counts = ch.table_b, ch.row_of_lane, ch.back_counts
-                plan.wtables = ch.wtables
-        handle._combine_plans[key] = plan
+            _assert(handle._counts is not None, 'the EP > 1 combine needs a handle made by this build\'s dispatch')
+            plan = build_ep_plan(self.kernels, handle, num_ranks=R, rank=self.rank_idx, single=single_reduction,
+                                 num_chunks=num_chunks, hidden=hidden, window=window, stream=stream)
+        if not self._capturing:
+            if self.use_cuda:
+                ev = torch.cuda.Event()
+                ev.record(stream)
+                plan.ready = (stream, ev)
+            handle._combine_plans[key] = plan
         return plan
 
     def combine(self,
@@ -680,14 +711,14 @@ class ElasticBuffer(ExchangeMixin):
             return None
         if num_sms >= torch.cuda.get_device_properties(self.device).multi_processor_count:
             return None
-        streams = self.__dict__.setdefault('_budget_streams', {})
-        if num_sms not in streams:
+        key = (self.device.index, (num_sms + 7) // 8 * 8)     # budgets are whole CUs per XCD
+        if key not in _BUDGET_STREAMS:
             import ctypes
             from . import _lib
             raw = ctypes.c_void_p()
-            _lib.check(self.kernels.lib.deepep_stream_create_cu_budget(num_sms, ctypes.byref(raw)), 'cu_budget stream')
-            streams[num_sms] = (raw.value, torch.cuda.ExternalStream(raw.value, device=self.device))
-        return streams[num_sms][1]
+            _lib.check(self.kernels.lib.deepep_stream_create_cu_budget(key[1], ctypes.byref(raw)), 'cu_budget stream')
+            _BUDGET_STREAMS[key] = (raw.value, torch.cuda.ExternalStream(raw.value, device=self.device))
+        return _BUDGET_STREAMS[key][1]
 
     def _combine(self, x, topk_weights, bias_0, bias_1, handle, num_sms, previous_event,
                  previous_event_before_epilogue, async_with_compute_stream, allocate_on_comm_stream,
@@ -744,8 +775,16 @@ class ElasticBuffer(ExchangeMixin):
             stream = self.comm_stream
         with (self._null_ctx() if sync_mode else self._stream_ctx()):
             use_xgmi = R > 1 and self.transport == 'xgmi' and self.use_cuda
+            if use_xgmi and sync_mode and not self._capturing:
+                # the window is shared by every call: this call's first barrier must come after the
+                # earlier calls' work on the comm / phase-B / CU-budget streams that still reads it
+                # (a graph replays in stream order with what the capture depended on)
+                for other in [self.comm_stream, getattr(self, '_stream_b', None)] + \
+                        [v[1] for k, v in _BUDGET_STREAMS.items() if k[0] == self.device.index]:
+                    if other is not None and other != stream:
+                        stream.wait_stream(other)
             num_chunks = self._num_chunks(handle)
-            plan = None if use_xgmi else self._plan(handle, single_reduction, num_chunks)
+            plan = None if use_xgmi else self._plan(handle, single_reduction, num_chunks, hidden)
             combined_x = torch.empty((T, hidden), dtype=x.dtype, device=x.device)
             combined_w = torch.empty((T, K), dtype=torch.float32, device=x.device) if topk_weights is not None else None
             row_w = topk_weights if apply_topk_weights else None
@@ -764,31 +803,9 @@ class ElasticBuffer(ExchangeMixin):
             elif single_reduction and use_xgmi:
                 self._combine_xgmi_single(handle, x, row_w, wsrc, K, hidden, bias_0, bias_1, topk_weights,
                                           combined_x, combined_w, previous_event_before_epilogue, stream)
-            elif single_reduction and plan.chunks is not None:
+            elif single_reduction:
                 self._combine_single_chunks(plan, x, row_w, wsrc, hidden, bias_0, bias_1, combined_x, combined_w,
                                             previous_event_before_epilogue, stream)
-            elif single_reduction:
-                # every valid expanded row travels unreduced (kDoExpandedSend, combine.cuh:177-213);
-                # weighted: with its gating weight in a 16-byte row tail, applied by the one reduction
-                n_send = sum(plan.send_counts1)
-                w_elems = 8 if row_w is not None else 0
-                send = torch.empty((n_send, hidden + w_elems), dtype=x.dtype, device=x.device)
-                send_w = send[:, hidden:].view(torch.float32)[:, :1] if w_elems else None
-                self._mark(stream)
-                kern.combine_reduce(MODE_LOCAL, x, send[:, :hidden], n_send, table=plan.send_slots1,
-                                    wtable=plan.send_slots1 if w_elems else None, wsrc=wsrc if w_elems else None,
-                                    out_weights=send_w, stream=stream)
-                self._mark(stream)
-                recv = torch.empty((sum(plan.back_counts1), hidden + w_elems), dtype=x.dtype, device=x.device)
-                self._all_to_all(recv, send, plan.back_counts1, plan.send_counts1)
-                self._before_epilogue(previous_event_before_epilogue)
-                recv_w = recv[:, hidden:].view(torch.float32)[:, 0].contiguous() if w_elems else None
-                self._mark(stream)
-                kern.combine_reduce(MODE_EPILOGUE, recv[:, :hidden], combined_x, T, table=plan.table_b1,
-                                    row_weights=recv_w, bias0=bias_0, bias1=bias_1,
-                                    wtable=plan.table_b1 if w_elems else None, wsrc=recv_w, out_weights=combined_w,
-                                    stream=stream)
-                self._mark(stream)
             elif use_xgmi:
                 self._combine_xgmi(handle, x, expanded, row_w, wsrc, K, hidden, bias_0, bias_1, topk_weights,
                                    combined_x, combined_w, previous_event_before_epilogue, stream)

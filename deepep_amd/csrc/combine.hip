@@ -25,9 +25,6 @@
 #include <stdarg.h>
 
 #include <algorithm>
-#include <map>
-#include <mutex>
-#include <tuple>
 
 #include "../../include/deepep_amd.h"
 
@@ -206,6 +203,13 @@ combine_rows_kernel(const Params p) {
     }
     const int64_t u = it / nchunks;
     const int c = static_cast<int>(it - u * nchunks);
+    // A barrier of this window timed out (bit 2 of the error flag, set by deepep_sym_barrier /
+    // _wait): the rows in flight are not trustworthy, so no store reaches a peer and the output is
+    // poisoned with NaN instead of holding a silently wrong sum.
+    const bool aborted = p.error_flag != nullptr && (__hip_atomic_load(p.error_flag, __ATOMIC_RELAXED,
+                                                                       __HIP_MEMORY_SCOPE_AGENT) & 2);
+    if (aborted && p.out_rows != nullptr) return;
+    if (aborted) my_slot = -1;
     const uint64_t valid = __ballot(my_slot >= 0);
     const int n = __popcll(valid);
 
@@ -326,6 +330,10 @@ combine_rows_kernel(const Params p) {
         }
     }
 
+    if (aborted) {
+#pragma unroll
+        for (int v = 0; v < kVPT; ++v) result[v] = (u32x4){0x7fc07fc0u, 0x7fc07fc0u, 0x7fc07fc0u, 0x7fc07fc0u};
+    }
     const __amdgpu_buffer_rsrc_t orow = row_rsrc(out_row, p.hidden * 2);
 #pragma unroll
     for (int v = 0; v < kVPT; ++v)
@@ -351,6 +359,10 @@ combine_stream_kernel(const Params p) {
     const int width = p.table == nullptr ? 1 : p.table_width;
     // one unit per wave, or (a grid capped at the resident capacity) units strided over the waves
     const int64_t stride = static_cast<int64_t>(gridDim.x) * 4;
+    // a timed-out barrier (see combine_rows_kernel): no peer stores, NaN output
+    const bool aborted = p.error_flag != nullptr && (__hip_atomic_load(p.error_flag, __ATOMIC_RELAXED,
+                                                                       __HIP_MEMORY_SCOPE_AGENT) & 2);
+    if (aborted && p.out_rows != nullptr) return;
     for (int64_t u = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6); u < p.num_units; u += stride) {
     int32_t my_slot = -1;
     float my_w = 0.0f;
@@ -362,6 +374,7 @@ combine_stream_kernel(const Params p) {
         }
         if constexpr (kWeighted) my_w = my_slot >= 0 ? p.row_weights[my_slot] : 0.0f;
     }
+    if (aborted) my_slot = -1;
     const uint64_t valid = __ballot(my_slot >= 0);
     const int n = __popcll(valid);
 
@@ -446,6 +459,7 @@ combine_stream_kernel(const Params p) {
                 if (n > 0) acc_add(a, result[q]);
                 result[q] = acc_pack(a);
             }
+            if (aborted) result[q] = (u32x4){0x7fc07fc0u, 0x7fc07fc0u, 0x7fc07fc0u, 0x7fc07fc0u};
             __builtin_amdgcn_raw_buffer_store_b128(result[q], orow, vi * 16, 0, kStoreAux);
         }
     };
@@ -499,16 +513,13 @@ struct LaunchConfig {
 };
 LaunchConfig g_config;
 
-// Item kernel vs streaming kernel.  Both give identical bits, but which is faster depends on the
-// machine: on config 2 the streaming kernel ran 161 us against 171 us on one MI355X box and
-// 187-196 us against 175 us on another (tools/probe_tok.py, interleaved in one process).  So by
-// default the first large launch of each shape times both on the caller's stream (three launches
-// each, same arguments: the kernels are pure functions of their inputs) and keeps the faster; a
-// launch being captured into a graph, or a small one, takes the item kernel without tuning.
-int g_kernel_choice = -1;        // -1 autotune, else a candidate of launch_combine (0/4 item kernel, 1-3 streaming)
+// Item kernel vs streaming kernel.  Both give identical bits; which is faster depends on the box
+// (config 2: the streaming kernel ran 161 us against 171 us on one MI355X and 187-197 us against
+// 175 us on most others).  The item kernel is the default; nothing is timed
+// inside a call (a per-shape autotune used to, with a host sync in the call path).
+// deepep_set_kernel_choice forces another candidate.
+int g_kernel_choice = -1;        // -1 default (the item kernel), else a candidate of launch_combine
 int g_last_choice = 0;
-std::mutex g_tune_mutex;
-std::map<std::tuple<int, int, int, int, int, int, int>, int> g_tuned;
 
 template <int kMode, bool kWeighted, int kVPT, bool kFull, int kAux, bool kLDS, int kWaves, int kGroup>
 void launch_shape(const Params& p, int64_t items, hipStream_t stream) {
@@ -609,6 +620,14 @@ __attribute__((visibility("hidden"))) int deepep_amd_set_error(int code, const c
 }
 
 int deepep_amd_abi_version(void) { return DEEPEP_AMD_ABI_VERSION; }
+
+#ifndef DEEPEP_BUILD_ID
+#define DEEPEP_BUILD_ID "unknown-build-id"
+#endif
+// The build id (hash of sources, header and flags, deepep_amd/_lib.py) stored with a marker so that
+// it can be read from the file without loading it.
+__attribute__((used)) static const char g_build_id[] = "DEEPEP_BUILD_ID=" DEEPEP_BUILD_ID;
+const char* deepep_amd_build_id(void) { return g_build_id + 16; }
 
 const char* deepep_amd_last_error(void) { return g_last_error; }
 
@@ -748,9 +767,9 @@ int launch_combine(int mode, int weighted, const Params& p_in, deepep_stream_t s
     sh.waves = p.units_per_block == 4 ? 4 : (p.units_per_block == 8 ? 8 : (mode == DEEPEP_MODE_LOCAL ? 4 : 8));
     sh.group = g_config.rows_in_flight > 0 ? g_config.rows_in_flight : 8;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    // The streaming kernel (one wave per unit, chunks pipelined) whenever it applies and the shape
-    // is automatic: an explicit units_per_block / LDS / rows-in-flight setting selects the item
-    // kernel (which also serves tables wider than kStreamWidth and ragged hidden sizes).
+    // A forced streaming kernel (one wave per unit, chunks pipelined) applies only when the shape is
+    // automatic: an explicit units_per_block / LDS / rows-in-flight setting selects the item kernel
+    // (which also serves tables wider than kStreamWidth and ragged hidden sizes).
     const bool stream_ok = (p.table == nullptr || p.table_width <= kStreamWidth) && nvec % (64 * sh.vpt) == 0 &&
                            p.units_per_block == 0 && g_config.stage_lds < 0 && g_config.rows_in_flight == 0;
     auto launch_items = [&]() {
@@ -781,7 +800,7 @@ int launch_combine(int mode, int weighted, const Params& p_in, deepep_stream_t s
     // candidates: 0 item kernel, 1 streaming kernel (sh.vpt vectors per lane), 2 streaming kernel with
     // 1 vector per lane (half the registers, more waves per SIMD), 3 streaming kernel on a persistent
     // grid (sh.vpt vectors per lane)
-    // 4: the item kernel with XCD-contiguous workgroup order -- forced only, never autotuned: it lost
+    // 4: the item kernel with XCD-contiguous workgroup order -- it lost
     // on every measurement (config 2 188.4 vs 175.3 us, EP = 8 phase A 318 vs 301, phase B 126 vs
     // 115): neighbouring items spread over all XCDs stream better
     auto launch_choice = [&](int c) {
@@ -789,56 +808,7 @@ int launch_combine(int mode, int weighted, const Params& p_in, deepep_stream_t s
         if (c == 0 || c == 4) launch_items();
         else launch_streaming(c == 2 ? 1 : sh.vpt, c == 3);
     };
-    constexpr int kCandidates = 4;
-    int choice = 0;
-    if (stream_ok) {
-        if (g_kernel_choice >= 0) {
-            choice = g_kernel_choice;
-        } else if (static_cast<int64_t>(p.num_units) * nvec >= (int64_t(1) << 20)) {   // >= 16 MiB written
-            int units_log2 = 0;
-            while ((int64_t(1) << (units_log2 + 1)) <= p.num_units) ++units_log2;
-            const auto key = std::make_tuple(mode, weighted, sh.vpt, sh.policy, p.table == nullptr ? 1 : p.table_width,
-                                             p.hidden, units_log2);
-            std::lock_guard<std::mutex> lock(g_tune_mutex);
-            const auto it = g_tuned.find(key);
-            if (it != g_tuned.end()) {
-                choice = it->second;
-            } else {
-                hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-                if (hipStreamIsCapturing(s, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone) {
-                    // two passes, forward then reverse candidate order, so a clock drift during
-                    // tuning does not favour the candidates timed last
-                    constexpr int kSeg = 2 * kCandidates;
-                    hipEvent_t e[kSeg + 1] = {};
-                    bool ok = true;
-                    for (auto& ev : e) ok = ok && hipEventCreate(&ev) == hipSuccess;
-                    if (ok) {
-                        for (int c = 0; c < kCandidates; ++c) launch_choice(c);          // warm every candidate
-                        ok = hipEventRecord(e[0], s) == hipSuccess;
-                        for (int g = 0; g < kSeg; ++g) {
-                            const int c = g < kCandidates ? g : kSeg - 1 - g;
-                            for (int r = 0; r < 2; ++r) launch_choice(c);
-                            ok = ok && hipEventRecord(e[g + 1], s) == hipSuccess;
-                        }
-                        ok = ok && hipEventSynchronize(e[kSeg]) == hipSuccess;
-                        float t[kCandidates] = {};
-                        for (int g = 0; ok && g < kSeg; ++g) {
-                            float dt = 0.0f;
-                            ok = hipEventElapsedTime(&dt, e[g], e[g + 1]) == hipSuccess;
-                            t[g < kCandidates ? g : kSeg - 1 - g] += dt;
-                        }
-                        for (int c = 1; ok && c < kCandidates; ++c)
-                            if (t[c] < t[choice]) choice = c;
-                        if (ok) g_tuned[key] = choice;
-                        else choice = 0;
-                    }
-                    for (auto& ev : e)
-                        if (ev != nullptr) (void)hipEventDestroy(ev);
-                    (void)hipGetLastError();
-                }
-            }
-        }
-    }
+    const int choice = (stream_ok && g_kernel_choice >= 0) ? g_kernel_choice : 0;
     g_last_choice = choice;
     launch_choice(choice);
     const hipError_t err = hipGetLastError();
@@ -886,9 +856,7 @@ int deepep_build_local_plan(const int32_t* src_metadata, int num_recv_tokens, in
 
 int deepep_set_kernel_choice(int choice) {
     if (choice < -1 || choice > 4) return set_error(DEEPEP_ERR_INVALID_ARG, "kernel choice must be -1 or 0..4");
-    std::lock_guard<std::mutex> lock(g_tune_mutex);
     g_kernel_choice = choice;
-    if (choice == -1) g_tuned.clear();
     return DEEPEP_OK;
 }
 

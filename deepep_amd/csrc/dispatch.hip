@@ -149,8 +149,13 @@ pack_kernel(const uint8_t* __restrict__ x, int64_t x_stride, int x_bytes,
             const int64_t* __restrict__ topk_idx, const float* __restrict__ topk_weights, int K,
             int32_t src_base, const int32_t* __restrict__ dst_slot, const int32_t* __restrict__ send_offsets, int R,
             uint8_t* __restrict__ packed, const uint64_t* __restrict__ dest_bases, int64_t row_bytes,
-            int sf_off, int idx_off, int w_off, int src_off) {
+            int sf_off, int idx_off, int w_off, int src_off, const int32_t* __restrict__ error_flag) {
     const int t = blockIdx.x, lane = threadIdx.x;
+    // the window barrier before this push timed out (bit 2): the peers may still read their
+    // windows, so nothing is stored into them (the call's results are invalid and the next call raises)
+    if (kPeer && error_flag != nullptr &&
+        (__hip_atomic_load(error_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 2))
+        return;
     // lane r holds the byte address of the destination row for rank r (0: not routed to r)
     uint64_t my_row = 0;
     if (lane < R) {
@@ -323,9 +328,13 @@ copy_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int x_bytes, 
             int N, int K, const int32_t* __restrict__ meta, int expanded,
             const uint8_t* __restrict__ x_direct, int64_t x_direct_stride,
             const uint8_t* __restrict__ sf_direct, int64_t sf_direct_stride, int num_max_tokens,
-            uint8_t* __restrict__ recv_x, uint8_t* __restrict__ recv_sf, float* __restrict__ recv_w) {
+            uint8_t* __restrict__ recv_x, uint8_t* __restrict__ recv_sf, float* __restrict__ recv_w,
+            int64_t num_out_rows, int32_t* __restrict__ error_flag) {
     constexpr int kChunkVecs = 128;                        // 64 lanes x 2 x 16 B
     const int lane = threadIdx.x & 63;
+    // a timed-out window barrier (bit 2): the received rows are not trustworthy, store nothing
+    if (error_flag != nullptr && (__hip_atomic_load(error_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 2))
+        return;
     const int nvec = x_bytes / 16;
     const int nchunks = max(1, (nvec + kChunkVecs - 1) / kChunkVecs);
     const int64_t it = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
@@ -346,6 +355,10 @@ copy_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int x_bytes, 
         if (lane < K) my_dst = meta[i * (K + 2) + 2 + lane];
     } else if (lane == 0) {
         my_dst = static_cast<int32_t>(i);
+    }
+    if (my_dst >= num_out_rows) {                          // never store past the outputs
+        if (error_flag != nullptr) atomicOr(error_flag, 1);
+        my_dst = -1;
     }
     const uint64_t dmask = __ballot(my_dst >= 0);
     const int v0 = c * kChunkVecs + lane, v1 = v0 + 64;
@@ -435,7 +448,8 @@ int deepep_dispatch_pack(const void* x, int64_t x_row_stride_bytes, int x_bytes,
                          const int64_t* topk_idx, const float* topk_weights, int num_tokens, int num_topk,
                          int32_t src_base, const int32_t* dst_slot, const int32_t* send_offsets, int num_ranks,
                          void* packed, const uint64_t* dest_bases, int64_t row_bytes,
-                         int sf_off, int idx_off, int w_off, int src_off, deepep_stream_t stream) {
+                         int sf_off, int idx_off, int w_off, int src_off, const int32_t* error_flag,
+                         deepep_stream_t stream) {
     if (num_tokens == 0) return DEEPEP_OK;
     if (num_tokens < 0 || num_topk < 1 || num_topk > 32 || num_ranks < 1 || num_ranks > 64 || x_bytes % 16 ||
         sf_bytes % 4 || row_bytes % 16 || !a16(x) || (dest_bases == nullptr && !a16(packed)) ||
@@ -448,13 +462,13 @@ int deepep_dispatch_pack(const void* x, int64_t x_row_stride_bytes, int x_bytes,
                            static_cast<const uint8_t*>(x), x_row_stride_bytes, x_bytes,
                            static_cast<const uint8_t*>(sf), sf_row_stride_bytes, sf_bytes,
                            topk_idx, topk_weights, num_topk, src_base, dst_slot, send_offsets, num_ranks,
-                           static_cast<uint8_t*>(packed), dest_bases, row_bytes, sf_off, idx_off, w_off, src_off);
+                           static_cast<uint8_t*>(packed), dest_bases, row_bytes, sf_off, idx_off, w_off, src_off, error_flag);
     else
         hipLaunchKernelGGL(pack_kernel<false>, dim3(num_tokens), dim3(64), 0, s,
                            static_cast<const uint8_t*>(x), x_row_stride_bytes, x_bytes,
                            static_cast<const uint8_t*>(sf), sf_row_stride_bytes, sf_bytes,
                            topk_idx, topk_weights, num_topk, src_base, dst_slot, send_offsets, num_ranks,
-                           static_cast<uint8_t*>(packed), dest_bases, row_bytes, sf_off, idx_off, w_off, src_off);
+                           static_cast<uint8_t*>(packed), dest_bases, row_bytes, sf_off, idx_off, w_off, src_off, error_flag);
     return launch_status("dispatch_pack");
 }
 
@@ -503,9 +517,11 @@ int deepep_dispatch_copy(const void* packed, int64_t row_bytes, int x_bytes, int
                          int num_recv, int num_topk, const int32_t* src_metadata, int expanded,
                          const void* x_direct, int64_t x_direct_stride_bytes,
                          const void* sf_direct, int64_t sf_direct_stride_bytes, int num_max_tokens,
-                         void* recv_x, void* recv_sf, float* recv_topk_weights, deepep_stream_t stream) {
+                         void* recv_x, void* recv_sf, float* recv_topk_weights, int64_t num_out_rows,
+                         int32_t* error_flag, deepep_stream_t stream) {
     if (num_recv == 0) return DEEPEP_OK;
     if (num_recv < 0 || num_topk < 1 || num_topk > 32 || x_bytes % 16 || row_bytes % 16 || !a16(packed) ||
+        num_out_rows < 0 ||
         !a16(recv_x) || (recv_sf != nullptr && sf_bytes % 4) || src_metadata == nullptr ||
         (x_direct != nullptr && (!a16(x_direct) || x_direct_stride_bytes % 16 || num_max_tokens < 1 ||
                                  (recv_sf != nullptr && sf_direct == nullptr))))
@@ -518,7 +534,8 @@ int deepep_dispatch_copy(const void* packed, int64_t row_bytes, int x_bytes, int
                        num_recv, num_topk, src_metadata, expanded,
                        static_cast<const uint8_t*>(x_direct), x_direct_stride_bytes,
                        static_cast<const uint8_t*>(sf_direct), sf_direct_stride_bytes, num_max_tokens,
-                       static_cast<uint8_t*>(recv_x), static_cast<uint8_t*>(recv_sf), recv_topk_weights);
+                       static_cast<uint8_t*>(recv_x), static_cast<uint8_t*>(recv_sf), recv_topk_weights,
+                       num_out_rows, error_flag);
     return launch_status("dispatch_copy");
 }
 

@@ -180,10 +180,12 @@ int deepep_stream_create_cu_budget(int num_cus, deepep_stream_t* stream) {
     hipError_t e = hipGetDevice(&dev);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
     if (e != hipSuccess) return hip_fail(e, "CU count");
-    if (num_cus > n) num_cus = n;
     // Mask bit b is CU b / 8 of XCD b % 8 (probed on MI355X, tools/probe_cumask.py), and an XCD whose
-    // bits are all clear is not restricted at all; so the budget is the FIRST num_cus bits: num_cus / 8
-    // CUs on every XCD.
+    // bits are all clear is not restricted at all; so the budget is the FIRST num_cus bits, rounded up
+    // to a whole number of CUs per XCD (a multiple of 8, at least 8): fewer bits would leave whole XCDs
+    // unrestricted, and a remainder would spread the budget unevenly.
+    num_cus = (num_cus + 7) / 8 * 8;
+    if (num_cus > n) num_cus = n;
     uint32_t mask[64] = {};
     const int words = (n + 31) / 32;
     if (words > 64) return deepep_amd_set_error(DEEPEP_ERR_UNSUPPORTED, "cu_budget: more than 2048 CUs");

@@ -16,25 +16,10 @@ from typing import List, Optional
 import torch
 import torch.distributed as dist
 
-from .handle import ChunkPlan, CombinePlan, EPHandle, weight_table, window_tables
 from .kernels import MODE_EPILOGUE, MODE_LOCAL
 from .utils import align
 
 _WINDOW_IDS = itertools.count(1)            # symmetric windows created by this process
-
-
-def _interleave_by_rank(units: torch.Tensor, dest_rank: torch.Tensor, num_ranks: int) -> torch.Tensor:
-    """Reorder a phase-A launch's units (ascending, hence grouped by destination rank) round-robin
-    over the destinations: the waves in flight at any moment then store to every peer at once, so
-    all of xGMI's point-to-point links carry traffic instead of one link at a time.  Units are
-    independent, so the order changes no result."""
-    if units.numel() == 0 or num_ranks == 1:
-        return units
-    d = dest_rank[units]
-    counts = torch.bincount(d, minlength=num_ranks)
-    start = torch.cumsum(counts, 0) - counts
-    pos = torch.arange(units.numel(), device=units.device) - start[d]        # units are sorted by d
-    return units[torch.argsort(pos * num_ranks + d)]
 
 
 class ExchangeMixin:
@@ -55,15 +40,11 @@ class ExchangeMixin:
         than one chunk, phase A of chunk c+1 runs while RCCL moves chunk c and phase B of chunk
         c runs on a second stream while RCCL moves chunk c+1."""
         kern = self.kernels
-        w_elems = 0 if topk_weights is None else align(K * 4, 16) // 2
+        w_elems = 0 if topk_weights is None else align(K * 4, 16) // 2     # the plan's packed-row layout
         row_elems = hidden + w_elems
         pipelined = len(plan.chunks) > 1 and self.use_cuda
-        wkey = (row_elems // 2, hidden // 2)
         if w_elems:
-            # every table phase B reads is built before the phase-B stream forks off this one
-            for ch in plan.chunks:
-                if wkey not in ch.wtables:
-                    ch.wtables[wkey] = weight_table(ch.row_of_lane, *wkey)
+            assert all(ch.wtable_b is not None for ch in plan.chunks), 'receive rows too large for int32 weight indices'
         if pipelined:
             if getattr(self, '_stream_b', None) is None:
                 self._stream_b = torch.cuda.Stream(device=self.device)
@@ -104,7 +85,7 @@ class ExchangeMixin:
                 sb = stream_b if pipelined else stream
                 if work is not None:
                     work.wait()
-                wtable_b = ch.wtables[wkey] if w_elems else None
+                wtable_b = ch.wtable_b if w_elems else None
                 recv_wsrc = recv.view(torch.float32).view(-1) if w_elems else None
                 lo, hi = ch.lo, ch.hi
                 self._mark(sb)
@@ -198,20 +179,10 @@ class ExchangeMixin:
             old.destroy()
         # plans cache peer row addresses: they are valid for this window only (a process-unique id,
         # since one handle may serve several buffers)
-        if getattr(self, '_sym_gen', None) is not None:
+        if self._sym_gen is not None:
             self._old_sym_gens.add(self._sym_gen)
-        else:
-            self._old_sym_gens = set()
         self._sym_gen = next(_WINDOW_IDS)
         return self._sym
-
-    def _window_plan(self, handle: EPHandle, key: tuple):
-        """The handle's cached xGMI plan for `key` under the current window, dropping plans that
-        address an earlier (freed) window."""
-        stale = [k for k in handle._combine_plans if k[0] in ('xgmi', 'xgmi-single') and k[-1] in self._old_sym_gens]
-        for k in stale:
-            del handle._combine_plans[k]
-        return handle._combine_plans.get(key + (self._sym_gen,))
 
     def _combine_xgmi(self, handle, x, expanded, row_w, wsrc, K, hidden, bias_0, bias_1, topk_weights,
                       combined_x, combined_w, previous_event_before_epilogue, stream) -> None:
@@ -230,54 +201,14 @@ class ExchangeMixin:
         row_bytes = align(hidden * 2, 16) + align(K * 4, 16)
         sym = self._window(row_bytes, rows_per_slot=T_max)
         num_chunks = min(self._num_chunks(handle), 63)
-        key = ('xgmi', R, row_bytes, num_chunks)
-        plan = self._window_plan(handle, key)
-        if plan is None:
-            plan = CombinePlan(num_ranks=R, num_tokens=T, num_topk=K, expanded=expanded)
-            meta = handle.recv_src_metadata
-            recv_counts = handle._recv_counts
-            if recv_counts is None:
-                psum = [0] + [int(v) for v in handle.psum_num_recv_tokens_per_scaleup_rank.tolist()]
-                recv_counts = [psum[i + 1] - psum[i] for i in range(R)]
-            n_recv = sum(recv_counts)
-            plan.recv_counts = recv_counts
-            m = meta[:n_recv].to(torch.int64)
-            src_rank = torch.div(m[:, 1], K, rounding_mode='floor')
-            src_tok = m[:, 0] % T_max
-            slot = torch.full_like(src_rank, r) if rank_layout else m[:, 1] % K
-            out_rows = sym.data_bases_dev[src_rank] + (slot * T_max + src_tok) * row_bytes
-            table_b, row_of_lane = window_tables(handle.topk_idx, handle.num_experts, R, T_max, rank_layout)
-            B = (T_max + num_chunks - 1) // num_chunks
-            chunk_of_row = torch.div(src_tok, B, rounding_mode='floor')
-            plan.chunks = []
-            for c in range(num_chunks):
-                rows = _interleave_by_rank((chunk_of_row == c).nonzero().view(-1), src_rank, R)
-                if expanded:
-                    table_a = m[rows, 2:].to(torch.int32).contiguous()
-                    wtable_a = table_a
-                else:                                         # units are interleaved: explicit rows
-                    table_a = rows.to(torch.int32).view(-1, 1).contiguous()
-                    wtable_a = (rows.view(-1, 1) * K + torch.arange(K, device=rows.device).view(1, K)).to(
-                        torch.int32).contiguous()
-                lo, hi = c * B, min((c + 1) * B, T)
-                plan.chunks.append(ChunkPlan(lo, max(lo, hi), table_a, wtable_a, [], [],
-                                             table_b[lo:hi], row_of_lane[lo:hi]))
-                plan.chunks[-1].out_rows = out_rows[rows].contiguous()
-            plan.window_row_bytes = row_bytes
-            handle._combine_plans[key + (self._sym_gen,)] = plan
+        plan = self._plan(handle, False, num_chunks, hidden, window=sym)
         kern = self.kernels
         w_off = align(hidden * 2, 16)
         n_rows = self._window_slots * T_max
         rows = sym.data[:n_rows * row_bytes].view(torch.bfloat16).view(n_rows, row_bytes // 2)
         recv_wsrc = sym.data[:n_rows * row_bytes].view(torch.float32) if topk_weights is not None else None
         pipelined = len(plan.chunks) > 1
-        wkey = (row_bytes // 4, w_off // 4)
-        if topk_weights is not None:
-            # built here, on the caller's stream, BEFORE the phase-B stream forks off it: a table built
-            # inside the phase-B loop would be written on one stream and read on the other
-            for ch in plan.chunks:
-                if wkey not in ch.wtables:
-                    ch.wtables[wkey] = weight_table(ch.row_of_lane, *wkey)
+        err = sym.error_flag                              # a timed-out barrier poisons the launches below
         sym.barrier(stream)                               # peers finished reading their windows
         if pipelined:
             if getattr(self, '_stream_b', None) is None:
@@ -296,7 +227,7 @@ class ExchangeMixin:
             kern.combine_reduce_scatter(x, ch.out_rows.shape[0], ch.out_rows, table=ch.table_a, row_weights=row_w,
                                         wtable=ch.wtable_a, wsrc=wsrc,
                                         num_weights=K if topk_weights is not None else 0,
-                                        weights_offset=w_off, stream=sa)
+                                        weights_offset=w_off, error_flag=err, stream=sa)
             self._mark(sa)
             sym.signal(1 + c, sa)
         if sa is not stream:
@@ -307,14 +238,15 @@ class ExchangeMixin:
             previous_event_before_epilogue.stream_wait(stream_b)
         for c, ch in enumerate(plan.chunks):
             sym.wait(1 + c, sb)
-            wtable_b = ch.wtables[wkey] if topk_weights is not None else None
+            wtable_b = ch.wtable_b if topk_weights is not None else None
             lo, hi = ch.lo, ch.hi
             self._mark(sb)
             kern.combine_reduce(MODE_EPILOGUE, rows[:, :hidden], combined_x[lo:hi], hi - lo, table=ch.table_b,
                                 bias0=bias_0[lo:hi] if bias_0 is not None else None,
                                 bias1=bias_1[lo:hi] if bias_1 is not None else None,
                                 wtable=wtable_b, wsrc=recv_wsrc,
-                                out_weights=combined_w[lo:hi] if combined_w is not None else None, stream=sb)
+                                out_weights=combined_w[lo:hi] if combined_w is not None else None,
+                                error_flag=err, stream=sb)
             self._mark(sb)
         if pipelined:
             stream.wait_stream(stream_b)
@@ -338,38 +270,7 @@ class ExchangeMixin:
         row_bytes = w_off + 16                # the weight tail is always reserved: one window size per buffer
         sym = self._window(row_bytes, rows_per_slot=T_max)
         num_chunks = min(self._num_chunks(handle), 63)
-        key = ('xgmi-single', R, row_bytes, num_chunks)
-        plan = self._window_plan(handle, key)
-        if plan is None:
-            plan = CombinePlan(num_ranks=R, num_tokens=T, num_topk=K, expanded=True)
-            meta = handle.recv_src_metadata
-            recv_counts = handle._recv_counts
-            if recv_counts is None:
-                psum = [0] + [int(v) for v in handle.psum_num_recv_tokens_per_scaleup_rank.tolist()]
-                recv_counts = [psum[i + 1] - psum[i] for i in range(R)]
-            m = meta[:sum(recv_counts)].to(torch.int64)
-            slots = m[:, 2:]
-            i_idx, k_idx = (slots >= 0).nonzero(as_tuple=True)           # every valid (received token, lane)
-            rows_exp = slots[i_idx, k_idx]
-            src_rank = torch.div(m[i_idx, 1], K, rounding_mode='floor')
-            src_tok = m[i_idx, 0] % T_max
-            out_rows = sym.data_bases_dev[src_rank] + (k_idx * T_max + src_tok) * row_bytes
-            k_all = torch.arange(K, device=handle.topk_idx.device).view(1, K)
-            t_all = torch.arange(T, device=handle.topk_idx.device).view(T, 1)
-            table_b = torch.where(handle.topk_idx >= 0, k_all * T_max + t_all, torch.full_like(handle.topk_idx, -1))
-            table_b = table_b.to(torch.int32).contiguous()
-            B = (T_max + num_chunks - 1) // num_chunks
-            chunk_of = torch.div(src_tok, B, rounding_mode='floor')
-            plan.chunks = []
-            for c in range(num_chunks):
-                sel = _interleave_by_rank((chunk_of == c).nonzero().view(-1), src_rank, R)
-                lo, hi = c * B, min((c + 1) * B, T)
-                ch = ChunkPlan(lo, max(lo, hi), rows_exp[sel].to(torch.int32).view(-1, 1).contiguous(), None, [], [],
-                               table_b[lo:hi], table_b[lo:hi])
-                ch.out_rows = out_rows[sel].contiguous()
-                plan.chunks.append(ch)
-            plan.window_row_bytes = row_bytes
-            handle._combine_plans[key + (self._sym_gen,)] = plan
+        plan = self._plan(handle, True, num_chunks, hidden, window=sym)
         kern = self.kernels
         n_rows = K * T_max
         win = sym.data[:n_rows * row_bytes]
@@ -377,6 +278,7 @@ class ExchangeMixin:
         win_w = win.view(torch.float32).view(K, T_max, row_bytes // 4)[:, :, w_off // 4] if with_w else None
         recv_w = torch.empty((K, T_max), dtype=torch.float32, device=x.device) if with_w else None
         pipelined = len(plan.chunks) > 1
+        err = sym.error_flag                              # a timed-out barrier poisons the launches below
         sym.barrier(stream)                               # peers finished reading their windows
         if pipelined:
             if getattr(self, '_stream_b', None) is None:
@@ -387,7 +289,8 @@ class ExchangeMixin:
             self._mark(stream)
             kern.combine_reduce_scatter(x, ch.out_rows.shape[0], ch.out_rows, table=ch.table_a,
                                         wtable=ch.table_a if with_w else None, wsrc=wsrc if with_w else None,
-                                        num_weights=1 if with_w else 0, weights_offset=w_off, stream=stream)
+                                        num_weights=1 if with_w else 0, weights_offset=w_off, error_flag=err,
+                                        stream=stream)
             self._mark(stream)
             sym.signal(1 + c, stream)
         self._before_epilogue(previous_event_before_epilogue)
@@ -408,7 +311,8 @@ class ExchangeMixin:
                                 bias0=bias_0[lo:hi] if bias_0 is not None else None,
                                 bias1=bias_1[lo:hi] if bias_1 is not None else None,
                                 wtable=ch.table_b if with_w else None, wsrc=rw,
-                                out_weights=combined_w[lo:hi] if combined_w is not None else None, stream=sb)
+                                out_weights=combined_w[lo:hi] if combined_w is not None else None,
+                                error_flag=err, stream=sb)
             self._mark(sb)
         if pipelined:
             stream.wait_stream(stream_b)

@@ -169,8 +169,46 @@ class HipKernels:
                                                     _stream_handle(stream))
         _lib.check(rc, 'dispatch_expert_counts')
 
+    # ------------------------------------------------------------------ EP > 1 combine plan (plan.hip)
+    def route_block_counts(self, topk_idx, num_experts, num_ranks, num_blocks, tok, pairs, stream=None):
+        """tok / pairs: int32 [num_ranks, num_blocks] (64-token blocks of this rank's tokens)."""
+        _require(topk_idx.is_cuda and topk_idx.dtype == torch.int64 and topk_idx.is_contiguous(), 'topk_idx int64')
+        for t in (tok, pairs):
+            _require(t.dtype == torch.int32 and t.is_contiguous() and t.numel() == num_ranks * num_blocks,
+                     'block counts must be contiguous int32 [num_ranks, num_blocks]')
+        T, K = topk_idx.shape
+        rc = self.lib.deepep_route_block_counts(ptr(topk_idx), T, K, num_experts, num_ranks, num_blocks, ptr(tok),
+                                                ptr(pairs), _stream_handle(stream))
+        _lib.check(rc, 'route_block_counts')
+
+    def plan_expert(self, meta, num_topk, num_ranks, rank, num_max_tokens, recv_tok, recv_pairs, num_blocks,
+                    blocks_per_chunk, flags, table_a, wtable_a, window_bases, window_row_bytes, out_rows,
+                    stream=None):
+        _require(meta.is_cuda and meta.dtype == torch.int32 and meta.is_contiguous(), 'recv_src_metadata int32')
+        _require(table_a.dtype == torch.int32 and table_a.is_contiguous(), 'table_a int32')
+        _require(wtable_a is None or (wtable_a.dtype == torch.int32 and wtable_a.is_contiguous()), 'wtable_a int32')
+        _require(out_rows is None or (out_rows.dtype == torch.int64 and out_rows.is_contiguous() and
+                                      window_bases is not None), 'out_rows int64 with window bases')
+        rc = self.lib.deepep_plan_expert(ptr(meta), num_topk, num_ranks, rank, num_max_tokens, ptr(recv_tok),
+                                         ptr(recv_pairs), num_blocks, blocks_per_chunk, flags, ptr(table_a),
+                                         ptr(wtable_a), ptr(window_bases), window_row_bytes, ptr(out_rows),
+                                         _stream_handle(stream))
+        _lib.check(rc, 'plan_expert')
+
+    def plan_source(self, topk_idx, num_experts, num_ranks, num_max_tokens, dst_slot, send_tok, send_pairs,
+                    num_blocks, blocks_per_chunk, flags, row_floats, weights_offset, table_b, wtable, stream=None):
+        _require(topk_idx.is_cuda and topk_idx.dtype == torch.int64 and topk_idx.is_contiguous(), 'topk_idx int64')
+        _require(table_b.dtype == torch.int32 and table_b.is_contiguous(), 'table_b int32')
+        _require(wtable is None or (wtable.dtype == torch.int32 and wtable.is_contiguous()), 'wtable int32')
+        T, K = topk_idx.shape
+        rc = self.lib.deepep_plan_source(ptr(topk_idx), T, K, num_experts, num_ranks, num_max_tokens, ptr(dst_slot),
+                                         ptr(send_tok), ptr(send_pairs), num_blocks, blocks_per_chunk, flags,
+                                         row_floats, weights_offset, ptr(table_b), table_b.shape[1], ptr(wtable),
+                                         _stream_handle(stream))
+        _lib.check(rc, 'plan_source')
+
     def dispatch_pack(self, x_bytes, sf_bytes, topk_idx, topk_weights, src_base, dst_slot, send_offsets,
-                      packed, layout: RowLayout, dest_bases=None, stream=None):
+                      packed, layout: RowLayout, dest_bases=None, error_flag=None, stream=None):
         """x_bytes / sf_bytes: [T, bytes] uint8 views (rows may be strided).  dest_bases: optional
         int64 [R] device tensor of per-destination buffer addresses (peer windows) instead of `packed`."""
         T, K = topk_idx.shape
@@ -182,7 +220,7 @@ class HipKernels:
             ptr(sf_bytes), sf_bytes.stride(0) if sf_bytes is not None and T else 0, layout.sf_bytes,
             ptr(topk_idx), ptr(topk_weights), T, K, src_base, ptr(dst_slot), ptr(send_offsets),
             dst_slot.shape[1], ptr(packed), ptr(dest_bases), layout.row_bytes, layout.sf_off, layout.idx_off,
-            layout.w_off, layout.src_off, _stream_handle(stream))
+            layout.w_off, layout.src_off, ptr(error_flag), _stream_handle(stream))
         _lib.check(rc, 'dispatch_pack')
 
     def dispatch_count(self, packed, layout: RowLayout, num_recv, rank, num_local_experts, rank_psum, meta,
@@ -208,7 +246,7 @@ class HipKernels:
         _lib.check(rc, 'dispatch_slots')
 
     def dispatch_copy(self, packed, layout: RowLayout, num_recv, meta, expanded, recv_x_bytes, recv_sf_bytes,
-                      recv_w, x_direct=None, sf_direct=None, num_max_tokens: int = 0, stream=None):
+                      recv_w, x_direct=None, sf_direct=None, num_max_tokens: int = 0, error_flag=None, stream=None):
         """x_direct / sf_direct: [T, bytes] uint8 views of the sender's rows (one rank: the packed rows
         then carry only metadata and row i's x is x_direct[src_metadata[i][0] % num_max_tokens])."""
         x_bytes = x_direct.shape[1] if x_direct is not None else layout.x_bytes
@@ -220,7 +258,7 @@ class HipKernels:
                                            ptr(sf_direct), sf_direct.stride(0) if sf_direct is not None else 0,
                                            num_max_tokens,
                                            ptr(recv_x_bytes), ptr(recv_sf_bytes), ptr(recv_w),
-                                           _stream_handle(stream))
+                                           recv_x_bytes.shape[0], ptr(error_flag), _stream_handle(stream))
         _lib.check(rc, 'dispatch_copy')
 
     def combine_buffer_size(self, num_max_tokens_per_rank: int, hidden: int, num_topk: int,

@@ -31,6 +31,9 @@
  *       (deep_ep/include/deep_ep/impls/dispatch.cuh:79-258, 336-392)
  *   deepep_dispatch_count / _scan / _slots / _copy   (receive side)
  *       dispatch_copy_epilogue_impl (deep_ep/include/deep_ep/impls/dispatch_copy_epilogue.cuh:11-323)
+ *   deepep_route_block_counts / deepep_plan_expert / deepep_plan_source   (EP > 1 combine plan)
+ *       the addressing combine_impl and combine_reduce_epilogue_impl derive inside every launch
+ *       (combine.cuh:96-106, combine_reduce_epilogue.cuh:62-95), built once per handle on the device
  * The Python-facing runtime call these serve is _C.ElasticBuffer.combine
  * (csrc/elastic/buffer.hpp:1179-1343), re-implemented in deepep_amd/buffer.py.
  */
@@ -45,7 +48,7 @@ extern "C" {
 
 typedef struct ihipStream_t* deepep_stream_t;   /* == hipStream_t */
 
-#define DEEPEP_AMD_ABI_VERSION 9
+#define DEEPEP_AMD_ABI_VERSION 10
 
 #define DEEPEP_OK               0
 #define DEEPEP_ERR_INVALID_ARG  (-1)
@@ -59,6 +62,10 @@ typedef struct ihipStream_t* deepep_stream_t;   /* == hipStream_t */
 
 int deepep_amd_abi_version(void);
 const char* deepep_amd_last_error(void);
+/* 16 hex digits: sha256 of the sources, this header and the compile flags the library was built
+ * from (deepep_amd/_lib.py source_build_id); the Python loader refuses a binary whose id does not
+ * match the sources next to it. */
+const char* deepep_amd_build_id(void);
 
 /*
  * Per unit u in [0, num_units): gather the source rows listed in
@@ -82,8 +89,10 @@ const char* deepep_amd_last_error(void);
  *                  (a stride lets the weights ride in the tail of packed exchange rows)
  *   units_per_block  workgroup shape: 4 = 4 (row, column-chunk) items per 256-thread workgroup,
  *                  8 = 8 items per 512-thread workgroup, 0 = automatic (4 for LOCAL, else 8)
- *   error_flag     device int or NULL; set to 1 when a slot is >= num_src_rows
- *                  (such slots are skipped, never dereferenced)
+ *   error_flag     device int or NULL; bit 1 is set when a slot is >= num_src_rows (such slots are
+ *                  skipped, never dereferenced).  When bit 2 is already set (a symmetric-window
+ *                  barrier timed out, deepep_sym_barrier) the launch stores NaN rows instead of sums
+ *                  (and deepep_combine_reduce_scatter stores nothing into the peers' windows)
  */
 int deepep_combine_reduce(int mode, int weighted,
                           const void* src, int64_t num_src_rows, int64_t src_row_stride,
@@ -136,11 +145,7 @@ int deepep_set_launch_config(int vec_per_lane, int stage_lds, int store_policy, 
  *      once, units strided over the waves;
  *   4  the item kernel with XCD-contiguous workgroup order (each of the 8 XCDs takes one
  *      contiguous eighth of the items; measured slower, so only when forced);
- *  -1  (default) autotune: the first launch of each shape that writes >= 16 MiB times 0-3
- *      on the caller's stream (2 + 2 launches each, in forward then reverse order, one host sync)
- *      and keeps the fastest; launches that
- *      are being captured into a graph, or smaller, use the item kernel.  Setting -1 forgets earlier
- *      choices.
+ *  -1  (default) the item kernel.  Nothing is timed or synchronised inside a call.
  * All of them produce identical bits.  deepep_last_kernel_choice() says which one the last launch used.
  */
 int deepep_set_kernel_choice(int choice);
@@ -171,13 +176,16 @@ int deepep_dispatch_expert_counts(const int64_t* topk_idx, int num_tokens, int n
 /* Write packed row send_offsets[r] + dst_slot[t][r] for every (token t, destination r), in `packed`
  * (dest_bases NULL: one local buffer for an all-to-all) or in rank r's buffer at dest_bases[r] (device
  * uint64 [num_ranks]: the peers' symmetric windows, system-scope stores -- the xGMI push of
- * dispatch.cuh:373-392); src_global_idx = src_base + t.  topk_weights may be NULL (zeros are sent). */
+ * dispatch.cuh:373-392); src_global_idx = src_base + t.  topk_weights may be NULL (zeros are sent).
+ * error_flag (device int or NULL): with dest_bases, nothing is stored once bit 2 is set (the window
+ * barrier before the push timed out). */
 int deepep_dispatch_pack(const void* x, int64_t x_row_stride_bytes, int x_bytes,
                          const void* sf, int64_t sf_row_stride_bytes, int sf_bytes,
                          const int64_t* topk_idx, const float* topk_weights, int num_tokens, int num_topk,
                          int32_t src_base, const int32_t* dst_slot, const int32_t* send_offsets, int num_ranks,
                          void* packed, const uint64_t* dest_bases, int64_t row_bytes,
-                         int sf_off, int idx_off, int w_off, int src_off, deepep_stream_t stream);
+                         int sf_off, int idx_off, int w_off, int src_off, const int32_t* error_flag,
+                         deepep_stream_t stream);
 
 /* Receive side, pass 1: src_metadata columns 0-1 ({src_global_idx, src_rank * K + master lane}),
  * recv_topk_idx (local expert or -1, int64 [num_recv][K], may be NULL) and per-256-row expert
@@ -202,12 +210,65 @@ int deepep_dispatch_slots(const void* packed, int64_t row_bytes, int idx_off, in
 /* Pass 4: recv_x / recv_sf rows (row i, or every local slot when expanded) and top-k weights
  * ([num_recv][K] or, expanded, [slot]).  recv_sf / recv_topk_weights may be NULL.  With x_direct
  * (one rank: nothing was exchanged, the packed rows carry only metadata) the x / sf bytes of row i
- * are read from x_direct / sf_direct at row src_metadata[i][0] % num_max_tokens. */
+ * are read from x_direct / sf_direct at row src_metadata[i][0] % num_max_tokens.  Destination rows
+ * >= num_out_rows (the rows recv_x holds) are skipped and set bit 1 of error_flag (device int or
+ * NULL); once bit 2 is set (a timed-out window barrier) nothing is stored. */
 int deepep_dispatch_copy(const void* packed, int64_t row_bytes, int x_bytes, int sf_off, int sf_bytes, int w_off,
                          int num_recv, int num_topk, const int32_t* src_metadata, int expanded,
                          const void* x_direct, int64_t x_direct_stride_bytes,
                          const void* sf_direct, int64_t sf_direct_stride_bytes, int num_max_tokens,
-                         void* recv_x, void* recv_sf, float* recv_topk_weights, deepep_stream_t stream);
+                         void* recv_x, void* recv_sf, float* recv_topk_weights, int64_t num_out_rows,
+                         int32_t* error_flag, deepep_stream_t stream);
+
+/* ------------------------------------------------------------------ EP > 1 combine plan
+ * The EP > 1 combine runs in pipeline chunks of source tokens: chunk c = tokens
+ * [c * B, (c + 1) * B) of every rank, B = blocks_per_chunk * DEEPEP_PLAN_BLOCK_TOKENS.  Phase A on an
+ * expert rank reduces the chunk's received rows into partials; they travel to their source ranks
+ * (RCCL all-to-all of the chunk's rows grouped by source rank, or xGMI stores into the source rank's
+ * window); phase B on the source rank reduces each token's partials.  These three calls build every
+ * table of that schedule on the device from the dispatch's counts, so a first combine needs no host
+ * synchronisation.  Counts are per block of DEEPEP_PLAN_BLOCK_TOKENS consecutive tokens of a source
+ * rank, int32 [num_ranks][num_blocks] (num_blocks >= ceil(num_max_tokens / 64)).
+ */
+#define DEEPEP_PLAN_BLOCK_TOKENS 64
+#define DEEPEP_PLAN_EXPANDED     1    /* x is the expanded layout (metadata columns 2.. are rows)       */
+#define DEEPEP_PLAN_SINGLE       2    /* single reduction: every valid (row, lane) travels unreduced     */
+#define DEEPEP_PLAN_INTERLEAVE   4    /* phase-A units round-robin over source ranks (xGMI stores)      */
+#define DEEPEP_PLAN_RANK_LAYOUT  8    /* receive slot = expert rank (R <= K), else the master lane        */
+#define DEEPEP_PLAN_WINDOW      16    /* source side: rows are window rows slot * T_max + t               */
+
+/* Sender side of the notify: tok_counts[r][b] = tokens of block b routed to rank r, pair_counts[r][b] =
+ * (token, lane) entries of block b routed to r (blocks past num_tokens are zero). */
+int deepep_route_block_counts(const int64_t* topk_idx, int num_tokens, int num_topk, int num_experts, int num_ranks,
+                              int num_blocks, int32_t* tok_counts, int32_t* pair_counts, deepep_stream_t stream);
+
+/* Expert side: phase-A units of every chunk, concatenated in chunk order.  recv_tok / recv_pairs are
+ * the counts received from every source rank (rows received per source block).  Inside a chunk, units
+ * are grouped by source rank (the send buffer of an all-to-all), or round-robin over the source ranks
+ * with DEEPEP_PLAN_INTERLEAVE.  Multiple reduction: one unit per received row i; table_a[u] = the
+ * metadata slots of i (expanded, K wide) or i (1 wide), wtable_a[u][k] = i * K + k (non-expanded,
+ * may be NULL).  Single reduction: one unit per valid (row, lane) in (row, lane) order, table_a[u] =
+ * the expanded row (1 wide).  out_rows (optional, the xGMI transport): byte address of unit u's row,
+ * window_bases[src_rank] + (slot * num_max_tokens + src_token) * window_row_bytes, slot = rank (rank
+ * layout) or the master lane (multiple reduction), the lane (single reduction) -- combine.cuh:96-106. */
+int deepep_plan_expert(const int32_t* src_metadata, int num_topk, int num_ranks, int rank, int num_max_tokens,
+                       const int32_t* recv_tok, const int32_t* recv_pairs, int num_blocks, int blocks_per_chunk,
+                       int flags, int32_t* table_a, int32_t* wtable_a, const uint64_t* window_bases,
+                       int64_t window_row_bytes, uint64_t* out_rows, deepep_stream_t stream);
+
+/* Source side, per owned token t (chunk c = t / B).  Multiple reduction: table_b [T][min(R, K)] = the
+ * rows of t's partials in ascending dedup-master-lane order (a rank's master is its highest top-k
+ * lane; combine_reduce_epilogue.cuh:74-95), then -1; wtable [T][K] (or NULL) = row(rank of lane k) *
+ * row_floats + weights_offset + k, or -1: the float index of lane k's weight in the packed receive rows.
+ * A row is the partial's row in chunk c's receive buffer (grouped by expert rank, ascending token:
+ * dst_slot [T][R] from deepep_dispatch_route gives the rank among earlier tokens) or, with
+ * DEEPEP_PLAN_WINDOW, the window row slot * num_max_tokens + t.  Single reduction: table_b [T][K] = the
+ * row of (t, k): receive-buffer order (expert rank, then (token, lane)) or window row k * T_max + t. */
+int deepep_plan_source(const int64_t* topk_idx, int num_tokens, int num_topk, int num_experts, int num_ranks,
+                       int num_max_tokens, const int32_t* dst_slot, const int32_t* send_tok,
+                       const int32_t* send_pairs, int num_blocks, int blocks_per_chunk, int flags,
+                       int64_t row_floats, int64_t weights_offset, int32_t* table_b, int table_b_width,
+                       int32_t* wtable, deepep_stream_t stream);
 
 /* ------------------------------------------------------------------ symmetric buffer over xGMI
  * Replaces the reference's NCCLSymmetricMemoryContext (csrc/elastic/nccl.cu:62-153, buffer.hpp:181-208)
@@ -262,8 +323,8 @@ int deepep_combine_reduce_scatter(int weighted,
                                   const float* wsrc, int num_weights, int64_t weights_offset,
                                   int32_t* error_flag, deepep_stream_t stream);
 
-/* A CU budget: a stream whose kernels run on `num_cus` compute units only
- * (hipExtStreamCreateWithCUMask, the first num_cus mask bits = num_cus / 8 CUs on every XCD),
+/* A CU budget: a stream whose kernels run on `num_cus` compute units only, rounded up to a multiple
+ * of 8 (hipExtStreamCreateWithCUMask, the first num_cus mask bits = num_cus / 8 CUs on every XCD),
  * leaving the rest to overlapping
  * compute.  It is how this build honours an explicit num_sms (the reference sizes combine_impl's
  * grid with it, csrc/kernels/elastic/combine.hpp:135, elastic.py:1086-1088). */

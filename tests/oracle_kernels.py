@@ -10,6 +10,7 @@ from typing import Optional
 import torch
 
 import oracle
+from tests import plan_ref
 
 
 def _p(t: Optional[torch.Tensor]):
@@ -53,6 +54,22 @@ class OracleKernels:
             ok = (topk_idx >= 0) & (inv.view(-1, 1) >= 0)
             wtable.copy_(torch.where(ok, inv.view(-1, 1) * num_topk + k, torch.full_like(topk_idx, -1)).to(torch.int32))
 
+    # ------------------------------------------------------------------ EP > 1 plan (tests/plan_ref.py)
+    def route_block_counts(self, topk_idx, num_experts, num_ranks, num_blocks, tok, pairs, stream=None):
+        t, p = plan_ref.route_block_counts(topk_idx, num_experts, num_ranks, num_blocks)
+        tok.copy_(t)
+        pairs.copy_(p)
+
+    def plan_expert(self, meta, num_topk, num_ranks, rank, num_max_tokens, recv_tok, recv_pairs, num_blocks,
+                    blocks_per_chunk, flags, table_a, wtable_a, window_bases, window_row_bytes, out_rows, stream=None):
+        plan_ref.plan_expert(meta, num_topk, num_ranks, rank, num_max_tokens, recv_tok, recv_pairs, num_blocks,
+                             blocks_per_chunk, flags, table_a, wtable_a, window_bases, window_row_bytes, out_rows)
+
+    def plan_source(self, topk_idx, num_experts, num_ranks, num_max_tokens, dst_slot, send_tok, send_pairs,
+                    num_blocks, blocks_per_chunk, flags, row_floats, weights_offset, table_b, wtable, stream=None):
+        plan_ref.plan_source(topk_idx, num_experts, num_ranks, num_max_tokens, dst_slot, send_tok, send_pairs,
+                             num_blocks, blocks_per_chunk, flags, row_floats, weights_offset, table_b, wtable)
+
     # ------------------------------------------------------------------ dispatch primitives (CPU stand-ins)
     def dispatch_route(self, topk_idx, num_experts, num_ranks, dst_slot, send_counts, stream=None):
         epr = num_experts // num_ranks
@@ -68,7 +85,7 @@ class OracleKernels:
         counts.copy_(torch.bincount(valid, minlength=num_experts)[:num_experts].to(torch.int32))
 
     def dispatch_pack(self, x_bytes, sf_bytes, topk_idx, topk_weights, src_base, dst_slot, send_offsets,
-                      packed, layout, dest_bases=None, stream=None):
+                      packed, layout, dest_bases=None, error_flag=None, stream=None):
         assert dest_bases is None, 'the CPU stand-in packs into one local buffer'
         t_idx, r_idx = (dst_slot >= 0).nonzero(as_tuple=True)
         dest = (send_offsets[r_idx] + dst_slot[t_idx, r_idx]).long()
@@ -129,7 +146,7 @@ class OracleKernels:
                         run[e] += 1
 
     def dispatch_copy(self, packed, layout, num_recv, meta, expanded, recv_x_bytes, recv_sf_bytes, recv_w,
-                      x_direct=None, sf_direct=None, num_max_tokens=0, stream=None):
+                      x_direct=None, sf_direct=None, num_max_tokens=0, error_flag=None, stream=None):
         N, K = num_recv, layout.num_topk
         if x_direct is not None:
             t = (meta[:N, 0].long() % num_max_tokens)

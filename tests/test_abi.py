@@ -33,7 +33,16 @@ def test_exports_every_declared_symbol(lib):
 
 
 def test_abi_version(lib):
-    assert lib.deepep_amd_abi_version() == 9
+    assert lib.deepep_amd_abi_version() == 10
+
+
+def test_build_id_matches_sources(lib):
+    """The loaded binary was built from the tracked sources (build() rebuilds on any difference and
+    the loader refuses a stale binary)."""
+    from deepep_amd import _lib
+    want = _lib.source_build_id()
+    assert want is not None and len(want) == 16
+    assert lib.deepep_amd_build_id().decode() == want == _lib.binary_build_id(_lib.LIB_PATH)
 
 
 def test_invalid_arguments_are_rejected_without_a_gpu(lib):
@@ -60,7 +69,7 @@ def test_invalid_arguments_are_rejected_without_a_gpu(lib):
     # zero units: nothing to do, success without a launch
     assert lib.deepep_combine_reduce(1, 0, 16, 1, 8, None, 0, 1, None, None, None, 48, 8, 0, 8,
                                      None, 0, None, None, 0, 0, 0, None, None) == 0
-    # kernel choice: -1 (autotune), 0-4; anything else is rejected with a message
+    # kernel choice: -1 (default: the item kernel), 0-4; anything else is rejected with a message
     assert lib.deepep_set_kernel_choice(5) == -1 and b'kernel choice' in lib.deepep_amd_last_error()
     assert lib.deepep_set_kernel_choice(-2) == -1
     for c in (0, 1, 2, 3, 4, -1):
@@ -70,6 +79,16 @@ def test_invalid_arguments_are_rejected_without_a_gpu(lib):
     assert lib.deepep_set_launch_config(3, -1, -1, 0) == -1
     assert lib.deepep_set_launch_config(0, -1, -1, 3) == -1
     assert lib.deepep_set_launch_config(0, -1, -1, 0) == 0
+    # EP > 1 plan builders: rank out of range, too few blocks, wrong table width, single w/o expanded
+    assert lib.deepep_plan_expert(16, 8, 8, 8, 64, 16, 16, 1, 1, 1, 16, None, None, 0, None, None) == -1
+    assert b'plan_expert' in lib.deepep_amd_last_error()
+    assert lib.deepep_plan_expert(16, 8, 8, 0, 64, 16, 16, 1, 1, 2, 16, None, None, 0, None, None) == -1
+    assert lib.deepep_plan_source(16, 200, 8, 64, 8, 256, 16, 16, 16, 1, 1, 0, 0, 0, 16, 8, None, None) == -1
+    assert lib.deepep_plan_source(16, 64, 8, 64, 8, 256, 16, 16, 16, 1, 1, 0, 0, 0, 16, 7, None, None) == -1
+    assert lib.deepep_route_block_counts(16, 200, 8, 64, 8, 1, 16, 16, None) == -1
+    assert lib.deepep_route_block_counts(None, 0, 8, 64, 8, 0, None, None, None) == 0     # nothing to count
+    # a CU budget is whole CUs per XCD; nonsense is rejected
+    assert lib.deepep_stream_create_cu_budget(0, None) == -1
 
 
 def test_buffer_size_matches_reference_formula(lib):

@@ -174,6 +174,35 @@ def test_kernel_reduce_scatter_rows(kern, weighted, hidden):
     assert torch.equal(got_w, out_w)
 
 
+def test_kernel_poisoned_by_timed_out_barrier(kern):
+    """Bit 2 of the error flag (a symmetric-window barrier timed out): the reduce writes NaN rows and the
+    scatter (phase A into peers' windows) stores nothing; bit 1 (bad slot) alone changes nothing."""
+    rng = np.random.default_rng(3)
+    src = _bf16(_random_rows(rng, 64, 1024))
+    table = torch.randint(0, 64, (16, 8), dtype=torch.int32, device='cuda')
+    for flag, choice in ((2, 0), (3, 1), (2, 3)):
+        assert kern.lib.deepep_set_kernel_choice(choice) == 0
+        try:
+            err = torch.full((1,), flag, dtype=torch.int32, device='cuda')
+            out = torch.zeros((16, 1024), dtype=torch.bfloat16, device='cuda')
+            kern.combine_reduce(MODE_FUSED, src, out, 16, table=table, error_flag=err)
+            win = torch.zeros((16 * 2048,), dtype=torch.uint8, device='cuda')
+            addr = torch.arange(16, device='cuda', dtype=torch.int64) * 2048 + win.data_ptr()
+            kern.combine_reduce_scatter(src, 16, addr, table=table, error_flag=err)
+            torch.cuda.synchronize()
+            assert bool(torch.isnan(out.float()).all()), flag
+            assert int(win.count_nonzero()) == 0, flag
+        finally:
+            kern.lib.deepep_set_kernel_choice(-1)
+    err = torch.ones((1,), dtype=torch.int32, device='cuda')
+    out = torch.zeros((16, 1024), dtype=torch.bfloat16, device='cuda')
+    kern.combine_reduce(MODE_FUSED, src, out, 16, table=table, error_flag=err)
+    ref = torch.zeros_like(out)
+    kern.combine_reduce(MODE_FUSED, src, ref, 16, table=table)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+
+
 def test_kernel_empty_and_errors(kern):
     src = torch.zeros((4, 64), dtype=torch.bfloat16, device='cuda')
     out = torch.empty((0, 64), dtype=torch.bfloat16, device='cuda')
@@ -192,48 +221,8 @@ def test_kernel_empty_and_errors(kern):
 
 # ----------------------------------------------------------------------------- ElasticBuffer level
 
-class _ThreadComm:
-    """all_to_all_single among threads that each drive one simulated rank on the same GPU."""
-
-    def __init__(self, n):
-        self.n = n
-        self.bar = threading.Barrier(n)
-        self.slots = [None] * n
-
-    def a2a(self, rank, out, inp, out_splits=None, in_splits=None):
-        torch.cuda.synchronize()
-        self.slots[rank] = (inp, in_splits if in_splits is not None else [inp.shape[0] // self.n] * self.n)
-        self.bar.wait()
-        pos = 0
-        for s in range(self.n):
-            sinp, splits = self.slots[s]
-            start = sum(splits[:rank])
-            cnt = splits[rank]
-            out[pos:pos + cnt].copy_(sinp[start:start + cnt])
-            pos += cnt
-        torch.cuda.synchronize()
-        self.bar.wait()
-
-
-class _Done:
-    """Completed work handle (the thread exchange synchronises the device before returning)."""
-
-    def wait(self):
-        return True
-
-
-class _FakeGroup:
-    def __init__(self, rank, n, comm):
-        self._rank, self._n, self.comm = rank, n, comm
-
-    def rank(self):
-        return self._rank
-
-    def size(self):
-        return self._n
-
-    def barrier(self):
-        self.comm.bar.wait()
+# the simulated ranks' exchange has ProcessGroupNCCL's stream semantics (tests/sim.py)
+from tests.sim import FakeGroup as _FakeGroup, ThreadComm as _ThreadComm  # noqa: E402
 
 
 def _buffer_case(rank, world, fixture, comm, results):
@@ -254,8 +243,7 @@ def _buffer_case(rank, world, fixture, comm, results):
             grp = dist.group.WORLD
         buf = ElasticBuffer(grp, num_max_tokens_per_rank=T, hidden=H, num_topk=K)
         if world > 1:
-            buf._a2a = lambda out, inp, os_=None, is_=None: comm.a2a(rank, out, inp, os_, is_)
-            buf._a2a_async = lambda out, inp, os_, is_: (comm.a2a(rank, out, inp, os_, is_), _Done())[1]
+            comm.install(buf, rank)
         idx = torch.from_numpy(me['topk_idx'].copy()).cuda()
         w = torch.from_numpy(me['topk_weights'].copy()).cuda()
         x = _bf16(me['x']) if 'x' in me else torch.randn((T, H), device='cuda').to(torch.bfloat16)
@@ -305,7 +293,7 @@ def _buffer_case(rank, world, fixture, comm, results):
         from tests.test_buffer_cpu import _weighted_single
         sbuf = ElasticBuffer(grp, num_max_tokens_per_rank=T, hidden=H, num_topk=K, allow_multiple_reduction=False)
         if world > 1:
-            sbuf._a2a, sbuf._a2a_async = buf._a2a, buf._a2a_async
+            comm.install(sbuf, rank)
         for nb in (0, 1, 2):
             bias = None if nb == 0 else (biases[0] if nb == 1 else tuple(biases))
             out, out_w, _ = sbuf.combine(x_exp, ex_handle, bias=bias)
@@ -384,12 +372,12 @@ def test_config2_full_size_bitwise(weighted, T, skew):
     ref, _ = oracle.phase_b(recv, None, idx.cpu().numpy(), E, 1, True, True)
     lib = buf.kernels.lib
     try:
-        # the item kernel, the streaming kernel (2 and 1 vectors per lane, persistent), and the autotuned choice
+        # the item kernel, the streaming kernel (2 and 1 vectors per lane, persistent), XCD order, default
         for choice in (0, 1, 2, 3, 4, -1):
             assert lib.deepep_set_kernel_choice(choice) == 0
             out, out_w, _ = buf.combine(y, handle, topk_weights=ex_w, apply_topk_weights=weighted)
             torch.cuda.synchronize()
-            assert lib.deepep_last_kernel_choice() in ((choice,) if choice >= 0 else (0, 1, 2, 3))
+            assert lib.deepep_last_kernel_choice() == (choice if choice >= 0 else 0)
             assert np.array_equal(_u16(out), ref), f'kernel choice {choice}'
             assert torch.equal(out_w, w)
     finally:

@@ -128,7 +128,7 @@ def _ep_thread(rank, world, seed, comm, results):
     """One simulated rank of a random EP = `world` case (threads on the one GPU, all-to-all by copies)."""
     try:
         from deepep_amd import ElasticBuffer
-        from tests.test_combine_gpu import _Done, _FakeGroup
+        from tests.sim import FakeGroup as _FakeGroup
         torch.cuda.set_device(0)
         rng = np.random.default_rng(seed)            # same stream in every thread: same global case
         K = int(rng.choice([1, 2, 4, 6, 8]))
@@ -163,8 +163,7 @@ def _ep_thread(rank, world, seed, comm, results):
         g_idx, g_w = torch.from_numpy(idx_all[rank]).cuda(), torch.from_numpy(w_all[rank]).cuda()
         for amr in (True, False):
             buf = ElasticBuffer(grp, num_max_tokens_per_rank=T, hidden=H, num_topk=K, allow_multiple_reduction=amr)
-            buf._a2a = lambda out, inp, os_=None, is_=None: comm.a2a(rank, out, inp, os_, is_)
-            buf._a2a_async = lambda out, inp, os_, is_: (comm.a2a(rank, out, inp, os_, is_), _Done())[1]
+            comm.install(buf, rank)
             _, _, ex_w, handle, _ = buf.dispatch(x, topk_idx=g_idx, topk_weights=g_w, num_experts=E, do_expand=True)
             if not np.array_equal(handle.recv_src_metadata.cpu().numpy(), metas[rank]):
                 failures.append(f'amr={amr}: recv_src_metadata')
@@ -207,7 +206,7 @@ def test_random_shapes_ep_sim(case, monkeypatch, kernel_choice):
     """Random EP = 2..8 cases (ragged per-rank batches incl. empty ranks, top-k 1..8, R > K and
     R <= K layouts, chunked and one-shot exchange), all ranks simulated by threads on the GPU."""
     import threading
-    from tests.test_combine_gpu import _ThreadComm
+    from tests.sim import ThreadComm as _ThreadComm
     rng = np.random.default_rng(1000 + case)
     world = int(rng.choice([2, 3, 4, 5, 8]))
     if rng.random() < 0.5:

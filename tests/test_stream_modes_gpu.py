@@ -132,13 +132,12 @@ def test_stream_modes_ep1(monkeypatch, avoid_record_stream):
 def _sim_rank(rank, world, comm, results):
     try:
         from deepep_amd import ElasticBuffer
-        from tests.test_combine_gpu import _Done, _FakeGroup
+        from tests.sim import FakeGroup as _FakeGroup
         torch.cuda.set_device(0)
         T, H, K, E = 1100, 1024, 8, 32
         x, idx, w = _inputs(T, H, K, E, 100 + rank)
         buf = ElasticBuffer(_FakeGroup(rank, world, comm), num_max_tokens_per_rank=T, hidden=H, num_topk=K)
-        buf._a2a = lambda out, inp, os_=None, is_=None: comm.a2a(rank, out, inp, os_, is_)
-        buf._a2a_async = lambda out, inp, os_, is_: (comm.a2a(rank, out, inp, os_, is_), _Done())[1]
+        comm.install(buf, rank)
         results[rank] = _run_modes(buf, x, idx, w, E, T, H, f'ep{world} rank {rank}')
     except Exception:
         import traceback
@@ -148,7 +147,7 @@ def _sim_rank(rank, world, comm, results):
 
 def test_stream_modes_ep4_pipelined(monkeypatch):
     """EP = 4, 1100 tokens per rank -> the 4-chunk pipelined exchange (phase B on a second stream)."""
-    from tests.test_combine_gpu import _ThreadComm
+    from tests.sim import ThreadComm as _ThreadComm
     monkeypatch.setenv('DEEPEP_COMBINE_CHUNKS', '4')
     world = 4
     comm = _ThreadComm(world)

@@ -1,0 +1,303 @@
+"""The combine needs no host synchronisation, and its EP > 1 schedule is ordered by streams alone.
+
+* The EP > 1 plan kernels (deepep_plan_expert / _source, deepep_route_block_counts) against their CPU
+  restatement (tests/plan_ref.py), bit for bit, over rank counts, top-k, chunking, both reduction
+  recipes, both layouts and both transports' addressing.
+* A FIRST combine on a fresh handle (EP = 1, and EP = 4 / 8 simulated by threads whose exchange has
+  ProcessGroupNCCL's stream semantics, tests/sim.py) runs under torch.cuda.set_sync_debug_mode("error")
+  -- any host sync raises -- and is bitwise equal to the oracle; the reference's combine has no CPU
+  sync either (csrc/elastic/buffer.hpp:1179-1343).
+* The first combine on a fresh handle is captured into a HIP graph with no eager call before it.
+* The pipelined EP > 1 schedule (phase A(c) | exchange(c) | phase B(c) on a second stream) is correct
+  only because of its stream waits: with the exchange delayed on its stream, dropping the wait for it
+  makes the result wrong, which this test detects.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from tests import plan_ref
+from tests.sim import FakeGroup, ThreadComm, run_threads
+
+pytestmark = pytest.mark.gpu
+
+
+def _u16(t: torch.Tensor) -> np.ndarray:
+    return t.detach().cpu().contiguous().view(torch.int16).numpy().view(np.uint16)
+
+
+def _bf16(a: np.ndarray) -> torch.Tensor:
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.int16)).view(torch.bfloat16).cuda()
+
+
+def _routing(world, T, K, E, seed, masked=0.1):
+    rng = np.random.default_rng(seed)
+    idx_all, w_all = [], []
+    for _ in range(world):
+        scores = rng.random((T, E))
+        idx = np.argsort(-scores, axis=1)[:, :K].astype(np.int64)
+        idx[rng.random((T, K)) < masked] = -1
+        idx_all.append(idx)
+        w_all.append((rng.random((T, K)).astype(np.float32) * (idx >= 0)).astype(np.float32))
+    return rng, idx_all, w_all
+
+
+def _expanded_inputs(rng, disp, idx_all, w_all, T, H):
+    """Per expert rank: expanded rows (random bf16, one per (token, lane) received) and their weights."""
+    x_all, wexp_all = [], []
+    for d in disp:
+        n = d['num_expanded']
+        x_all.append(oracle.f32_to_bf16(rng.standard_normal((n, H)).astype(np.float32)))
+        we = np.zeros((n,), np.float32)
+        for row, (g, k) in enumerate(d['expanded_src']):
+            s, t = divmod(int(g), T)
+            we[row] = w_all[s][t, k]
+        wexp_all.append(we)
+    return x_all, wexp_all
+
+
+@pytest.fixture(scope='module')
+def kern():
+    from deepep_amd.kernels import HipKernels
+    return HipKernels()
+
+
+# ----------------------------------------------------------------------------- plan kernels
+@pytest.mark.parametrize('world,K,T,chunks', [(2, 8, 200, 3), (3, 4, 130, 1), (4, 2, 333, 4), (8, 8, 700, 4),
+                                              (8, 8, 64, 1), (5, 1, 97, 2)])
+def test_plan_kernels_match_reference(kern, world, K, T, chunks):
+    from deepep_amd import _lib
+    from deepep_amd.handle import chunk_geometry
+    E = world * max(2, (K + world - 1) // world + 1)
+    rng, idx_all, _ = _routing(world, T, K, E, seed=world * 100 + K)
+    nb, bpc, _ = chunk_geometry(T, chunks)
+    disp = oracle.simulate_dispatch(idx_all, E, T)
+    # per-source block counts: HIP vs the restatement
+    tok_all, pairs_all = [], []
+    for s in range(world):
+        idx = torch.from_numpy(idx_all[s]).cuda()
+        tok = torch.empty((world, nb), dtype=torch.int32, device='cuda')
+        pairs = torch.empty_like(tok)
+        kern.route_block_counts(idx, E, world, nb, tok, pairs)
+        rt, rp = plan_ref.route_block_counts(torch.from_numpy(idx_all[s]), E, world, nb)
+        assert torch.equal(tok.cpu(), rt) and torch.equal(pairs.cpu(), rp)
+        tok_all.append(rt)
+        pairs_all.append(rp)
+    bases = torch.tensor([(1 << 40) * (s + 1) for s in range(world)], dtype=torch.int64)
+    for r in range(world):
+        meta = torch.from_numpy(disp[r]['src_metadata']).cuda()
+        recv_tok = torch.stack([tok_all[s][r] for s in range(world)])        # [source, block]
+        recv_pairs = torch.stack([pairs_all[s][r] for s in range(world)])
+        for single in (False, True):
+            for expanded in ((True,) if single else (True, False)):
+                for window in (False, True):
+                    flags = ((_lib.PLAN_EXPANDED if expanded else 0) | (_lib.PLAN_SINGLE if single else 0) |
+                             (_lib.PLAN_RANK_LAYOUT if world <= K and not single else 0) |
+                             (_lib.PLAN_INTERLEAVE if window else 0))
+                    total = int((recv_pairs if single else recv_tok).sum())
+                    width = K if expanded and not single else 1
+                    outs = []
+                    for dev in ('cuda', 'cpu'):
+                        ta = torch.full((total, width), -7, dtype=torch.int32, device=dev)
+                        wa = torch.full((total, K), -7, dtype=torch.int32, device=dev) if not expanded else None
+                        orow = torch.full((total,), -7, dtype=torch.int64, device=dev) if window else None
+                        args = (K, world, r, T, recv_tok.to(dev), recv_pairs.to(dev), nb, bpc, flags, ta, wa,
+                                bases.to(dev) if window else None, 14400 if window else 0, orow)
+                        if dev == 'cuda':
+                            kern.plan_expert(meta, *args)
+                        else:
+                            plan_ref.plan_expert(meta.cpu(), *args)
+                        outs.append([t.cpu() if t is not None else None for t in (ta, wa, orow)])
+                    for g, c, name in zip(outs[0], outs[1], ('table_a', 'wtable_a', 'out_rows')):
+                        assert (g is None) == (c is None)
+                        assert g is None or torch.equal(g, c), (r, single, expanded, window, name)
+        # source side (this rank's own tokens)
+        idx = torch.from_numpy(idx_all[r]).cuda()
+        dst = torch.empty((T, world), dtype=torch.int32, device='cuda')
+        send_counts = torch.empty((world,), dtype=torch.int32, device='cuda')
+        kern.dispatch_route(idx, E, world, dst, send_counts)
+        for single in (False, True):
+            for window in (False, True):
+                flags = ((_lib.PLAN_SINGLE if single else 0) | (_lib.PLAN_WINDOW if window else 0) |
+                         (_lib.PLAN_RANK_LAYOUT if world <= K and not single else 0))
+                width = K if single else min(world, K)
+                outs = []
+                for dev in ('cuda', 'cpu'):
+                    tb = torch.full((T, width), -7, dtype=torch.int32, device=dev)
+                    wt = None if single else torch.full((T, K), -7, dtype=torch.int32, device=dev)
+                    args = (E, world, T, dst.to(dev), tok_all[r].to(dev), pairs_all[r].to(dev), nb, bpc, flags,
+                            0 if single else 3600, 0 if single else 3584, tb, wt)
+                    if dev == 'cuda':
+                        kern.plan_source(idx, *args)
+                    else:
+                        plan_ref.plan_source(idx.cpu(), *args)
+                    outs.append((tb.cpu(), wt.cpu() if wt is not None else None))
+                assert torch.equal(outs[0][0], outs[1][0]), (r, single, window, 'table_b')
+                assert (outs[0][1] is None and outs[1][1] is None) or torch.equal(outs[0][1], outs[1][1]), \
+                    (r, single, window, 'wtable')
+
+
+# ----------------------------------------------------------------------------- sync-free first combine
+def _group1():
+    import torch.distributed as dist
+    if not dist.is_initialized():
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        os.environ.setdefault('MASTER_PORT', '29561')
+        dist.init_process_group('gloo', rank=0, world_size=1)
+    return dist.group.WORLD
+
+
+def _sync_free_rank(rank, world, T, H, K, E, comm, results):
+    try:
+        torch.cuda.set_device(0)
+        from deepep_amd import ElasticBuffer
+        rng, idx_all, w_all = _routing(world, T, K, E, seed=77 + world)
+        disp = oracle.simulate_dispatch(idx_all, E, T)
+        x_all, wexp_all = _expanded_inputs(rng, disp, idx_all, w_all, T, H)
+        bias = [oracle.f32_to_bf16(rng.standard_normal((T, H)).astype(np.float32)) for _ in range(world)]
+        metas = [d['src_metadata'] for d in disp]
+        expect = oracle.combine_ep(x_all, metas, idx_all, E, T, expanded=True, topk_weights_per_rank=wexp_all,
+                                   bias_per_rank=[(b, None) for b in bias])[rank]
+        expect_single = oracle.combine_ep(x_all, metas, idx_all, E, T, expanded=True, allow_multiple_reduction=False,
+                                          bias_per_rank=[(b, None) for b in bias])[rank][0]
+        grp = FakeGroup(rank, world, comm) if world > 1 else _group1()
+        failures = []
+        for amr in (True, False):
+            buf = ElasticBuffer(grp, num_max_tokens_per_rank=T, hidden=H, num_topk=K, allow_multiple_reduction=amr)
+            if world > 1:
+                comm.install(buf, rank)
+            x = torch.zeros((T, H), dtype=torch.bfloat16, device='cuda')
+            _, _, ex_w, handle, _ = buf.dispatch(x, topk_idx=torch.from_numpy(idx_all[rank]).cuda(),
+                                                 topk_weights=torch.from_numpy(w_all[rank]).cuda(), num_experts=E,
+                                                 do_expand=True)
+            if not np.array_equal(handle.recv_src_metadata.cpu().numpy(), metas[rank]):
+                failures.append(f'amr={amr}: metadata')
+            xin, b = _bf16(x_all[rank]), _bf16(bias[rank])
+            assert not handle._combine_plans                 # the combine below is the handle's first
+            torch.cuda.synchronize()
+            if world > 1:
+                comm.bar.wait()
+            if rank == 0:
+                torch.cuda.set_sync_debug_mode('error')
+            if world > 1:
+                comm.bar.wait()
+            try:
+                if amr:
+                    out, out_w, _ = buf.combine(xin, handle, topk_weights=ex_w, bias=b)
+                else:
+                    out, out_w, _ = buf.combine(xin, handle, bias=b)
+            finally:
+                if world > 1:
+                    comm.bar.wait()
+                if rank == 0:
+                    torch.cuda.set_sync_debug_mode(0)
+            torch.cuda.synchronize()
+            if not np.array_equal(_u16(out), expect[0] if amr else expect_single):
+                failures.append(f'amr={amr}: combined_x')
+            if amr and not np.array_equal(out_w.cpu().numpy(), expect[1]):
+                failures.append('combined_topk_weights')
+        results[rank] = failures
+    except Exception:
+        import traceback
+        results[rank] = [traceback.format_exc()]
+        if comm is not None:
+            comm.bar.abort()
+
+
+@pytest.mark.parametrize('world,T', [(1, 1024), (4, 1024), (8, 1088)])
+def test_first_combine_has_no_host_sync(world, T):
+    """Fresh dispatch, then the handle's FIRST combine (plan built on the device, pipelined exchange at
+    EP > 1: T >= 1024 gives 4 chunks) under set_sync_debug_mode('error'); bitwise vs the oracle."""
+    H, K, E = 256, 8, 64
+    comm = ThreadComm(world) if world > 1 else None
+    results = run_threads(world, _sync_free_rank, (world, T, H, K, E, comm))
+    assert len(results) == world, results
+    bad = {r: f for r, f in results.items() if f}
+    assert not bad, bad
+
+
+def test_first_combine_captured_into_a_graph():
+    """The first combine on a fresh handle (its plan is built by kernels inside the capture) is captured
+    into a HIP graph and replays bitwise; an eager call afterwards agrees."""
+    from deepep_amd import ElasticBuffer
+    T, H, K, E = 640, 2048, 8, 64
+    rng, idx_all, w_all = _routing(1, T, K, E, seed=5)
+    buf = ElasticBuffer(_group1(), num_max_tokens_per_rank=T, hidden=H, num_topk=K)
+    x = torch.zeros((T, H), dtype=torch.bfloat16, device='cuda')
+    _, _, ex_w, handle, _ = buf.dispatch(x, topk_idx=torch.from_numpy(idx_all[0]).cuda(),
+                                         topk_weights=torch.from_numpy(w_all[0]).cuda(), num_experts=E, do_expand=True)
+    y = _bf16(oracle.f32_to_bf16(rng.standard_normal((handle.num_expanded_tokens, H)).astype(np.float32)))
+    bias = _bf16(oracle.f32_to_bf16(rng.standard_normal((T, H)).astype(np.float32)))
+    assert not handle._combine_plans
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        out, out_w, _ = buf.combine(y, handle, topk_weights=ex_w, bias=bias, apply_topk_weights=True)
+    assert not handle._combine_plans                 # the captured plan belongs to the graph
+    graph.replay()
+    torch.cuda.synchronize()
+    meta = handle.recv_src_metadata.cpu().numpy()
+    part, _ = oracle.phase_a(_u16(y), meta, K, True, ex_w.cpu().numpy(), weighted=True)
+    recv = np.zeros((1, T, H), np.uint16)
+    recv[0, meta[:, 0] % T] = part
+    ref, _ = oracle.phase_b(recv, None, idx_all[0], E, 1, True, True, _u16(bias))
+    assert np.array_equal(_u16(out), ref)
+    assert np.array_equal(out_w.cpu().numpy(), w_all[0])
+    eager, eager_w, _ = buf.combine(y, handle, topk_weights=ex_w, bias=bias, apply_topk_weights=True)
+    torch.cuda.synchronize()
+    assert torch.equal(eager, out) and torch.equal(eager_w, out_w)
+
+
+# ----------------------------------------------------------------------------- stream ordering
+def _ordering_rank(rank, world, T, H, K, E, comm, drop_wait, results):
+    try:
+        torch.cuda.set_device(0)
+        from deepep_amd import ElasticBuffer
+        rng, idx_all, w_all = _routing(world, T, K, E, seed=31)
+        disp = oracle.simulate_dispatch(idx_all, E, T)
+        x_all, _ = _expanded_inputs(rng, disp, idx_all, w_all, T, H)
+        metas = [d['src_metadata'] for d in disp]
+        expect = oracle.combine_ep(x_all, metas, idx_all, E, T, expanded=True)[rank][0]
+        buf = ElasticBuffer(FakeGroup(rank, world, comm), num_max_tokens_per_rank=T, hidden=H, num_topk=K)
+        comm.install(buf, rank)
+        x = torch.zeros((T, H), dtype=torch.bfloat16, device='cuda')
+        _, _, _, handle, _ = buf.dispatch(x, topk_idx=torch.from_numpy(idx_all[rank]).cuda(), num_experts=E,
+                                          do_expand=True)
+        xin = _bf16(x_all[rank])
+        buf.combine(xin * 3, handle)                     # warm: plan cached, receive buffers of this size freed
+        torch.cuda.synchronize()
+        comm.bar.wait()
+        if drop_wait:                                   # a schedule that forgets to wait for the exchange
+            import tests.sim as sim
+            real = buf._a2a_async
+
+            def no_wait(out, inp, os_, is_):
+                work = real(out, inp, os_, is_)
+                return sim.Work(torch.cuda.Event())      # never recorded: waiting on it orders nothing
+            buf._a2a_async = no_wait
+        comm.delay_cycles = 20_000_000                  # the exchange lands ~10 ms after it is queued
+        out, _, _ = buf.combine(xin, handle)
+        torch.cuda.synchronize()
+        results[rank] = np.array_equal(_u16(out), expect)
+    except Exception:
+        import traceback
+        results[rank] = traceback.format_exc()
+        comm.bar.abort()
+
+
+def test_pipelined_schedule_is_ordered_by_its_stream_waits():
+    """EP = 4, 4 chunks, the exchange delayed on its own stream: the real schedule is bitwise right;
+    the same schedule with the exchange's wait dropped is caught (phase B reads receive rows that
+    have not landed)."""
+    T, H, K, E, world = 1024, 256, 8, 32, 4
+    for drop_wait in (False, True):
+        comm = ThreadComm(world)
+        results = run_threads(world, _ordering_rank, (world, T, H, K, E, comm, drop_wait))
+        assert len(results) == world and all(isinstance(v, bool) for v in results.values()), results
+        if drop_wait:
+            assert not all(results.values()), 'a schedule without the exchange wait went undetected'
+        else:
+            assert all(results.values()), results

@@ -179,6 +179,58 @@ def _worker(rank, world, port, seed, T, H, K, queue, empty_rank=-1, chunks=0):
                     failures.append('xgmi eager combine between graph replays')
         xb._sym.check()
         del graph
+        # An async combine (comm stream) followed at once by a sync-mode combine on the caller's stream
+        # with other inputs, no wait on the first call's event: both use the one window, so the second
+        # call's barrier must not pass before the first call's phase B has read it.
+        x2_all = [oracle.f32_to_bf16(oracle.bf16_to_f32(v) * 2) for v in x_exp_all]
+        expect2 = oracle.combine_ep(x2_all, [d['src_metadata'] for d in disp], idx_all, E, T, expanded=True,
+                                    topk_weights_per_rank=w_exp_all, bias_per_rank=[(b, None) for b in b_all])
+        g_in2 = _bf16(x2_all[rank], dev)
+        for it in range(2):
+            a_out, a_w, ev = xb.combine(g_in, handle, topk_weights=ex_w, bias=g_bias, async_with_compute_stream=True)
+            s_out, s_w, _ = xb.combine(g_in2, handle, topk_weights=ex_w, bias=g_bias)
+            ev.current_stream_wait()
+            torch.cuda.synchronize()
+            if not np.array_equal(_u16(a_out), expect[rank][0]):
+                failures.append(f'async xgmi combine overtaken by the next sync call ({it})')
+            if not np.array_equal(_u16(s_out), expect2[rank][0]):
+                failures.append(f'sync xgmi combine after an async one ({it})')
+        # A timed-out barrier poisons the launches behind it (bit 2 of the window's error flag): no
+        # partial reaches a peer and the output is NaN, not a silently wrong sum; the next call raises.
+        torch.cuda.synchronize()
+        xb._sym.error_flag.fill_(2)
+        p_out, _, _ = xb.combine(g_in, handle, topk_weights=ex_w, bias=g_bias)
+        torch.cuda.synchronize()
+        if not bool(torch.isnan(p_out.float()).all()):
+            failures.append('combine after a timed-out barrier is not poisoned')
+        xb._sym.error_flag.zero_()
+        try:
+            xb.combine(g_in, handle, topk_weights=ex_w, bias=g_bias)
+            failures.append('the call after a timed-out barrier did not raise')
+        except RuntimeError as e:
+            if 'did not arrive' not in str(e):
+                raise
+        out, _, _ = xb.combine(g_in, handle, topk_weights=ex_w, bias=g_bias)        # usable again
+        torch.cuda.synchronize()
+        if not np.array_equal(_u16(out), expect[rank][0]):
+            failures.append('xgmi combine after the poisoned call')
+        # The FIRST combine on a fresh handle captured into a HIP graph, no eager call before it: its
+        # plan (window row addresses included) is built by kernels inside the capture.
+        _, _, ex_w2, handle2, _ = xb.dispatch(x, topk_idx=torch.from_numpy(idx_all[rank]).to(dev),
+                                              topk_weights=torch.from_numpy(w_all[rank]).to(dev),
+                                              num_experts=E, do_expand=True)
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            f_out, f_w, _ = xb.combine(g_in, handle2, topk_weights=ex_w2, bias=g_bias)
+        for it in range(2):
+            f_out.zero_()
+            graph.replay()
+            torch.cuda.synchronize()
+            if not (np.array_equal(_u16(f_out), expect[rank][0]) and np.array_equal(f_w.cpu().numpy(), expect[rank][1])):
+                failures.append(f'first xgmi combine captured, replay {it}')
+        del graph
+        xb._sym.check()
         # gating-weighted variant: xGMI and RCCL paths agree bit for bit
         outs = {}
         for transport, b in bufs.items():

@@ -16,7 +16,7 @@ from tools.kbench import timeit  # noqa: E402
 def main():
     torch.cuda.set_device(0)
     from deepep_amd.kernels import HipKernels, MODE_EPILOGUE, MODE_LOCAL
-    from deepep_amd.handle import epilogue_tables
+    from tests.plan_ref import epilogue_tables
     kern = HipKernels()
     R, T, H, K, E = 8, 8192, 7168, 8, 256
     epr = E // R

@@ -23,7 +23,7 @@ def main():
     os.environ.setdefault('MASTER_PORT', '29617')
     dist.init_process_group('gloo', rank=0, world_size=1)
     from deepep_amd import ElasticBuffer
-    from deepep_amd.handle import epilogue_tables
+    from tests.plan_ref import epilogue_tables
     from deepep_amd.kernels import MODE_EPILOGUE, MODE_FUSED, MODE_LOCAL, RowLayout
     T, H, K, E, R = 8192, 7168, 8, 256, 8
     flush = torch.empty((512 << 20) // 4, dtype=torch.int32, device='cuda')

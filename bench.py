@@ -375,7 +375,7 @@ def main():
     dev = torch.device('cuda', torch.cuda.current_device())
     torch.manual_seed(0 + rank)
     if args.skew != 1.0:
-        from deepep_amd.utils import get_unbalanced_scores
+        from workloads import get_unbalanced_scores
         scores = get_unbalanced_scores(T, E, world, K, args.skew, device=dev)
     else:
         scores = torch.rand((T, E), device=dev)
@@ -384,7 +384,7 @@ def main():
     x = torch.randn((T, H), device=dev).to(torch.bfloat16)
     buf = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=T, hidden=H, num_topk=K)
     if args.fp8_dispatch:
-        from deepep_amd.utils import per_token_cast_to_fp8
+        from workloads import per_token_cast_to_fp8
         x = per_token_cast_to_fp8(x)
     ex_x, _, ex_w, handle, _ = buf.dispatch(x, topk_idx=topk_idx, topk_weights=topk_w, num_experts=E, do_expand=True)
     ex_shape = (ex_x[0] if isinstance(ex_x, tuple) else ex_x).shape
@@ -608,7 +608,7 @@ def main():
     n_disp = 50
     x_disp = torch.randn((T, H), device=dev).to(torch.bfloat16)
     if args.fp8_dispatch:
-        from deepep_amd.utils import per_token_cast_to_fp8
+        from workloads import per_token_cast_to_fp8
         x_disp = per_token_cast_to_fp8(x_disp)
 
     def time_dispatch(b):

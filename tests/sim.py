@@ -112,6 +112,8 @@ class FakeGroup:
 
 def run_threads(world: int, target, args=(), timeout: float = 300) -> dict:
     """Run target(rank, *args, results) on `world` threads; returns results {rank: failures}."""
+    torch.cuda.init()                                   # CUDA initialised here, not lazily by racing threads
+    torch.cuda.get_device_properties(0)
     results = {}
     threads = [threading.Thread(target=target, args=(r, *args, results)) for r in range(world)]
     for t in threads:

@@ -354,7 +354,7 @@ def test_config2_full_size_bitwise(weighted, T, skew):
     H, K, E = 7168, 8, 256
     g = torch.Generator(device='cuda').manual_seed(11)
     if skew != 1.0:
-        from deepep_amd.utils import get_unbalanced_scores
+        from workloads import get_unbalanced_scores
         torch.manual_seed(11)
         scores = get_unbalanced_scores(T, E, 8, K, skew, device='cuda')
     else:
@@ -467,7 +467,7 @@ def test_hip_graph_cached_dispatch_and_combine():
 
 def test_fp8_dispatch_then_bf16_combine():
     """BASELINE config 4 at EP=1: FP8 (e4m3, per-128 scales) dispatch, BF16 combine."""
-    from deepep_amd.utils import per_token_cast_back, per_token_cast_to_fp8
+    from workloads import per_token_cast_back, per_token_cast_to_fp8
     T, H, K, E = 256, 7168, 8, 64
     buf, idx, w, g = _ep1_setup(T, H, K, E, seed=4)
     x = torch.randn((T, H), device='cuda', generator=g).to(torch.bfloat16)

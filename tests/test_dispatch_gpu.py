@@ -106,7 +106,7 @@ def _run_dispatch(kern, dev, ranks, E, K, H, T_max, expanded, alignment, fp8, di
     (3, 6, 24, 257, 128, True, 4, False, 0.2, True),
 ])
 def test_dispatch_primitives_match_cpu(hip, R, K, E, T, H, expanded, alignment, fp8, masked, skew):
-    from deepep_amd.utils import per_token_cast_to_fp8
+    from workloads import per_token_cast_to_fp8
     gen = torch.Generator().manual_seed(R * 1000 + K)
     ranks = []
     for r in range(R):
@@ -141,7 +141,7 @@ def test_dispatch_primitives_match_cpu(hip, R, K, E, T, H, expanded, alignment, 
 ])
 def test_dispatch_direct_copy_one_rank(hip, K, E, T, H, expanded, fp8):
     """One rank: the metadata-only pack + direct copy gives the same handle and rows as the packed path."""
-    from deepep_amd.utils import per_token_cast_to_fp8
+    from workloads import per_token_cast_to_fp8
     gen = torch.Generator().manual_seed(K * 100 + T)
     idx, w = _routing(T, E, K, 1, 0.1, False, gen)
     x = torch.randn((T, H), generator=gen).to(torch.bfloat16)
@@ -167,7 +167,7 @@ def test_dispatch_modes_on_gpu(alignment, do_cpu_sync, do_handle_copy, fp8):
     import os
     import torch.distributed as dist
     from deepep_amd import ElasticBuffer
-    from deepep_amd.utils import per_token_cast_to_fp8
+    from workloads import per_token_cast_to_fp8
     from tests.helpers import dispatch_mode_checks
     if not dist.is_initialized():
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')

@@ -1,0 +1,149 @@
+"""BASELINE configs 3, 4 and 5 at full size: 8 EP ranks, each simulated by a thread on the one GPU
+(exchange with ProcessGroupNCCL's stream semantics, tests/sim.py), through ElasticBuffer's HIP
+dispatch and the pipelined (4-chunk) combine.
+
+  C3  8 x 8192 tokens, hidden 7168, top-8, 256 experts, uniform routing: plain + bias, and the
+      gating-weighted combine (apply_topk_weights)
+  C4  the same with the FP8 dispatch (per-128 e4m3 + fp32 scales) chained into the BF16 combine:
+      every expanded FP8 row is checked against its source token, the dequantised rows are the
+      expert outputs the combine reduces
+  C5  8 x 16384 tokens, skewed routing (get_unbalanced_scores, rank 0's experts ~4x the tokens)
+
+The reference's own test checks bitwise at 4096 tokens x 7168 x top-6 across 8 ranks
+(tests/elastic/test_ep.py:502-511, 577-580).  Here every rank's output is checked bitwise against
+the oracle (oracle.combine_ep, pinned to refs.combine) on a fixed subsample of 512 of its tokens
+with ALL of their partials (every expert rank's rows of those tokens), and the top-k weight
+pass-through is checked for every token.
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from tests.sim import FakeGroup, ThreadComm, run_threads
+
+pytestmark = pytest.mark.gpu
+
+SAMPLE = 512
+
+
+def _u16(t: torch.Tensor) -> np.ndarray:
+    return t.detach().cpu().contiguous().view(torch.int16).numpy().view(np.uint16)
+
+
+def _rank(rank, world, T, H, K, E, skew, fp8, weighted, comm, shared, results):
+    try:
+        torch.cuda.set_device(0)
+        from deepep_amd import ElasticBuffer
+        from workloads import get_unbalanced_scores, per_token_cast_back, per_token_cast_to_fp8
+        g = torch.Generator(device='cuda').manual_seed(4242 + rank)
+        if skew != 1.0:
+            with comm.lock:                                   # the bisection uses torch's global generator
+                torch.manual_seed(4242 + rank)
+                scores = get_unbalanced_scores(T, E, world, K, skew, device='cuda')
+        else:
+            scores = torch.rand((T, E), device='cuda', generator=g)
+        w, idx = torch.topk(scores, K, dim=-1, sorted=False)
+        idx = idx.to(torch.int64).contiguous()
+        w = w.contiguous()
+        x = torch.randn((T, H), device='cuda', generator=g).to(torch.bfloat16)
+        bias = torch.randn((T, H), device='cuda', generator=g).to(torch.bfloat16)
+        buf = ElasticBuffer(FakeGroup(rank, world, comm), num_max_tokens_per_rank=T, hidden=H, num_topk=K)
+        comm.install(buf, rank)
+        failures = []
+        if fp8:
+            xq = per_token_cast_to_fp8(x)
+            shared[('xq', rank)] = xq
+            (ex_q, ex_sf), _, ex_w, handle, _ = buf.dispatch(xq, topk_idx=idx, topk_weights=w, num_experts=E,
+                                                             do_expand=True)
+            comm.bar.wait()
+            # every expanded FP8 row (and its scales) is its source token's, bit for bit
+            q_all = torch.cat([shared[('xq', s)][0].view(torch.uint8) for s in range(world)])
+            sf_all = torch.cat([shared[('xq', s)][1] for s in range(world)])
+            meta = handle.recv_src_metadata
+            src = meta[:, 0].long()
+            for k in range(K):
+                rows = meta[:, 2 + k]
+                ok = rows >= 0
+                if not torch.equal(ex_q.view(torch.uint8)[rows[ok].long()], q_all[src[ok]]) or \
+                        not torch.equal(ex_sf[rows[ok].long()], sf_all[src[ok]]):
+                    failures.append(f'fp8 dispatch rows of lane {k}')
+            y = per_token_cast_back(ex_q, ex_sf)                  # the expert outputs
+        else:
+            _, _, ex_w, handle, _ = buf.dispatch(x, topk_idx=idx, topk_weights=w, num_experts=E, do_expand=True)
+            y = torch.randn((handle.num_expanded_tokens, H), device='cuda', generator=g).to(torch.bfloat16)
+        b = None if weighted or fp8 else bias
+        out, out_w, _ = buf.combine(y, handle, topk_weights=ex_w, bias=b, apply_topk_weights=weighted)
+        torch.cuda.synchronize()
+        if getattr(buf, '_stream_b', None) is None:          # made by the pipelined schedule only
+            failures.append('the combine did not take the pipelined schedule')
+        if not torch.equal(out_w, w):
+            failures.append('combined_topk_weights (all tokens)')
+        shared[rank] = dict(meta=handle.recv_src_metadata.cpu().numpy(), y=y, ex_w=ex_w, idx=idx.cpu().numpy(),
+                            out=out, bias=b)
+        comm.bar.wait()
+        # ---- the oracle on this rank's sampled tokens, with every expert rank's rows of them
+        S = np.sort(np.random.default_rng(99 + rank).choice(T, SAMPLE, replace=False))
+        pos = np.full(T, -1, np.int64)
+        pos[S] = np.arange(SAMPLE)
+        x_sub, m_sub, w_sub = [], [], []
+        for r in range(world):
+            m = shared[r]['meta']
+            sel = (m[:, 0] // T == rank) & (pos[m[:, 0] % T] >= 0)
+            mr = m[sel].copy()
+            slots = mr[:, 2:]
+            valid = slots >= 0
+            src_rows = torch.from_numpy(slots[valid].astype(np.int64)).cuda()
+            x_sub.append(_u16(shared[r]['y'][src_rows]) if src_rows.numel() else np.zeros((0, H), np.uint16))
+            w_sub.append(shared[r]['ex_w'][src_rows].cpu().numpy())
+            new = np.full(slots.shape, -1, np.int32)
+            new[valid] = np.arange(int(valid.sum()), dtype=np.int32)
+            mr[:, 2:] = new
+            mr[:, 0] = rank * SAMPLE + pos[mr[:, 0] % T]
+            m_sub.append(mr)
+        idx_sub = [shared[rank]['idx'][S] if s == rank else np.zeros((0, K), np.int64) for s in range(world)]
+        bias_sub = [(_u16(b[torch.from_numpy(S).cuda()]) if s == rank and b is not None else None, None)
+                    for s in range(world)]
+        exp, exp_w = oracle.combine_ep(x_sub, m_sub, idx_sub, E, SAMPLE, expanded=True, topk_weights_per_rank=w_sub,
+                                       bias_per_rank=bias_sub, weighted=weighted)[rank]
+        got = _u16(out[torch.from_numpy(S).cuda()])
+        if not np.array_equal(got, exp):
+            bad = np.argwhere(got != exp)
+            failures.append(f'combined_x differs on {len(bad)} elements of the sample, first {bad[:3].tolist()}')
+        if not np.array_equal(exp_w, w.cpu().numpy()[S]):
+            failures.append('oracle weights of the sample')
+        comm.bar.wait()
+        results[rank] = failures
+    except Exception:
+        import traceback
+        results[rank] = [traceback.format_exc()]
+        comm.bar.abort()
+
+
+def _run(T, skew=1.0, fp8=False, weighted=False):
+    import threading
+    world, H, K, E = 8, 7168, 8, 256
+    torch.cuda.init()                                   # not lazily from 8 threads at once
+    torch.cuda.get_device_properties(0)
+    comm = ThreadComm(world)
+    comm.lock = threading.Lock()
+    shared = {}
+    results = run_threads(world, _rank, (world, T, H, K, E, skew, fp8, weighted, comm, shared), timeout=600)
+    del shared
+    torch.cuda.empty_cache()
+    assert len(results) == world, results
+    bad = {r: f for r, f in results.items() if f}
+    assert not bad, bad
+
+
+@pytest.mark.parametrize('weighted', [False, True], ids=['plain_bias', 'gating_weighted'])
+def test_config3_ep8_8192_tokens(weighted):
+    _run(8192, weighted=weighted)
+
+
+def test_config4_ep8_fp8_dispatch_bf16_combine():
+    _run(8192, fp8=True)
+
+
+def test_config5_ep8_16384_tokens_skewed():
+    _run(16384, skew=4.0)

@@ -50,7 +50,20 @@ def _init_dist(n_gpus: int):
 
 
 def _cpu_threads() -> int:
+    """Host threads for the CPU baseline: the GPU box's CPU share per GPU (16; os.cpu_count() there
+    reports the whole machine's CPUs, many times as many -- both are in the line)."""
     return max(1, min(16, int(os.environ.get('OMP_NUM_THREADS', '16')), os.cpu_count() or 1))
+
+
+def _cpu_model() -> str:
+    try:
+        with open('/proc/cpuinfo') as f:
+            for line in f:
+                if line.startswith('model name'):
+                    return line.split(':', 1)[1].strip()
+    except OSError:
+        pass
+    return 'unknown'
 
 
 def _cpu_baseline(y: torch.Tensor, table: torch.Tensor, w: torch.Tensor, weighted: bool, min_seconds: float):
@@ -91,6 +104,7 @@ def _cpu_baseline(y: torch.Tensor, table: torch.Tensor, w: torch.Tensor, weighte
             if el >= min_seconds:
                 break
     return dict(value=round(bytes_per * reps / el / 1e9, 3), unit='GB/s', cores=n_thr, kind='port',
+                cpu_model=_cpu_model(), os_cpu_count=os.cpu_count(),
                 sample=f'{reps} full pass(es) of the bench batch ({T} tokens x top-{K} x hidden {H}, host copy) '
                        f'through oracle_combine_rows (C restatement, fused {"weighted" if weighted else "plain"}), '
                        f'{n_thr} threads, {el:.1f} s')
@@ -336,16 +350,24 @@ def _bench_single(y, handle, ex_w, weighted, total_bytes, steps, warmup, dev, re
     return res
 
 
-def _pmc_traffic(workload: str):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_traffic.py), if any."""
+def _pmc_traffic(workload: str, build_id: str):
+    """HBM bytes per launch of the dominant kernel from the rocprofv3 PMC passes in
+    profiles/pmc_traffic.json (tools/gpu_session.sh `pmc` step -> tools/summarize_prof.py), accepted
+    only when they were collected with THIS library build (same build id: sources, header, flags);
+    otherwise None and the reason.  Returns (bytes or None, build id of the counters, note)."""
     path = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
     try:
         with open(path) as f:
-            data = json.load(f)
-        entry = data.get(workload)
-        return None if entry is None else float(entry['hbm_bytes_per_launch'])
-    except (OSError, ValueError, KeyError):
-        return None
+            entry = json.load(f).get(workload)
+    except (OSError, ValueError):
+        entry = None
+    if entry is None or 'hbm_bytes_per_launch' not in entry:
+        return None, None, f'no PMC pass for {workload} in profiles/pmc_traffic.json'
+    if entry.get('build_id') != build_id:
+        return None, entry.get('build_id'), (f'PMC pass collected with build {entry.get("build_id")}, this is '
+                                             f'{build_id}: stale, not reported')
+    return float(entry['hbm_bytes_per_launch']), build_id, ('2 x FETCH_SIZE + WRITE_SIZE (KiB x 1024), '
+                                                             'MI355X_MICROARCH.md gfx950 corrections, same build')
 
 
 def main():
@@ -537,8 +559,11 @@ def main():
                              'the K unreduced rows per token in a [K, T] receive window), same algorithmic bytes')
         del win, win_w
         workload = f'combine_fused_{"weighted" if weighted else "plain"}_t{T}_h{H}_k{K}'
+        build_id = kern.lib.deepep_amd_build_id().decode()
+        traffic, traffic_build, traffic_note = _pmc_traffic(workload, build_id)
         roofline = dict(bound='hbm', achieved=round(achieved, 1), peak=HBM_PEAK_GBPS, unit='GB/s',
-                        frac=round(achieved / HBM_PEAK_GBPS, 4), traffic=_pmc_traffic(workload),
+                        frac=round(achieved / HBM_PEAK_GBPS, 4), traffic=traffic, traffic_build_id=traffic_build,
+                        traffic_note=traffic_note, build_id=build_id,
                         kernel=('combine_rows_kernel<FUSED>', 'combine_stream_kernel<FUSED, 2 vectors/lane>',
                                 'combine_stream_kernel<FUSED, 1 vector/lane>',
                                 'combine_stream_kernel<FUSED, persistent grid>',
@@ -550,7 +575,7 @@ def main():
                         bytes_per_launch=bytes_rank, in_region_us_per_step=round(comm_ms * 1e3, 2),
                         same_run_d2d_copy_gbps=round(copy_gbps, 1), single_reduction_phase_b=single_b)
 
-    phases = None
+    phases = su_line = None
     if world > 1:
         # Per-phase device time of the EP > 1 combine (phase A | exchange | phase B), same step
         buf._phase_events = []
@@ -584,6 +609,19 @@ def main():
         dist.all_reduce(vals, op=dist.ReduceOp.MAX)
         xb = torch.tensor([float(x_bytes)], dtype=torch.float64, device=dev)
         dist.all_reduce(xb)
+        # The reference's "SU" combine bandwidth (tests/elastic/test_ep.py:287-346, the BASELINE.md
+        # figure): num_scaleup_recv_tokens x (H * 2 + K * 4) bytes / combine time, per rank, local
+        # tokens included (ignore_local_traffic off); the bottleneck (slowest) rank is reported.
+        su_bytes = n_recv * (H * 2 + K * 4)
+        su = torch.tensor([su_bytes / (ms_per_step * 1e-3) / 1e9, su_bytes / ((t_a + t_x) * 1e-3) / 1e9],
+                          dtype=torch.float64, device=dev)
+        dist.all_reduce(su, op=dist.ReduceOp.MIN)
+        su_line = dict(gbps_per_rank=round(float(su[0]), 1), gbps_per_rank_phase_a_exchange=round(float(su[1]), 1),
+                       bytes_rank0=su_bytes,
+                       note='reference definition: received tokens x (2H + 4K) / t; gbps_per_rank uses the whole '
+                            'pipelined combine step (RCCL transport, the main loop), gbps_per_rank_phase_a_exchange '
+                            'the unpipelined phase A + exchange (the analogue of combine_impl, which the reference '
+                            'times); min over ranks')
         phases = dict(phase_a_ms=round(float(vals[2]), 4), exchange_ms=round(float(vals[1]), 4),
                       phase_b_ms=round(float(vals[3]), 4),
                       reduce_only_gbps=round(total_bytes / (float(vals[0]) * 1e-3) / 1e9, 1),
@@ -709,7 +747,7 @@ def main():
                        'tokens_per_rank': T, 'hidden': H, 'topk': K, 'experts': E, 'accumulate': 'fp32',
                        'parallelism': f'ep{world}', 'transport': transport},
             'roofline': roofline, 'cpu_baseline': cpu_baseline, 'cpu_torch': cpu_torch, 'loopback': loopback,
-            'phases': phases, 'rccl': rccl, 'xgmi': xgmi, 'single_reduction': single,
+            'phases': phases, 'su_bandwidth': su_line, 'rccl': rccl, 'xgmi': xgmi, 'single_reduction': single,
             'dispatch': dispatch,
         }
         print(json.dumps(line), flush=True)

@@ -67,7 +67,7 @@ SIGNATURES = {
                                    _I, _I,
                                    _P, _I64,
                                    _P, _P, _I,
-                                   _I64,
+                                   _I64, _I,
                                    _I, _P,
                                    _P]),
     'deepep_build_local_plan': (_I, [_P, _I, _I, _I, _I, _P, _I, _I, _P, _P, _P]),
@@ -98,7 +98,7 @@ SIGNATURES = {
     'deepep_stream_create_cu_budget': (_I, [_I, ctypes.POINTER(ctypes.c_void_p)]),
     'deepep_stream_destroy': (_I, [_P]),
     'deepep_combine_reduce_scatter': (_I, [_I, _P, _I64, _I64, _P, _I64, _I, _P, _P, _I, _I, _P, _I64, _P, _I,
-                                           _I64, _P, _P]),
+                                           _I64, _I, _P, _P]),
 }
 
 

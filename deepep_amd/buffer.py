@@ -161,7 +161,7 @@ class ElasticBuffer(ExchangeMixin):
         # no collective set-up (a window too small for a later call is re-allocated there).
         if self.transport == 'xgmi' and self.num_ranks > 1 and self.use_cuda and \
                 int(os.environ.get('DEEPEP_EAGER_WINDOW', 1)) and not hasattr(group, 'comm'):
-            self._window(1, slots=1, rows_per_slot=1)
+            self._window(self._window_bytes(hidden, num_topk, num_max_tokens_per_rank), slots=1, rows_per_slot=1)
 
     def _group_barrier(self) -> None:
         """torch.cuda.synchronize(); group barrier; synchronize (elastic.py:365-367)."""
@@ -173,6 +173,22 @@ class ElasticBuffer(ExchangeMixin):
             self.group.barrier()
         if self.use_cuda:
             torch.cuda.synchronize()
+
+    def _window_bytes(self, hidden: int, num_topk: int, num_max_tokens: int) -> int:
+        """Bytes the xGMI window needs for calls of the declared shape (this build's line-aligned
+        packed rows: handle.packed_row_layout, kernels.RowLayout), so a first dispatch or combine of
+        that shape never re-allocates it (a collective with a host sync); 0 when the shape is not
+        declared (num_bytes then sizes the window)."""
+        if hidden <= 0 or num_max_tokens <= 0:
+            return 0
+        from .handle import packed_row_layout
+        K = num_topk or 32
+        R = self.num_ranks
+        slots, single = (min(R, K), False) if self.allow_multiple_reduction else (K, True)
+        combine = slots * num_max_tokens * packed_row_layout(hidden, K, True, single)[0]
+        dispatch = R * num_max_tokens * max(RowLayout.make(hidden * 2, 0, K).row_bytes,
+                                            RowLayout.make(hidden, ceil_div(hidden, 128) * 4, K).row_bytes)
+        return max(combine, dispatch)
 
     # ------------------------------------------------------------------ infrastructure
     @property
@@ -679,6 +695,8 @@ class ElasticBuffer(ExchangeMixin):
         _assert(num_qps <= self.num_allocated_qps, 'Allocated QPs are not enough')
         bias_0, bias_1 = self._unpack_bias(bias)
         budget = self._cu_budget_stream(explicit_sms)
+        if budget is not None and self.use_cuda and torch.cuda.current_stream() == budget:
+            budget = None     # the caller already runs on the budget stream: no stream hops needed
         if budget is None:
             return self._combine(x, topk_weights, bias_0, bias_1, handle, num_sms, previous_event,
                                  previous_event_before_epilogue, async_with_compute_stream,
@@ -701,6 +719,12 @@ class ElasticBuffer(ExchangeMixin):
             self.comm_stream = saved
             if not capturing:
                 saved.wait_stream(budget)
+
+    def get_cu_budget_stream(self, num_sms: int) -> Optional[torch.cuda.Stream]:
+        """The stream restricted to `num_sms` CUs (rounded up to whole CUs per XCD) that an explicit
+        `combine(..., num_sms=num_sms)` runs on; None for the whole chip.  A caller that issues the
+        combine from this stream (torch.cuda.stream(...)) skips the two cross-stream hops."""
+        return self._cu_budget_stream(num_sms)
 
     def _cu_budget_stream(self, num_sms: int):
         """The CU-budget stream for an explicit num_sms (None when 0 or at least the CU count).

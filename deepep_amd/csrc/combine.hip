@@ -25,6 +25,8 @@
 #include <stdarg.h>
 
 #include <algorithm>
+#include <map>
+#include <mutex>
 
 #include "../../include/deepep_amd.h"
 
@@ -90,12 +92,14 @@ struct Params {
     const float* wsrc;
     float* out_weights;
     int num_weights;
+    int weights_pad;             // floats written per unit's weight row (>= num_weights; zeros past them)
     int64_t out_weights_stride;  // floats between consecutive units' weight rows
     int units_per_block;
     int32_t* error_flag;
     const uint64_t* out_rows;    // scatter (phase A over xGMI): byte address of unit u's output row, or NULL
     int64_t weights_offset;      // scatter: byte offset of the weights inside the output row
     int xcd_blocks;              // item kernel: 1 = XCD-contiguous workgroup order (see xcd_block)
+    int cap_cus;                 // > 0: persistent grid, at most the workgroups this many CUs hold at once
 };
 
 // Workgroups are dealt round-robin to the 8 XCDs (workgroup b runs on XCD b % 8).  With
@@ -148,59 +152,13 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void* row, int 
 }
 
 // One wave per item = (unit u, column chunk c): the chunk is 64 lanes x kVPT x 16 B of every
-// source row of u.  A workgroup of kWaves waves takes kWaves consecutive items.  The unit's slot table row
-// (and its gating weights) is staged once per workgroup in LDS (kLDS) or per wave in registers,
-// one entry per lane; the valid slots are then visited in ascending order through the ballot mask,
+// source row of u.  The unit's slot table row (and its gating weights) arrive in my_slot / my_w, one
+// entry per lane; the valid slots are then visited in ascending order through the ballot mask,
 // which is exactly the compacted order of compute_topk_slots (combine_utils.cuh:41-53).
-template <int kMode, bool kWeighted, int kVPT, bool kFull, int kStoreAux, bool kLDS, int kWaves = 4, int kGroup = 8>
-__global__ void __launch_bounds__(64 * kWaves)
-combine_rows_kernel(const Params p) {
+template <int kMode, bool kWeighted, int kVPT, bool kFull, int kStoreAux, int kGroup>
+__device__ __forceinline__ void combine_item(const Params& p, int64_t it, int nchunks, int nvec, int lane,
+                                             int32_t my_slot, float my_w) {
     constexpr int kChunkVecs = 64 * kVPT;
-    const int tid = static_cast<int>(threadIdx.x), lane = tid & 63, wave = tid >> 6;
-    const int nvec = p.hidden >> 3;                          // 16-byte vectors per row
-    const int nchunks = (nvec + kChunkVecs - 1) / kChunkVecs;
-    const int64_t items = static_cast<int64_t>(p.num_units) * nchunks;
-    const int64_t blk = p.xcd_blocks ? xcd_block(blockIdx.x, gridDim.x) : static_cast<int64_t>(blockIdx.x);
-    const int64_t it0 = blk * kWaves;
-    const int64_t it = it0 + wave;
-    const int width = p.table == nullptr ? 1 : p.table_width;
-
-    auto load_slot = [&](int64_t u, int j) -> int32_t {
-        int32_t s = p.table == nullptr ? static_cast<int32_t>(u) : p.table[u * p.table_stride + j];
-        if (s >= p.num_src_rows) {                           // never dereference a bad slot
-            if (p.error_flag != nullptr) atomicOr(p.error_flag, 1);
-            s = -1;
-        }
-        return s;
-    };
-
-    int32_t my_slot = -1;
-    float my_w = 0.0f;
-    if constexpr (kLDS) {
-        __shared__ int32_t s_slot[kWaves][kMaxWidth];
-        __shared__ float s_w[kWaves][kMaxWidth];
-        const int64_t u_first = it0 / nchunks;
-        const int nu = static_cast<int>(min(it0 + kWaves - 1, items - 1) / nchunks - u_first) + 1;
-        if (tid < nu * width) {                             // nu * width <= kWaves * 32 threads
-            const int ul = tid / width, j = tid - ul * width;
-            const int32_t s = load_slot(u_first + ul, j);
-            s_slot[ul][j] = s;
-            if constexpr (kWeighted) s_w[ul][j] = s >= 0 ? p.row_weights[s] : 0.0f;
-        }
-        __syncthreads();
-        if (it >= items) return;
-        const int ul = static_cast<int>(it / nchunks - u_first);
-        if (lane < width) {
-            my_slot = s_slot[ul][lane];
-            if constexpr (kWeighted) my_w = s_w[ul][lane];
-        }
-    } else {
-        if (it >= items) return;
-        if (lane < width) {
-            my_slot = load_slot(it / nchunks, lane);
-            if constexpr (kWeighted) my_w = my_slot >= 0 ? p.row_weights[my_slot] : 0.0f;
-        }
-    }
     const int64_t u = it / nchunks;
     const int c = static_cast<int>(it - u * nchunks);
     // A barrier of this window timed out (bit 2 of the error flag, set by deepep_sym_barrier /
@@ -217,9 +175,12 @@ combine_rows_kernel(const Params p) {
     //      written once per unit by the wave owning chunk 0
     uint16_t* const out_row = p.out_rows != nullptr ? reinterpret_cast<uint16_t*>(p.out_rows[u])
                                                      : p.out + u * p.out_stride;
-    if (c == 0 && p.num_weights > 0 && lane < p.num_weights) {
-        const int64_t i = p.wtable == nullptr ? u * p.num_weights + lane
-                                              : static_cast<int64_t>(p.wtable[u * p.wtable_stride + lane]);
+    if (c == 0 && p.num_weights > 0 && lane < p.weights_pad) {
+        // weights_pad > num_weights: a packed row's whole 128-byte tail line is written (zeros past the
+        // weights), so the memory side never merges a partial line
+        const int64_t i = lane >= p.num_weights ? -1
+                          : p.wtable == nullptr ? u * p.num_weights + lane
+                                                : static_cast<int64_t>(p.wtable[u * p.wtable_stride + lane]);
         float* const ow = p.out_rows != nullptr
                               ? reinterpret_cast<float*>(reinterpret_cast<char*>(out_row) + p.weights_offset)
                               : p.out_weights + u * p.out_weights_stride;
@@ -340,6 +301,72 @@ combine_rows_kernel(const Params p) {
         __builtin_amdgcn_raw_buffer_store_b128(result[v], orow, vidx[v] * 16, 0, kStoreAux);
 }
 
+// A workgroup of kWaves waves takes kWaves consecutive items (a virtual block); the unit's slot table
+// row (and its gating weights) is staged once per workgroup in LDS (kLDS) or per wave in registers.
+// The grid is one workgroup per virtual block, or -- on a CU-budget stream, or when forced -- capped
+// at the workgroups the (budgeted) CUs hold at once, each walking virtual blocks grid-stride
+// (p.persistent): the waves then stay resident instead of a launch per 2 KiB item.
+template <int kMode, bool kWeighted, int kVPT, bool kFull, int kStoreAux, bool kLDS, int kWaves = 4, int kGroup = 8,
+          bool kPersistent = false>
+__global__ void __launch_bounds__(64 * kWaves)
+combine_rows_kernel(const Params p) {
+    constexpr int kChunkVecs = 64 * kVPT;
+    __shared__ int32_t s_slot[kWaves][kMaxWidth];
+    __shared__ float s_w[kWaves][kMaxWidth];
+    const int tid = static_cast<int>(threadIdx.x), lane = tid & 63, wave = tid >> 6;
+    const int nvec = p.hidden >> 3;                          // 16-byte vectors per row
+    const int nchunks = (nvec + kChunkVecs - 1) / kChunkVecs;
+    const int64_t items = static_cast<int64_t>(p.num_units) * nchunks;
+    const int64_t nblocks = (items + kWaves - 1) / kWaves;
+    const int width = p.table == nullptr ? 1 : p.table_width;
+
+    auto load_slot = [&](int64_t u, int j) -> int32_t {
+        int32_t s = p.table == nullptr ? static_cast<int32_t>(u) : p.table[u * p.table_stride + j];
+        if (s >= p.num_src_rows) {                           // never dereference a bad slot
+            if (p.error_flag != nullptr) atomicOr(p.error_flag, 1);
+            s = -1;
+        }
+        return s;
+    };
+
+    auto block = [&](int64_t vb) {
+        const int64_t blk = p.xcd_blocks ? xcd_block(vb, nblocks) : vb;
+        const int64_t it0 = blk * kWaves;
+        const int64_t it = it0 + wave;
+        int32_t my_slot = -1;
+        float my_w = 0.0f;
+        if constexpr (kLDS) {
+            if (vb != blockIdx.x) __syncthreads();          // the previous block's waves read s_slot
+            const int64_t u_first = it0 / nchunks;
+            const int nu = static_cast<int>(min(it0 + kWaves - 1, items - 1) / nchunks - u_first) + 1;
+            if (tid < nu * width) {                         // nu * width <= kWaves * 32 threads
+                const int ul = tid / width, j = tid - ul * width;
+                const int32_t s = load_slot(u_first + ul, j);
+                s_slot[ul][j] = s;
+                if constexpr (kWeighted) s_w[ul][j] = s >= 0 ? p.row_weights[s] : 0.0f;
+            }
+            __syncthreads();
+            if (it < items && lane < width) {
+                const int ul = static_cast<int>(it / nchunks - u_first);
+                my_slot = s_slot[ul][lane];
+                if constexpr (kWeighted) my_w = s_w[ul][lane];
+            }
+        } else {
+            if (it < items && lane < width) {
+                my_slot = load_slot(it / nchunks, lane);
+                if constexpr (kWeighted) my_w = my_slot >= 0 ? p.row_weights[my_slot] : 0.0f;
+            }
+        }
+        if (it < items)
+            combine_item<kMode, kWeighted, kVPT, kFull, kStoreAux, kGroup>(p, it, nchunks, nvec, lane, my_slot, my_w);
+    };
+    if constexpr (kPersistent) {
+        for (int64_t vb = blockIdx.x; vb < nblocks; vb += gridDim.x) block(vb);
+    } else {
+        block(blockIdx.x);                          // one virtual block per workgroup
+    }
+}
+
 // Streaming variant: one wave owns a whole unit (all of its column chunks), for slot tables of at
 // most kStreamWidth entries and hidden sizes that are a whole number of chunks.  The unit's slots,
 // weights and weight pass-through are handled once; then the chunks are walked in order with the
@@ -380,9 +407,10 @@ combine_stream_kernel(const Params p) {
 
     uint16_t* const out_row = p.out_rows != nullptr ? reinterpret_cast<uint16_t*>(p.out_rows[u])
                                                      : p.out + u * p.out_stride;
-    if (p.num_weights > 0 && lane < p.num_weights) {           // top-k weight pass-through, once per unit
-        const int64_t i = p.wtable == nullptr ? u * p.num_weights + lane
-                                              : static_cast<int64_t>(p.wtable[u * p.wtable_stride + lane]);
+    if (p.num_weights > 0 && lane < p.weights_pad) {           // top-k weight pass-through, once per unit
+        const int64_t i = lane >= p.num_weights ? -1
+                          : p.wtable == nullptr ? u * p.num_weights + lane
+                                                : static_cast<int64_t>(p.wtable[u * p.wtable_stride + lane]);
         float* const ow = p.out_rows != nullptr
                               ? reinterpret_cast<float*>(reinterpret_cast<char*>(out_row) + p.weights_offset)
                               : p.out_weights + u * p.out_weights_stride;
@@ -475,24 +503,41 @@ combine_stream_kernel(const Params p) {
     }
 }
 
+int device_cus() {
+    static int cus = 0;
+    if (cus == 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                    hipSuccess)
+            cus = 256;
+    }
+    return cus;
+}
+
+// CU-budget streams created by deepep_stream_create_cu_budget (symmetric.hip) and their CU counts:
+// a launch on one takes a persistent grid sized to the budget.
+std::mutex g_budget_mutex;
+std::map<hipStream_t, int> g_budget_cus;
+
+int budget_cus_of(hipStream_t s) {
+    if (s == nullptr) return 0;
+    std::lock_guard<std::mutex> lock(g_budget_mutex);
+    const auto it = g_budget_cus.find(s);
+    return it == g_budget_cus.end() ? 0 : it->second;
+}
+
 // persistent: the grid is capped at the workgroups the chip holds at once (occupancy x CUs), so
 // there is no partial last round of long-lived waves; otherwise one unit per wave
 template <int kMode, bool kWeighted, int kVPT, int kAux>
 void launch_stream_policy(const Params& p, bool persistent, hipStream_t stream) {
     const auto kernel = combine_stream_kernel<kMode, kWeighted, kVPT, kAux>;
     int64_t blocks = (p.num_units + 3) / 4;
-    if (persistent) {
-        static int cap = 0;                       // per template instance
-        if (cap == 0) {
-            int per_cu = 0, dev = 0, cus = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) == hipSuccess &&
-                hipGetDevice(&dev) == hipSuccess &&
-                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
-                cap = std::max(1, per_cu * cus);
-            else
-                cap = 1 << 30;
-        }
-        blocks = std::min<int64_t>(blocks, cap);
+    if (persistent || p.cap_cus > 0) {
+        static int per_cu = 0;                    // per template instance
+        if (per_cu == 0 && hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess)
+            per_cu = 1;
+        blocks = std::min<int64_t>(blocks, std::max(1, per_cu) * static_cast<int64_t>(p.cap_cus > 0 ? p.cap_cus
+                                                                                                    : device_cus()));
     }
     hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream, p);
 }
@@ -523,9 +568,21 @@ int g_last_choice = 0;
 
 template <int kMode, bool kWeighted, int kVPT, bool kFull, int kAux, bool kLDS, int kWaves, int kGroup>
 void launch_shape(const Params& p, int64_t items, hipStream_t stream) {
-    const dim3 grid(static_cast<unsigned>((items + kWaves - 1) / kWaves)), block(64 * kWaves);
-    hipLaunchKernelGGL((combine_rows_kernel<kMode, kWeighted, kVPT, kFull, kAux, kLDS, kWaves, kGroup>), grid, block,
-                       0, stream, p);
+    const int64_t blocks = (items + kWaves - 1) / kWaves;
+    if constexpr (kGroup == 8) {
+        if (p.cap_cus > 0) {                      // persistent: what the (budgeted) CUs hold at once
+            const auto kernel = combine_rows_kernel<kMode, kWeighted, kVPT, kFull, kAux, kLDS, kWaves, kGroup, true>;
+            static int per_cu = 0;                // per template instance
+            if (per_cu == 0 &&
+                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 64 * kWaves, 0) != hipSuccess)
+                per_cu = 1;
+            const int64_t grid = std::min<int64_t>(blocks, static_cast<int64_t>(std::max(1, per_cu)) * p.cap_cus);
+            hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>(grid)), dim3(64 * kWaves), 0, stream, p);
+            return;
+        }
+    }
+    hipLaunchKernelGGL((combine_rows_kernel<kMode, kWeighted, kVPT, kFull, kAux, kLDS, kWaves, kGroup, false>),
+                       dim3(static_cast<unsigned>(blocks)), dim3(64 * kWaves), 0, stream, p);
 }
 
 // Workgroup shape and rows in flight.  The fused / epilogue reduces (8 rows per token at EP = 1):
@@ -619,6 +676,13 @@ __attribute__((visibility("hidden"))) int deepep_amd_set_error(int code, const c
     return set_error(code, "%s", msg);
 }
 
+// Budget streams (shared with symmetric.hip; not part of the public C-ABI): cus <= 0 forgets one.
+__attribute__((visibility("hidden"))) void deepep_amd_register_budget(void* stream, int cus) {
+    std::lock_guard<std::mutex> lock(g_budget_mutex);
+    if (cus > 0) g_budget_cus[static_cast<hipStream_t>(stream)] = cus;
+    else g_budget_cus.erase(static_cast<hipStream_t>(stream));
+}
+
 int deepep_amd_abi_version(void) { return DEEPEP_AMD_ABI_VERSION; }
 
 #ifndef DEEPEP_BUILD_ID
@@ -640,7 +704,7 @@ int deepep_combine_reduce(int mode, int weighted,
                           int num_units, int hidden,
                           const int32_t* wtable, int64_t wtable_stride,
                           const float* wsrc, float* out_weights, int num_weights,
-                          int64_t out_weights_stride,
+                          int64_t out_weights_stride, int weights_pad,
                           int units_per_block, int32_t* error_flag,
                           deepep_stream_t stream) {
     if (mode < DEEPEP_MODE_LOCAL || mode > DEEPEP_MODE_FUSED)
@@ -665,9 +729,10 @@ int deepep_combine_reduce(int mode, int weighted,
     if (out_weights != nullptr && (wsrc == nullptr || num_weights < 1 || num_weights > kMaxWidth))
         return set_error(DEEPEP_ERR_INVALID_ARG, "weight pass-through needs wsrc and 1 <= num_weights <= %d", kMaxWidth);
     if (out_weights_stride == 0) out_weights_stride = num_weights;
-    if (out_weights != nullptr && out_weights_stride < num_weights)
-        return set_error(DEEPEP_ERR_INVALID_ARG, "out_weights_stride (%lld) < num_weights (%d)",
-                         static_cast<long long>(out_weights_stride), num_weights);
+    if (weights_pad < num_weights) weights_pad = num_weights;
+    if (out_weights != nullptr && (out_weights_stride < weights_pad || weights_pad > 64))
+        return set_error(DEEPEP_ERR_INVALID_ARG, "out_weights_stride (%lld) < weights_pad (%d) or weights_pad > 64",
+                         static_cast<long long>(out_weights_stride), weights_pad);
     Params p;
     p.src = static_cast<const uint16_t*>(src);
     p.num_src_rows = num_src_rows;
@@ -687,12 +752,14 @@ int deepep_combine_reduce(int mode, int weighted,
     p.wsrc = wsrc;
     p.out_weights = out_weights;
     p.num_weights = out_weights != nullptr ? num_weights : 0;
+    p.weights_pad = weights_pad;
     p.out_weights_stride = out_weights_stride;
     p.units_per_block = units_per_block;
     p.error_flag = error_flag;
     p.out_rows = nullptr;
     p.weights_offset = 0;
     p.xcd_blocks = 0;
+    p.cap_cus = 0;
 
     return launch_combine(mode, weighted, p, stream);
 }
@@ -703,7 +770,7 @@ int deepep_combine_reduce_scatter(int weighted,
                                   const float* row_weights,
                                   const uint64_t* out_rows, int num_units, int hidden,
                                   const int32_t* wtable, int64_t wtable_stride,
-                                  const float* wsrc, int num_weights, int64_t weights_offset,
+                                  const float* wsrc, int num_weights, int64_t weights_offset, int weights_pad,
                                   int32_t* error_flag, deepep_stream_t stream) {
     if (num_units < 0 || hidden < 0)
         return set_error(DEEPEP_ERR_INVALID_ARG, "negative size (num_units=%d, hidden=%d)", num_units, hidden);
@@ -721,6 +788,8 @@ int deepep_combine_reduce_scatter(int weighted,
     if (num_weights > 0 && (wsrc == nullptr || num_weights > kMaxWidth || weights_offset < int64_t(hidden) * 2 ||
                             weights_offset % 4 != 0))
         return set_error(DEEPEP_ERR_INVALID_ARG, "weights need wsrc, num_weights <= %d and an offset past the row", kMaxWidth);
+    if (weights_pad < num_weights) weights_pad = num_weights;
+    if (weights_pad > 64) return set_error(DEEPEP_ERR_INVALID_ARG, "weights_pad > 64");
     Params p;
     p.src = static_cast<const uint16_t*>(src);
     p.num_src_rows = num_src_rows;
@@ -740,12 +809,14 @@ int deepep_combine_reduce_scatter(int weighted,
     p.wsrc = wsrc;
     p.out_weights = nullptr;
     p.num_weights = num_weights > 0 ? num_weights : 0;
+    p.weights_pad = weights_pad;
     p.out_weights_stride = 0;
     p.units_per_block = 0;
     p.error_flag = error_flag;
     p.out_rows = out_rows;
     p.weights_offset = weights_offset;
     p.xcd_blocks = 0;
+    p.cap_cus = 0;
     return launch_combine(DEEPEP_MODE_LOCAL, weighted, p, stream);
 }
 
@@ -803,12 +874,20 @@ int launch_combine(int mode, int weighted, const Params& p_in, deepep_stream_t s
     // 4: the item kernel with XCD-contiguous workgroup order -- it lost
     // on every measurement (config 2 188.4 vs 175.3 us, EP = 8 phase A 318 vs 301, phase B 126 vs
     // 115): neighbouring items spread over all XCDs stream better
+    // 5: the item kernel on a persistent grid (as many workgroups as the chip holds at once)
+    // On a CU-budget stream every candidate takes a persistent grid sized to the budget.
+    const int budget = budget_cus_of(s);
     auto launch_choice = [&](int c) {
         p.xcd_blocks = c == 4 ? 1 : 0;
-        if (c == 0 || c == 4) launch_items();
+        p.cap_cus = budget > 0 ? budget : (c == 5 ? device_cus() : 0);
+        // a persistent grid stages slots per wave (no workgroup barrier between a wave's items), so
+        // each wave streams at its own pace
+        sh.lds = g_config.stage_lds >= 0 ? g_config.stage_lds != 0 : p.cap_cus == 0;
+        if (c == 0 || c == 4 || c == 5) launch_items();
         else launch_streaming(c == 2 ? 1 : sh.vpt, c == 3);
     };
-    const int choice = (stream_ok && g_kernel_choice >= 0) ? g_kernel_choice : 0;
+    const int forced = g_kernel_choice;
+    const int choice = forced == 5 ? 5 : ((stream_ok && forced >= 0) ? forced : 0);
     g_last_choice = choice;
     launch_choice(choice);
     const hipError_t err = hipGetLastError();
@@ -855,7 +934,7 @@ int deepep_build_local_plan(const int32_t* src_metadata, int num_recv_tokens, in
 }
 
 int deepep_set_kernel_choice(int choice) {
-    if (choice < -1 || choice > 4) return set_error(DEEPEP_ERR_INVALID_ARG, "kernel choice must be -1 or 0..4");
+    if (choice < -1 || choice > 5) return set_error(DEEPEP_ERR_INVALID_ARG, "kernel choice must be -1 or 0..5");
     g_kernel_choice = choice;
     return DEEPEP_OK;
 }

@@ -24,6 +24,7 @@
 #include "../../include/deepep_amd.h"
 
 extern "C" int deepep_amd_set_error(int code, const char* msg);
+extern "C" void deepep_amd_register_budget(void* stream, int cus);
 
 namespace {
 
@@ -193,12 +194,14 @@ int deepep_stream_create_cu_budget(int num_cus, deepep_stream_t* stream) {
     hipStream_t s = nullptr;
     e = hipExtStreamCreateWithCUMask(&s, static_cast<uint32_t>(words), mask);
     if (e != hipSuccess) return hip_fail(e, "hipExtStreamCreateWithCUMask");
+    deepep_amd_register_budget(s, num_cus);          // combine launches on it size a persistent grid to it
     *stream = reinterpret_cast<deepep_stream_t>(s);
     return DEEPEP_OK;
 }
 
 int deepep_stream_destroy(deepep_stream_t stream) {
     if (stream == nullptr) return DEEPEP_OK;
+    deepep_amd_register_budget(stream, 0);
     const hipError_t e = hipStreamDestroy(reinterpret_cast<hipStream_t>(stream));
     return e == hipSuccess ? DEEPEP_OK : hip_fail(e, "hipStreamDestroy");
 }

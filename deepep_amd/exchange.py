@@ -16,8 +16,8 @@ from typing import List, Optional
 import torch
 import torch.distributed as dist
 
+from .handle import packed_row_layout
 from .kernels import MODE_EPILOGUE, MODE_LOCAL
-from .utils import align
 
 _WINDOW_IDS = itertools.count(1)            # symmetric windows created by this process
 
@@ -40,10 +40,12 @@ class ExchangeMixin:
         than one chunk, phase A of chunk c+1 runs while RCCL moves chunk c and phase B of chunk
         c runs on a second stream while RCCL moves chunk c+1."""
         kern = self.kernels
-        w_elems = 0 if topk_weights is None else align(K * 4, 16) // 2     # the plan's packed-row layout
-        row_elems = hidden + w_elems
+        # packed rows [bf16 partial | fp32 weights], whole 128-byte lines (handle.packed_row_layout)
+        with_w = topk_weights is not None
+        row_bytes, w_off, w_pad = packed_row_layout(hidden, K, with_w)
+        row_elems = row_bytes // 2
         pipelined = len(plan.chunks) > 1 and self.use_cuda
-        if w_elems:
+        if with_w:
             assert all(ch.wtable_b is not None for ch in plan.chunks), 'receive rows too large for int32 weight indices'
         if pipelined:
             if getattr(self, '_stream_b', None) is None:
@@ -62,10 +64,11 @@ class ExchangeMixin:
             with (torch.cuda.stream(sa) if sa is not stream else self._null_ctx()):
                 n_send = sum(ch.send_counts)
                 packed = torch.empty((n_send, row_elems), dtype=x.dtype, device=x.device)
-                partial_w = packed[:, hidden:].view(torch.float32)[:, :K] if w_elems else None
+                partial_w = packed.view(torch.float32)[:, w_off // 4:w_off // 4 + K] if with_w else None
                 self._mark(sa)
                 kern.combine_reduce(MODE_LOCAL, x, packed[:, :hidden], n_send, table=ch.table_a, row_weights=row_w,
-                                    wtable=ch.wtable_a, wsrc=wsrc, out_weights=partial_w, stream=sa)
+                                    wtable=ch.wtable_a, wsrc=wsrc, out_weights=partial_w, weights_pad=w_pad,
+                                    stream=sa)
                 self._mark(sa)
                 recv = torch.empty((sum(ch.back_counts), row_elems), dtype=x.dtype, device=x.device)
                 if pipelined:
@@ -85,8 +88,8 @@ class ExchangeMixin:
                 sb = stream_b if pipelined else stream
                 if work is not None:
                     work.wait()
-                wtable_b = ch.wtable_b if w_elems else None
-                recv_wsrc = recv.view(torch.float32).view(-1) if w_elems else None
+                wtable_b = ch.wtable_b if with_w else None
+                recv_wsrc = recv.view(torch.float32).view(-1) if with_w else None
                 lo, hi = ch.lo, ch.hi
                 self._mark(sb)
                 kern.combine_reduce(MODE_EPILOGUE, recv[:, :hidden], combined_x[lo:hi], hi - lo, table=ch.table_b,
@@ -107,8 +110,9 @@ class ExchangeMixin:
         runs while RCCL moves chunk c, and the one reduction of chunk c (weighted: the legacy fma
         chain) runs on a second stream while RCCL moves chunk c+1."""
         kern = self.kernels
-        w_elems = 8 if row_w is not None else 0
-        row_elems = hidden + w_elems
+        w_elems = 1 if row_w is not None else 0          # one gating weight per unreduced row
+        row_bytes, w_off, w_pad = packed_row_layout(hidden, 1, bool(w_elems), single=True)
+        row_elems = row_bytes // 2
         pipelined = self.use_cuda
         if pipelined:
             if getattr(self, '_stream_b', None) is None:
@@ -119,11 +123,11 @@ class ExchangeMixin:
         for ch in plan.chunks:
             n_send = sum(ch.send_counts)
             send = torch.empty((n_send, row_elems), dtype=x.dtype, device=x.device)
-            send_w = send[:, hidden:].view(torch.float32)[:, :1] if w_elems else None
+            send_w = send.view(torch.float32)[:, w_off // 4:w_off // 4 + 1] if w_elems else None
             self._mark(stream)
             kern.combine_reduce(MODE_LOCAL, x, send[:, :hidden], n_send, table=ch.table_a,
                                 wtable=ch.table_a if w_elems else None, wsrc=wsrc if w_elems else None,
-                                out_weights=send_w, stream=stream)
+                                out_weights=send_w, weights_pad=w_pad, stream=stream)
             self._mark(stream)
             recv = torch.empty((sum(ch.back_counts), row_elems), dtype=x.dtype, device=x.device)
             if pipelined:
@@ -140,7 +144,7 @@ class ExchangeMixin:
                 sb = stream_b if pipelined else stream
                 if work is not None:
                     work.wait()
-                recv_w = recv[:, hidden:].view(torch.float32)[:, 0].contiguous() if w_elems else None
+                recv_w = recv.view(torch.float32)[:, w_off // 4].contiguous() if w_elems else None
                 lo, hi = ch.lo, ch.hi
                 self._mark(sb)
                 kern.combine_reduce(MODE_EPILOGUE, recv[:, :hidden], combined_x[lo:hi], hi - lo, table=ch.table_b,
@@ -198,12 +202,11 @@ class ExchangeMixin:
         T = handle.topk_idx.shape[0]
         rank_layout = R <= K                              # use_rank_layout, combine_utils.cuh:8-13
         self._window_slots = min(R, K)
-        row_bytes = align(hidden * 2, 16) + align(K * 4, 16)
+        row_bytes, w_off, w_pad = packed_row_layout(hidden, K)     # the weight tail is always reserved
         sym = self._window(row_bytes, rows_per_slot=T_max)
         num_chunks = min(self._num_chunks(handle), 63)
         plan = self._plan(handle, False, num_chunks, hidden, window=sym)
         kern = self.kernels
-        w_off = align(hidden * 2, 16)
         n_rows = self._window_slots * T_max
         rows = sym.data[:n_rows * row_bytes].view(torch.bfloat16).view(n_rows, row_bytes // 2)
         recv_wsrc = sym.data[:n_rows * row_bytes].view(torch.float32) if topk_weights is not None else None
@@ -227,7 +230,7 @@ class ExchangeMixin:
             kern.combine_reduce_scatter(x, ch.out_rows.shape[0], ch.out_rows, table=ch.table_a, row_weights=row_w,
                                         wtable=ch.wtable_a, wsrc=wsrc,
                                         num_weights=K if topk_weights is not None else 0,
-                                        weights_offset=w_off, error_flag=err, stream=sa)
+                                        weights_offset=w_off, weights_pad=w_pad, error_flag=err, stream=sa)
             self._mark(sa)
             sym.signal(1 + c, sa)
         if sa is not stream:
@@ -266,8 +269,8 @@ class ExchangeMixin:
         T = handle.topk_idx.shape[0]
         with_w = topk_weights is not None
         self._window_slots = K
-        w_off = align(hidden * 2, 16)
-        row_bytes = w_off + 16                # the weight tail is always reserved: one window size per buffer
+        # the weight tail is always reserved: one window size per buffer
+        row_bytes, w_off, w_pad = packed_row_layout(hidden, 1, True, single=True)
         sym = self._window(row_bytes, rows_per_slot=T_max)
         num_chunks = min(self._num_chunks(handle), 63)
         plan = self._plan(handle, True, num_chunks, hidden, window=sym)
@@ -289,7 +292,8 @@ class ExchangeMixin:
             self._mark(stream)
             kern.combine_reduce_scatter(x, ch.out_rows.shape[0], ch.out_rows, table=ch.table_a,
                                         wtable=ch.table_a if with_w else None, wsrc=wsrc if with_w else None,
-                                        num_weights=1 if with_w else 0, weights_offset=w_off, error_flag=err,
+                                        num_weights=1 if with_w else 0, weights_offset=w_off, weights_pad=w_pad,
+                                        error_flag=err,
                                         stream=stream)
             self._mark(stream)
             sym.signal(1 + c, stream)

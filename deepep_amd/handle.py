@@ -75,6 +75,21 @@ class CombinePlan:
     ready: Optional[tuple] = None                     # (stream, event) the tables were built on
 
 
+LINE_BYTES = 128      # a memory-side line: packed rows are whole lines (a partial line costs a read-modify-write)
+
+
+def packed_row_layout(hidden: int, num_topk: int, with_weights: bool = True, single: bool = False):
+    """(row_bytes, weights_offset, weights_pad_floats) of a packed exchange row [bf16 row | fp32
+    weights]: the bf16 part and the weight tail each a whole number of 128-byte lines, so every row
+    starts on a line and the tail is written as full lines (zeros past the weights).  Measured on
+    EP = 8's phase A (tools/kphase.py): 32-byte aligned rows with a 32-byte weight tail 303 us,
+    line-aligned rows with a partial tail line 281 us, line-aligned rows without a tail 257 us.
+    single: one weight per row (the single reduction), else num_topk."""
+    w_off = align(hidden * 2, LINE_BYTES)
+    tail = align((1 if single else num_topk) * 4, LINE_BYTES) if with_weights else 0
+    return w_off + tail, w_off, tail // 4
+
+
 def chunk_geometry(num_max_tokens: int, num_chunks: int):
     """(blocks, blocks per chunk, chunks): chunks are whole 64-token blocks, so their exchange sizes
     are sums of block counts; fewer chunks than asked when the batch is small."""
@@ -114,8 +129,7 @@ def build_ep_plan(kern, handle: 'EPHandle', *, num_ranks: int, rank: int, single
     table_a = torch.empty((total, width_a), dtype=torch.int32, device=dev)
     wtable_a = torch.empty((total, K), dtype=torch.int32, device=dev) if not expanded else None
     if window is not None:
-        w_off = align(hidden * 2, 16)
-        row_bytes = w_off + (16 if single else align(K * 4, 16))
+        row_bytes = packed_row_layout(hidden, K, True, single)[0]
         out_rows = torch.empty((total,), dtype=torch.int64, device=dev)
         bases = window.data_bases_dev
     else:
@@ -130,12 +144,9 @@ def build_ep_plan(kern, handle: 'EPHandle', *, num_ranks: int, rank: int, single
     row_floats = w_off_f = 0
     if not single:
         # weight index into the packed rows: [bf16 partial | fp32 weights (16-byte aligned)]
-        if window is not None:
-            row_floats, w_off_f = row_bytes // 4, align(hidden * 2, 16) // 4
-            max_rows = min(R, K) * T_max
-        else:
-            row_floats, w_off_f = (hidden + align(K * 4, 16) // 2) // 2, hidden // 2
-            max_rows = max([sum(b) for b in back] + [0])
+        rb, w_off, _ = packed_row_layout(hidden, K, True)
+        row_floats, w_off_f = rb // 4, w_off // 4
+        max_rows = min(R, K) * T_max if window is not None else max([sum(b) for b in back] + [0])
         if max_rows * row_floats + w_off_f + K < 2 ** 31:
             wtable_b = torch.empty((T, K), dtype=torch.int32, device=dev)
     sflags = (PLAN_SINGLE if single else 0) | (PLAN_WINDOW if window is not None else 0) | \

@@ -35,7 +35,8 @@ class RowLayout:
         idx_off = align(sf_off + sf_bytes, 16)
         w_off = idx_off + align(num_topk * 8, 16)
         src_off = w_off + align(num_topk * 4, 16)
-        return RowLayout(x_bytes, sf_bytes, num_topk, sf_off, idx_off, w_off, src_off, src_off + 16)
+        # rows are whole 128-byte lines, so every row (and its x bytes) starts on a line
+        return RowLayout(x_bytes, sf_bytes, num_topk, sf_off, idx_off, w_off, src_off, align(src_off + 16, 128))
 
 
 def _require(cond: bool, msg: str) -> None:
@@ -71,7 +72,9 @@ class HipKernels:
                        wtable: Optional[torch.Tensor] = None, wsrc: Optional[torch.Tensor] = None,
                        out_weights: Optional[torch.Tensor] = None,
                        units_per_block: int = 0, error_flag: Optional[torch.Tensor] = None,
-                       stream=None) -> None:
+                       weights_pad: int = 0, stream=None) -> None:
+        """weights_pad: floats written per weight row (zeros past the weights); 32 fills a packed
+        row's 128-byte tail line, so no partial line reaches the memory side."""
         _require(src.is_cuda and out.is_cuda, 'combine tensors must be on the GPU')
         _require(src.dtype == torch.bfloat16 and out.dtype == torch.bfloat16, 'combine rows must be bfloat16')
         _require(src.dim() == 2 and out.dim() == 2 and (src.numel() == 0 or src.stride(1) == 1) and
@@ -110,7 +113,7 @@ class HipKernels:
             ptr(out), out.stride(0) if out.shape[0] > 0 else hidden,
             num_units, hidden,
             ptr(w), w_stride,
-            ptr(wsrc), ptr(out_weights), num_weights, ow_stride,
+            ptr(wsrc), ptr(out_weights), num_weights, ow_stride, weights_pad,
             units_per_block, ptr(error_flag),
             _stream_handle(stream))
         _lib.check(rc, 'combine_reduce')
@@ -118,7 +121,7 @@ class HipKernels:
     def combine_reduce_scatter(self, src: torch.Tensor, num_units: int, out_rows: torch.Tensor,
                                table: Optional[torch.Tensor] = None, row_weights: Optional[torch.Tensor] = None,
                                wtable: Optional[torch.Tensor] = None, wsrc: Optional[torch.Tensor] = None,
-                               num_weights: int = 0, weights_offset: int = 0,
+                               num_weights: int = 0, weights_offset: int = 0, weights_pad: int = 0,
                                error_flag: Optional[torch.Tensor] = None, stream=None) -> None:
         """Phase A storing unit u's row at byte address out_rows[u] (a peer window over xGMI)."""
         _require(src.is_cuda and src.dtype == torch.bfloat16 and src.dim() == 2 and
@@ -135,7 +138,8 @@ class HipKernels:
         rc = self.lib.deepep_combine_reduce_scatter(
             int(row_weights is not None), ptr(src), src.shape[0], src.stride(0) if src.shape[0] > 0 else hidden,
             ptr(t), t_stride, t_width, ptr(row_weights), ptr(out_rows), num_units, hidden,
-            ptr(w), w_stride, ptr(wsrc), num_weights, weights_offset, ptr(error_flag), _stream_handle(stream))
+            ptr(w), w_stride, ptr(wsrc), num_weights, weights_offset, weights_pad, ptr(error_flag),
+            _stream_handle(stream))
         _lib.check(rc, 'combine_reduce_scatter')
 
     def build_local_plan(self, src_metadata: torch.Tensor, num_recv_tokens: int, num_topk: int,

@@ -87,6 +87,9 @@ const char* deepep_amd_build_id(void);
  *                  out_weights[u*out_weights_stride + k] = (i = wtable ? wtable[u*wtable_stride + k]
  *                                                             : u*num_weights + k) >= 0 ? wsrc[i] : 0
  *                  (a stride lets the weights ride in the tail of packed exchange rows)
+ *   weights_pad    floats written per weight row (<= 64; values below num_weights mean num_weights):
+ *                  the entries past num_weights are zeros.  32 writes a packed row's whole 128-byte
+ *                  tail line at once: a partial-line store costs the memory side a read-modify-write
  *   units_per_block  workgroup shape: 4 = 4 (row, column-chunk) items per 256-thread workgroup,
  *                  8 = 8 items per 512-thread workgroup, 0 = automatic (4 for LOCAL, else 8)
  *   error_flag     device int or NULL; bit 1 is set when a slot is >= num_src_rows (such slots are
@@ -103,7 +106,7 @@ int deepep_combine_reduce(int mode, int weighted,
                           int num_units, int hidden,
                           const int32_t* wtable, int64_t wtable_stride,
                           const float* wsrc, float* out_weights, int num_weights,
-                          int64_t out_weights_stride,
+                          int64_t out_weights_stride, int weights_pad,
                           int units_per_block, int32_t* error_flag,
                           deepep_stream_t stream);
 
@@ -311,16 +314,16 @@ int deepep_sym_wait(const uint64_t* peer_flags, int rank, int num_ranks, int slo
 /* Phase A writing straight into the owners' receive rows (combine_impl's NVLink push,
  * combine.cuh:96-106, 125-176, 215-226): the reduce of deepep_combine_reduce(DEEPEP_MODE_LOCAL, ...)
  * with unit u's bf16 row stored at byte address out_rows[u] (any rank's window, 16-byte aligned)
- * and, when num_weights > 0, its top-k weights (the wtable / wsrc pass-through rule above) at
- * out_rows[u] + weights_offset.  All these stores are system-scope write-through (sc0 sc1), so
- * they are visible to the owning GPU once the kernel has completed. */
+ * and, when num_weights > 0, its top-k weights (the wtable / wsrc pass-through rule above, weights_pad
+ * floats) at out_rows[u] + weights_offset.  All these stores are system-scope write-through (sc0 sc1),
+ * so they are visible to the owning GPU once the kernel has completed. */
 int deepep_combine_reduce_scatter(int weighted,
                                   const void* src, int64_t num_src_rows, int64_t src_row_stride,
                                   const int32_t* table, int64_t table_stride, int table_width,
                                   const float* row_weights,
                                   const uint64_t* out_rows, int num_units, int hidden,
                                   const int32_t* wtable, int64_t wtable_stride,
-                                  const float* wsrc, int num_weights, int64_t weights_offset,
+                                  const float* wsrc, int num_weights, int64_t weights_offset, int weights_pad,
                                   int32_t* error_flag, deepep_stream_t stream);
 
 /* A CU budget: a stream whose kernels run on `num_cus` compute units only, rounded up to a multiple

@@ -102,7 +102,7 @@ int main(void) {
         for (int with_bias = 0; with_bias <= 1; ++with_bias) {
             const void* b0 = with_bias ? d_bias : NULL;
             CHECK_EP(deepep_combine_reduce(DEEPEP_MODE_FUSED, weighted, d_y, N, H, d_plan, K, K, weighted ? d_w : NULL,
-                                           b0, NULL, d_out, H, T, H, d_plan, K, d_w, d_out_w, K, 0, 0, d_err, NULL));
+                                           b0, NULL, d_out, H, T, H, d_plan, K, d_w, d_out_w, K, 0, 0, 0, d_err, NULL));
             CHECK_HIP(hipDeviceSynchronize());
             CHECK_HIP(hipMemcpy(got, d_out, (size_t)T * H * 2, hipMemcpyDeviceToHost));
             CHECK_HIP(hipMemcpy(got_w, d_out_w, (size_t)T * K * 4, hipMemcpyDeviceToHost));
@@ -125,7 +125,7 @@ int main(void) {
     }
     /* error convention: hidden % 8 != 0 is rejected on the host, with a message, nothing launched */
     const int rc = deepep_combine_reduce(DEEPEP_MODE_FUSED, 0, d_y, N, H, d_plan, K, K, NULL, NULL, NULL, d_out, H, T,
-                                         H - 4, NULL, 0, NULL, NULL, 0, 0, 0, NULL, NULL);
+                                         H - 4, NULL, 0, NULL, NULL, 0, 0, 0, 0, NULL, NULL);
     if (rc != DEEPEP_ERR_INVALID_ARG || strlen(deepep_amd_last_error()) == 0) {
         fprintf(stderr, "invalid hidden: rc %d, message '%s'\n", rc, deepep_amd_last_error());
         ++fails;

@@ -21,7 +21,8 @@ class OracleKernels:
     name = 'oracle'
 
     def combine_reduce(self, mode, src, out, num_units, table=None, row_weights=None, bias0=None, bias1=None,
-                       wtable=None, wsrc=None, out_weights=None, units_per_block=0, error_flag=None, stream=None):
+                       wtable=None, wsrc=None, out_weights=None, units_per_block=0, error_flag=None, weights_pad=0,
+                       stream=None):
         assert src.device.type == 'cpu' and out.device.type == 'cpu'
         for t in (src, out, table, row_weights, bias0, bias1, wtable, wsrc, out_weights):
             assert t is None or t.dim() == 1 or t.stride(-1) == 1
@@ -36,6 +37,9 @@ class OracleKernels:
             _p(wsrc), _p(out_weights), out_weights.shape[1] if out_weights is not None else 0,
             out_weights.stride(0) if out_weights is not None else 0)
         assert rc == 0, 'oracle_combine_rows failed'
+        if out_weights is not None and weights_pad > out_weights.shape[1] and num_units:
+            wide = torch.as_strided(out_weights, (num_units, weights_pad), (out_weights.stride(0), 1))
+            wide[:, out_weights.shape[1]:] = 0                  # the rest of the row's tail line
 
     def build_local_plan(self, src_metadata, num_recv_tokens, num_topk, num_max_tokens_per_rank, expanded,
                          plan, num_tokens, topk_idx=None, wtable=None, stream=None):

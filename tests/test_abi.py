@@ -48,33 +48,33 @@ def test_build_id_matches_sources(lib):
 def test_invalid_arguments_are_rejected_without_a_gpu(lib):
     # mode out of range
     rc = lib.deepep_combine_reduce(7, 0, None, 0, 8, None, 0, 1, None, None, None, 16, 8, 1, 8,
-                                   None, 0, None, None, 0, 0, 0, None, None)
+                                   None, 0, None, None, 0, 0, 0, 0, None, None)
     assert rc == -1 and b'mode' in lib.deepep_amd_last_error()
     # hidden not a multiple of 8 elements
     rc = lib.deepep_combine_reduce(1, 0, 16, 1, 8, None, 0, 1, None, None, None, 16, 8, 1, 6,
-                                   None, 0, None, None, 0, 0, 0, None, None)
+                                   None, 0, None, None, 0, 0, 0, 0, None, None)
     assert rc == -1 and b'hidden' in lib.deepep_amd_last_error()
     # misaligned pointers
     rc = lib.deepep_combine_reduce(1, 0, 18, 1, 8, None, 0, 1, None, None, None, 32, 8, 1, 8,
-                                   None, 0, None, None, 0, 0, 0, None, None)
+                                   None, 0, None, None, 0, 0, 0, 0, None, None)
     assert rc == -1 and b'aligned' in lib.deepep_amd_last_error()
     # bias in the local phase
     rc = lib.deepep_combine_reduce(0, 0, 16, 1, 8, None, 0, 1, None, 32, None, 48, 8, 1, 8,
-                                   None, 0, None, None, 0, 0, 0, None, None)
+                                   None, 0, None, None, 0, 0, 0, 0, None, None)
     assert rc == -1 and b'bias' in lib.deepep_amd_last_error()
     # table width beyond top-32
     rc = lib.deepep_combine_reduce(1, 0, 16, 1, 8, 64, 40, 33, None, None, None, 48, 8, 1, 8,
-                                   None, 0, None, None, 0, 0, 0, None, None)
+                                   None, 0, None, None, 0, 0, 0, 0, None, None)
     assert rc == -1
     # zero units: nothing to do, success without a launch
     assert lib.deepep_combine_reduce(1, 0, 16, 1, 8, None, 0, 1, None, None, None, 48, 8, 0, 8,
-                                     None, 0, None, None, 0, 0, 0, None, None) == 0
-    # kernel choice: -1 (default: the item kernel), 0-4; anything else is rejected with a message
-    assert lib.deepep_set_kernel_choice(5) == -1 and b'kernel choice' in lib.deepep_amd_last_error()
+                                     None, 0, None, None, 0, 0, 0, 0, None, None) == 0
+    # kernel choice: -1 (default: the item kernel), 0-5; anything else is rejected with a message
+    assert lib.deepep_set_kernel_choice(6) == -1 and b'kernel choice' in lib.deepep_amd_last_error()
     assert lib.deepep_set_kernel_choice(-2) == -1
-    for c in (0, 1, 2, 3, 4, -1):
+    for c in (0, 1, 2, 3, 4, 5, -1):
         assert lib.deepep_set_kernel_choice(c) == 0
-    assert lib.deepep_last_kernel_choice() in (0, 1, 2, 3, 4)
+    assert lib.deepep_last_kernel_choice() in (0, 1, 2, 3, 4, 5)
     # launch configuration knobs out of range
     assert lib.deepep_set_launch_config(3, -1, -1, 0) == -1
     assert lib.deepep_set_launch_config(0, -1, -1, 3) == -1

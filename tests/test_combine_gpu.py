@@ -203,6 +203,37 @@ def test_kernel_poisoned_by_timed_out_barrier(kern):
     assert torch.equal(out, ref)
 
 
+@pytest.mark.parametrize('choice', [0, 1, 5])
+def test_kernel_weights_pad_fills_the_tail_line(kern, choice):
+    """weights_pad: each unit's weight row is written as weights_pad floats (the weights, then zeros) --
+    a packed row's whole 128-byte tail line -- and nothing past it."""
+    rng = np.random.default_rng(choice)
+    units, K, H = 23, 8, 1024
+    src = _bf16(_random_rows(rng, units * K, H))
+    table = torch.from_numpy(rng.integers(0, units * K, size=(units, K)).astype(np.int32)).cuda()
+    wsrc = torch.rand(units * K, device='cuda')
+    packed = torch.full((units, H + 128), 7.0, dtype=torch.bfloat16, device='cuda')
+    ow = packed.view(torch.float32)[:, H // 2:H // 2 + K]
+    assert kern.lib.deepep_set_kernel_choice(choice) == 0
+    try:
+        kern.combine_reduce(MODE_LOCAL, src, packed[:, :H], units, table=table, wtable=table, wsrc=wsrc,
+                            out_weights=ow, weights_pad=32)
+        torch.cuda.synchronize()
+    finally:
+        kern.lib.deepep_set_kernel_choice(-1)
+    tail = packed.view(torch.float32)[:, H // 2:]
+    assert torch.equal(tail[:, :K], wsrc[table.long()])
+    assert bool((tail[:, K:32] == 0).all())
+    assert bool((packed[:, H + 64:] == 7.0).all())                 # past the 32 floats: untouched
+    win = torch.full((units, H + 128), 7.0, dtype=torch.bfloat16, device='cuda')
+    addr = torch.arange(units, device='cuda', dtype=torch.int64) * (2 * H + 256) + win.data_ptr()
+    kern.combine_reduce_scatter(src, units, addr, table=table, wtable=table, wsrc=wsrc, num_weights=K,
+                                weights_offset=2 * H, weights_pad=32)
+    torch.cuda.synchronize()
+    assert torch.equal(win[:, :H], packed[:, :H])
+    assert torch.equal(win.view(torch.float32)[:, H // 2:], tail)
+
+
 def test_kernel_empty_and_errors(kern):
     src = torch.zeros((4, 64), dtype=torch.bfloat16, device='cuda')
     out = torch.empty((0, 64), dtype=torch.bfloat16, device='cuda')
@@ -372,8 +403,8 @@ def test_config2_full_size_bitwise(weighted, T, skew):
     ref, _ = oracle.phase_b(recv, None, idx.cpu().numpy(), E, 1, True, True)
     lib = buf.kernels.lib
     try:
-        # the item kernel, the streaming kernel (2 and 1 vectors per lane, persistent), XCD order, default
-        for choice in (0, 1, 2, 3, 4, -1):
+        # the item kernel, the streaming kernel (2 and 1 vectors per lane, persistent), XCD order, persistent, default
+        for choice in (0, 1, 2, 3, 4, 5, -1):
             assert lib.deepep_set_kernel_choice(choice) == 0
             out, out_w, _ = buf.combine(y, handle, topk_weights=ex_w, apply_topk_weights=weighted)
             torch.cuda.synchronize()

@@ -36,10 +36,12 @@ def _case(seed: int):
     return rng, T, H, K, E, masked
 
 
-@pytest.fixture(params=[0, 1, 2, 3, 4], ids=['item', 'stream', 'stream_vpt1', 'stream_persistent', 'item_xcd'])
+@pytest.fixture(params=[0, 1, 2, 3, 4, 5], ids=['item', 'stream', 'stream_vpt1', 'stream_persistent', 'item_xcd',
+                                                'item_persistent'])
 def kernel_choice(request):
     """Every combine kernel (deepep_set_kernel_choice): the item kernel and the streaming kernel at 2 and 1
-    vectors per lane and on a persistent grid, and the item kernel in XCD-contiguous order."""
+    vectors per lane and on a persistent grid, and the item kernel in XCD-contiguous order and on a
+    persistent grid."""
     from deepep_amd import _lib
     lib = _lib.load()
     assert lib.deepep_set_kernel_choice(request.param) == 0

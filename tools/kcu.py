@@ -1,6 +1,11 @@
 """Combine time under a CU budget (ElasticBuffer.combine(num_sms=n): kernels on a
-hipExtStreamCreateWithCUMask stream), BASELINE config 2 at EP = 1: shows the budget is honoured
-(time ~ 1 / CUs until HBM saturates) and what the combine costs when it leaves CUs to compute."""
+hipExtStreamCreateWithCUMask stream, persistent grid sized to the budget), BASELINE config 2 at
+EP = 1: what the combine costs when it leaves CUs to overlapping compute.
+
+Per budget: `api` = combine(num_sms=n) from the default stream (two cross-stream hops per call),
+`api_on_budget_stream` = the same call issued from the budget stream itself (no hops), `kernel` = the
+fused launch alone on the budget stream (item kernel, persistent), `kernel_stream` = the streaming
+kernel forced (deepep_set_kernel_choice(3), persistent)."""
 import json
 import os
 import sys
@@ -17,6 +22,7 @@ def main():
     os.environ.setdefault('MASTER_PORT', '29681')
     dist.init_process_group('gloo', rank=0, world_size=1)
     from deepep_amd import ElasticBuffer
+    from deepep_amd.kernels import MODE_FUSED
     T, H, K, E = 8192, 7168, 8, 256
     torch.manual_seed(0)
     w, idx = torch.topk(torch.rand((T, E), device='cuda'), K, dim=-1, sorted=False)
@@ -24,22 +30,55 @@ def main():
     _, _, ex_w, handle, _ = buf.dispatch(torch.zeros((T, H), dtype=torch.bfloat16, device='cuda'),
                                          topk_idx=idx.to(torch.int64), topk_weights=w, num_experts=E, do_expand=True)
     y = torch.randn((handle.num_expanded_tokens, H), device='cuda').to(torch.bfloat16)
+    ref, _, _ = buf.combine(y, handle, topk_weights=ex_w, apply_topk_weights=True)
+    plan = handle._combine_plans[('multi', 1)]
+    out = torch.empty((T, H), dtype=torch.bfloat16, device='cuda')
+    out_w = torch.empty((T, K), dtype=torch.float32, device='cuda')
     nbytes = T * (K * H * 2 + H * 2 + K * 8)
-    s = torch.cuda.current_stream()
-    for n in (0, 256, 224, 192, 160, 128, 96, 64, 32, 16):
-        def step():
-            return buf.combine(y, handle, topk_weights=ex_w, apply_topk_weights=True, num_sms=n)
+    lib = buf.kernels.lib
+
+    def timed(fn, s, n=20):
         for _ in range(3):
-            step()
+            fn()
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(s)
-        for _ in range(20):
-            step()
+        for _ in range(n):
+            fn()
         e1.record(s)
         torch.cuda.synchronize()
-        us = e0.elapsed_time(e1) * 1e3 / 20
-        print(json.dumps(dict(num_sms=n, us_per_call=round(us, 1), gbps=round(nbytes / us / 1e3, 1))), flush=True)
+        return e0.elapsed_time(e1) * 1e3 / n
+
+    for n in (0, 224, 192, 160, 128, 96, 64, 32, 16):
+        row = dict(num_sms=n)
+        s0 = torch.cuda.current_stream()
+        row['api_us'] = round(timed(lambda: buf.combine(y, handle, topk_weights=ex_w, apply_topk_weights=True,
+                                                        num_sms=n), s0), 1)
+        bs = buf.get_cu_budget_stream(n) if n else s0
+        with torch.cuda.stream(bs):
+            res = {}
+
+            def api():
+                res['o'] = buf.combine(y, handle, topk_weights=ex_w, apply_topk_weights=True, num_sms=n)[0]
+            row['api_on_budget_stream_us'] = round(timed(api, bs), 1)
+
+            def kern():
+                buf.kernels.combine_reduce(MODE_FUSED, y, out, T, table=plan.local_table, row_weights=ex_w,
+                                           wtable=plan.local_table, wsrc=ex_w, out_weights=out_w, stream=bs)
+            row['kernel_us'] = round(timed(kern, bs), 1)
+            torch.cuda.synchronize()
+            row['bitwise'] = bool(torch.equal(out, ref) and torch.equal(res['o'], ref))
+            lib.deepep_set_kernel_choice(3)
+            row['kernel_stream_us'] = round(timed(kern, bs), 1)
+            lib.deepep_set_kernel_choice(-1)
+            lib.deepep_set_launch_config(0, 1, -1, 0)          # persistent item kernel with LDS staging
+            row['kernel_lds_us'] = round(timed(kern, bs), 1)
+            lib.deepep_set_launch_config(0, -1, -1, 0)
+            torch.cuda.synchronize()
+            row['bitwise'] = row['bitwise'] and bool(torch.equal(out, ref))
+        for k in ('api_us', 'api_on_budget_stream_us', 'kernel_us', 'kernel_stream_us', 'kernel_lds_us'):
+            row[k.replace('_us', '_tbps')] = round(nbytes / row[k] / 1e6, 2)
+        print(json.dumps(row), flush=True)
     dist.destroy_process_group()
 
 

@@ -40,7 +40,7 @@ def main():
     table_a[ii, kk] = pos.to(torch.int32)
     y = torch.randn((n_exp, H), device='cuda', generator=g).to(torch.bfloat16)
     w = torch.rand((n_exp,), device='cuda', generator=g)
-    packed = torch.empty((n_recv, H + 16), dtype=torch.bfloat16, device='cuda')
+    packed = torch.empty((n_recv, H + 64), dtype=torch.bfloat16, device='cuda')   # the library's packed rows
     pw = packed[:, H:].view(torch.float32)[:, :K]
     s = torch.cuda.current_stream()
     bytes_a = n_exp * H * 2 + n_recv * (H * 2 + K * 4)
@@ -49,18 +49,34 @@ def main():
         for weighted, upb in ((True, 8), (True, 4), (False, 4)):
             us = timeit(lambda: kern.combine_reduce(MODE_LOCAL, y, packed[:, :H], n_recv, table=table_a,
                                                     row_weights=w if weighted else None, wtable=table_a, wsrc=w,
-                                                    out_weights=pw, units_per_block=upb, stream=s), s)
+                                                    out_weights=pw, weights_pad=32, units_per_block=upb, stream=s), s)
             print(json.dumps(dict(phase='A', weighted=weighted, rows_in_flight=rif, upb=upb, units=n_recv,
                                   rows=n_exp, us=round(us, 1), gbps=round(bytes_a / us / 1e3, 1))), flush=True)
     kern.lib.deepep_set_launch_config(0, -1, -1, 0)
     # the library's kernels on the automatic shape, forced (0 item, 1 streaming, 2 streaming 1 vector/lane)
     for rnd in range(2):
-        for choice in (0, 1, 2, 3, 4):
+        for choice in (0, 1, 2, 3, 4, 5):
             assert kern.lib.deepep_set_kernel_choice(choice) == 0
             us = timeit(lambda: kern.combine_reduce(MODE_LOCAL, y, packed[:, :H], n_recv, table=table_a, row_weights=w,
-                                                    wtable=table_a, wsrc=w, out_weights=pw, stream=s), s)
-            print(json.dumps(dict(phase='A', kernel=('item', 'stream', 'stream_vpt1', 'stream_persistent', 'item_xcd')[choice], round=rnd, us=round(us, 1),
+                                                    wtable=table_a, wsrc=w, out_weights=pw, weights_pad=32, stream=s), s)
+            print(json.dumps(dict(phase='A', kernel=('item', 'stream', 'stream_vpt1', 'stream_persistent', 'item_xcd', 'item_persistent')[choice], round=rnd, us=round(us, 1),
                                   gbps=round(bytes_a / us / 1e3, 1))), flush=True)
+    kern.lib.deepep_set_kernel_choice(-1)
+    # packed-row stride: 2H + 32 B (the weights' tail; rows only 32-byte aligned, so every 2 KiB chunk
+    # store straddles partial 128-byte lines) vs 2H + 128 B (128-byte aligned rows) vs 2H (no tail)
+    for rnd in range(2):
+        for tail, pad in ((16, 0), (64, 0), (64, 32), (0, 0)):
+            pk = torch.empty((n_recv, H + tail), dtype=torch.bfloat16, device='cuda')
+            pkw = pk[:, H:].view(torch.float32)[:, :K] if tail else None
+            for choice in (0, 5):
+                assert kern.lib.deepep_set_kernel_choice(choice) == 0
+                us = timeit(lambda: kern.combine_reduce(MODE_LOCAL, y, pk[:, :H], n_recv, table=table_a, row_weights=w,
+                                                        wtable=table_a if tail else None, wsrc=w if tail else None,
+                                                        out_weights=pkw, weights_pad=pad, stream=s), s)
+                print(json.dumps(dict(phase='A_stride', row_bytes=(H + tail) * 2, weights_pad=pad,
+                                      kernel=('item', 'item_persistent')[choice // 5],
+                                      round=rnd, us=round(us, 1), gbps=round(bytes_a / us / 1e3, 1))), flush=True)
+            del pk
     kern.lib.deepep_set_kernel_choice(-1)
     # same bytes, rows in a random order (no expert grouping): the scatter's cost
     perm = torch.randperm(n_exp, device='cuda', generator=g).to(torch.int32)
@@ -77,7 +93,7 @@ def main():
     # ---- phase B on rank 0: its own tokens over the partial rows it receives (rank layout)
     table_b, row_of_lane, back = epilogue_tables(idx[0], E, R)
     n_back = sum(back)
-    recv = torch.randn((n_back, H + 16), device='cuda', generator=g).to(torch.bfloat16)
+    recv = torch.randn((n_back, H + 64), device='cuda', generator=g).to(torch.bfloat16)
     out = torch.empty((T, H), dtype=torch.bfloat16, device='cuda')
     valid_b = int((table_b >= 0).sum())
     bytes_b = valid_b * H * 2 + T * H * 2
@@ -90,10 +106,10 @@ def main():
                                   gbps=round(bytes_b / us / 1e3, 1))), flush=True)
     kern.lib.deepep_set_launch_config(0, -1, -1, 0)
     for rnd in range(2):
-        for choice in (0, 1, 2, 3, 4):
+        for choice in (0, 1, 2, 3, 4, 5):
             assert kern.lib.deepep_set_kernel_choice(choice) == 0
             us = timeit(lambda: kern.combine_reduce(MODE_EPILOGUE, recv[:, :H], out, T, table=table_b, stream=s), s)
-            print(json.dumps(dict(phase='B', kernel=('item', 'stream', 'stream_vpt1', 'stream_persistent', 'item_xcd')[choice], round=rnd, us=round(us, 1),
+            print(json.dumps(dict(phase='B', kernel=('item', 'stream', 'stream_vpt1', 'stream_persistent', 'item_xcd', 'item_persistent')[choice], round=rnd, us=round(us, 1),
                                   gbps=round(bytes_b / us / 1e3, 1))), flush=True)
     kern.lib.deepep_set_kernel_choice(-1)
     # EP = 1 fused kernel, config 2 (8 rows per token, 65536 random expanded rows)

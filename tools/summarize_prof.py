@@ -24,6 +24,15 @@ def stats(path, out):
     print('\n'.join(lines))
 
 
+def _build_id():
+    """The build id of the in-tree library the counters were collected with (bench.py accepts the
+    traffic only for the same build)."""
+    import os
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from deepep_amd import _lib
+    return _lib.binary_build_id(_lib.LIB_PATH)
+
+
 def pmc(out, workload, algo_bytes, *paths):
     per = defaultdict(list)
     for p in paths:
@@ -32,7 +41,8 @@ def pmc(out, workload, algo_bytes, *paths):
                 continue
             per[r['Counter_Name']].append(float(r['Counter_Value']))
     avg = {k: sum(v) / len(v) for k, v in per.items()}
-    entry = {'counters_avg_per_launch': avg, 'algorithmic_bytes_per_launch': int(algo_bytes)}
+    entry = {'counters_avg_per_launch': avg, 'algorithmic_bytes_per_launch': int(algo_bytes),
+             'build_id': _build_id()}
     read = 2 * avg['FETCH_SIZE'] * 1024 if 'FETCH_SIZE' in avg else None
     write = avg['WRITE_SIZE'] * 1024 if 'WRITE_SIZE' in avg else None
     if read is not None and write is not None:
@@ -74,7 +84,7 @@ def pmc_phases(out, meta_json, *paths):
     res = {}
     for k, counters in per.items():
         avg = {c: sum(v) / len(v) for c, v in counters.items()}
-        e = {'counters_avg_per_launch': avg, 'algorithmic_bytes_per_launch': algo[k]}
+        e = {'counters_avg_per_launch': avg, 'algorithmic_bytes_per_launch': algo[k], 'build_id': _build_id()}
         if 'FETCH_SIZE' in avg and 'WRITE_SIZE' in avg:
             e['hbm_read_bytes_per_launch'] = 2 * avg['FETCH_SIZE'] * 1024
             e['hbm_write_bytes_per_launch'] = avg['WRITE_SIZE'] * 1024

@@ -151,6 +151,34 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void* row, int 
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(row), 0, bytes, 0x00020000);
 }
 
+// The pass-through weight of lane k of unit u: wsrc[wtable[u][k]] (or wsrc[u * num_weights + k]), 0
+// for masked lanes and for lanes past num_weights (the zeros of a padded tail line).  When the slot
+// table doubles as the weight table (the expanded layouts) the lane's slot is already in hand -- and
+// so is its weight when the reduction is weighted by the same array -- so no dependent gather
+// delays the wave's row loads.
+template <bool kWeighted>
+__device__ __forceinline__ float pass_through_weight(const Params& p, int64_t u, int lane, int32_t my_slot, float my_w) {
+    if (lane >= p.num_weights) return 0.0f;
+    if (p.table != nullptr && p.wtable == p.table && p.wtable_stride == p.table_stride && lane < p.table_width) {
+        if (kWeighted && p.wsrc == p.row_weights) return my_w;
+        return my_slot >= 0 ? p.wsrc[my_slot] : 0.0f;
+    }
+    const int64_t i = p.wtable == nullptr ? u * p.num_weights + lane
+                                          : static_cast<int64_t>(p.wtable[u * p.wtable_stride + lane]);
+    return i >= 0 ? p.wsrc[i] : 0.0f;
+}
+
+// Store it: into the unit's weight row, or the row tail of a peer's window (system scope, as the
+// row stores).  weights_pad > num_weights writes a packed row's whole 128-byte tail line.
+__device__ __forceinline__ void store_weight(const Params& p, int64_t u, uint16_t* out_row, int lane, float v) {
+    if (p.out_rows != nullptr) {
+        float* const ow = reinterpret_cast<float*>(reinterpret_cast<char*>(out_row) + p.weights_offset);
+        __hip_atomic_store(ow + lane, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else {
+        p.out_weights[u * p.out_weights_stride + lane] = v;
+    }
+}
+
 // One wave per item = (unit u, column chunk c): the chunk is 64 lanes x kVPT x 16 B of every
 // source row of u.  The unit's slot table row (and its gating weights) arrive in my_slot / my_w, one
 // entry per lane; the valid slots are then visited in ascending order through the ballot mask,
@@ -172,24 +200,11 @@ __device__ __forceinline__ void combine_item(const Params& p, int64_t it, int nc
     const int n = __popcll(valid);
 
     // ---- top-k weight pass-through (combine.cuh:215-226, combine_reduce_epilogue.cuh:127-141),
-    //      written once per unit by the wave owning chunk 0
+    //      written once per unit by the wave owning chunk 0: gathered here, stored after the row
     uint16_t* const out_row = p.out_rows != nullptr ? reinterpret_cast<uint16_t*>(p.out_rows[u])
                                                      : p.out + u * p.out_stride;
-    if (c == 0 && p.num_weights > 0 && lane < p.weights_pad) {
-        // weights_pad > num_weights: a packed row's whole 128-byte tail line is written (zeros past the
-        // weights), so the memory side never merges a partial line
-        const int64_t i = lane >= p.num_weights ? -1
-                          : p.wtable == nullptr ? u * p.num_weights + lane
-                                                : static_cast<int64_t>(p.wtable[u * p.wtable_stride + lane]);
-        float* const ow = p.out_rows != nullptr
-                              ? reinterpret_cast<float*>(reinterpret_cast<char*>(out_row) + p.weights_offset)
-                              : p.out_weights + u * p.out_weights_stride;
-        const float v = i >= 0 ? p.wsrc[i] : 0.0f;
-        if (p.out_rows != nullptr)              // a peer's window: system scope, as the row stores
-            __hip_atomic_store(ow + lane, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        else
-            ow[lane] = v;
-    }
+    const bool wlane = c == 0 && p.num_weights > 0 && lane < p.weights_pad;
+    const float wv = wlane ? pass_through_weight<kWeighted>(p, u, lane, my_slot, my_w) : 0.0f;
 
     int vidx[kVPT];
     bool vok[kVPT];
@@ -299,6 +314,7 @@ __device__ __forceinline__ void combine_item(const Params& p, int64_t it, int nc
 #pragma unroll
     for (int v = 0; v < kVPT; ++v)
         __builtin_amdgcn_raw_buffer_store_b128(result[v], orow, vidx[v] * 16, 0, kStoreAux);
+    if (wlane) store_weight(p, u, out_row, lane, wv);
 }
 
 // A workgroup of kWaves waves takes kWaves consecutive items (a virtual block); the unit's slot table
@@ -407,19 +423,8 @@ combine_stream_kernel(const Params p) {
 
     uint16_t* const out_row = p.out_rows != nullptr ? reinterpret_cast<uint16_t*>(p.out_rows[u])
                                                      : p.out + u * p.out_stride;
-    if (p.num_weights > 0 && lane < p.weights_pad) {           // top-k weight pass-through, once per unit
-        const int64_t i = lane >= p.num_weights ? -1
-                          : p.wtable == nullptr ? u * p.num_weights + lane
-                                                : static_cast<int64_t>(p.wtable[u * p.wtable_stride + lane]);
-        float* const ow = p.out_rows != nullptr
-                              ? reinterpret_cast<float*>(reinterpret_cast<char*>(out_row) + p.weights_offset)
-                              : p.out_weights + u * p.out_weights_stride;
-        const float v = i >= 0 ? p.wsrc[i] : 0.0f;
-        if (p.out_rows != nullptr)
-            __hip_atomic_store(ow + lane, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        else
-            ow[lane] = v;
-    }
+    const bool wlane = p.num_weights > 0 && lane < p.weights_pad;     // top-k weight pass-through, once per unit
+    const float wv = wlane ? pass_through_weight<kWeighted>(p, u, lane, my_slot, my_w) : 0.0f;
 
     // the valid lanes in ascending order (n <= kStreamWidth) with their row pointers and weights
     const u32x4* rows[kStreamWidth];
@@ -500,6 +505,7 @@ combine_stream_kernel(const Params p) {
         if (c + 2 < nchunks) issue(c + 2, va);
         finish(c + 1, vb);
     }
+    if (wlane) store_weight(p, u, out_row, lane, wv);
     }
 }
 

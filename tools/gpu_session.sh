@@ -53,6 +53,14 @@ for step in "$@"; do
         pmcphases) for c in FETCH_SIZE WRITE_SIZE; do
                     run pmcph_$c 300 rocprofv3 --pmc $c -d $OUT/pmcph_$c -o pmc --output-format csv -- python3 tools/pmc_phases.py
                 done ;;
+        pmccal) # request-size calibration of every phase kernel (incl. the dispatch copy): 3 passes
+                run pmccal_ws 300 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE TCC_EA0_WRREQ_sum -d $OUT/pmccal_ws -o pmc --output-format csv -- python3 tools/pmc_phases.py
+                run pmccal_rq 300 timeout -s KILL 120 rocprofv3 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum -d $OUT/pmccal_rq -o pmc --output-format csv -- python3 tools/pmc_phases.py
+                run pmccal_fs 300 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmccal_fs -o pmc --output-format csv -- python3 tools/pmc_phases.py ;;
+        pmccopy) # counter calibration on the dispatch copy's pattern against torch copies of known bytes
+                run pmccopy_ws 300 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE TCC_EA0_WRREQ_sum -d $OUT/pmccopy_ws -o pmc --output-format csv -- python3 tools/pmc_copycal.py
+                run pmccopy_rq 300 timeout -s KILL 120 rocprofv3 --pmc TCC_EA0_WRREQ_64B_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_DRAM_sum TCC_EA0_RDREQ_DRAM_sum -d $OUT/pmccopy_rq -o pmc --output-format csv -- python3 tools/pmc_copycal.py
+                run pmccopy_fs 300 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmccopy_fs -o pmc --output-format csv -- python3 tools/pmc_copycal.py ;;
         pmcplain) for c in FETCH_SIZE WRITE_SIZE; do
                     run pmcp_$c 600 rocprofv3 --pmc $c -d $OUT/pmcp_$c -o pmc --output-format csv -- python3 tools/pmc_run.py --plain
                 done ;;

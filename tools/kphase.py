@@ -65,15 +65,18 @@ def main():
     # packed-row stride: 2H + 32 B (the weights' tail; rows only 32-byte aligned, so every 2 KiB chunk
     # store straddles partial 128-byte lines) vs 2H + 128 B (128-byte aligned rows) vs 2H (no tail)
     for rnd in range(2):
-        for tail, pad in ((16, 0), (64, 0), (64, 32), (0, 0)):
+        for tail, pad in ((16, 0), (64, 0), (64, 32), (0, 0), (64, -1)):
             pk = torch.empty((n_recv, H + tail), dtype=torch.bfloat16, device='cuda')
-            pkw = pk[:, H:].view(torch.float32)[:, :K] if tail else None
+            pkw = pk[:, H:].view(torch.float32)[:, :K] if tail and pad >= 0 else None     # -1: tail left unwritten
+            pad = max(pad, 0)
             for choice in (0, 5):
                 assert kern.lib.deepep_set_kernel_choice(choice) == 0
                 us = timeit(lambda: kern.combine_reduce(MODE_LOCAL, y, pk[:, :H], n_recv, table=table_a, row_weights=w,
-                                                        wtable=table_a if tail else None, wsrc=w if tail else None,
+                                                        wtable=table_a if pkw is not None else None,
+                                                        wsrc=w if pkw is not None else None,
                                                         out_weights=pkw, weights_pad=pad, stream=s), s)
                 print(json.dumps(dict(phase='A_stride', row_bytes=(H + tail) * 2, weights_pad=pad,
+                                      weights_written=pkw is not None,
                                       kernel=('item', 'item_persistent')[choice // 5],
                                       round=rnd, us=round(us, 1), gbps=round(bytes_a / us / 1e3, 1))), flush=True)
             del pk

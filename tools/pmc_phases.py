@@ -73,15 +73,15 @@ def main():
     table_a[ii, kk] = pos.to(torch.int32)
     y8 = torch.randn((n_exp, H), device='cuda', generator=g).to(torch.bfloat16)
     w8 = torch.rand((n_exp,), device='cuda', generator=g)
-    packed8 = torch.empty((n_recv, H + 16), dtype=torch.bfloat16, device='cuda')
+    packed8 = torch.empty((n_recv, H + 64), dtype=torch.bfloat16, device='cuda')   # the library's packed rows
     pw = packed8[:, H:].view(torch.float32)[:, :K]
     for _ in range(3):
         flush.zero_()
         kern.combine_reduce(MODE_LOCAL, y8, packed8[:, :H], n_recv, table=table_a, row_weights=w8, wtable=table_a,
-                            wsrc=w8, out_weights=pw)
+                            wsrc=w8, out_weights=pw, weights_pad=32)
     meta_out['local'] = n_exp * H * 2 + n_recv * (H * 2 + K * 4)
     table_b, _, back = epilogue_tables(idx8[0], E, R)
-    recv = torch.randn((sum(back), H + 16), device='cuda', generator=g).to(torch.bfloat16)
+    recv = torch.randn((sum(back), H + 64), device='cuda', generator=g).to(torch.bfloat16)
     for _ in range(3):
         flush.zero_()
         kern.combine_reduce(MODE_EPILOGUE, recv[:, :H], out, T, table=table_b)

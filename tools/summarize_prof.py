@@ -66,7 +66,9 @@ def pmc_phases(out, meta_json, *paths):
     algo = json.load(open(meta_json))
 
     def kind(name):
-        if 'copy_kernel' in name:
+        # the dispatch copy is `copy_kernel(...)`; torch's dtype conversions (`..._copy_kernel_cuda`) also
+        # contain the substring, and counting them as the copy gave round 1's "anomaly"
+        if name.startswith('copy_kernel('):
             return 'copy'
         if 'combine_rows_kernel<2' in name:
             return 'fused'
@@ -78,13 +80,17 @@ def pmc_phases(out, meta_json, *paths):
     per = defaultdict(lambda: defaultdict(list))
     for p in paths:
         for r in csv.DictReader(open(p)):
-            k = kind(r.get('Kernel_Name', '').replace('(anonymous namespace)::', ''))
+            k = kind(r.get('Kernel_Name', '').replace('(anonymous namespace)::', '').lstrip())
             if k is not None:
                 per[k][r['Counter_Name']].append(float(r['Counter_Value']))
     res = {}
     for k, counters in per.items():
         avg = {c: sum(v) / len(v) for c, v in counters.items()}
-        e = {'counters_avg_per_launch': avg, 'algorithmic_bytes_per_launch': algo[k], 'build_id': _build_id()}
+        e = {'counters_avg_per_launch': avg, 'algorithmic_bytes_per_launch': algo[k], 'build_id': _build_id(),
+             'launches': len(next(iter(counters.values())))}
+        if 'TCC_EA0_RDREQ_sum' in avg and 'TCC_EA0_WRREQ_64B_sum' in avg:
+            e['ea_read_bytes_per_launch (RDREQ x 128 B)'] = avg['TCC_EA0_RDREQ_sum'] * 128
+            e['ea_write_bytes_per_launch (WRREQ_64B x 64 B)'] = avg['TCC_EA0_WRREQ_64B_sum'] * 64
         if 'FETCH_SIZE' in avg and 'WRITE_SIZE' in avg:
             e['hbm_read_bytes_per_launch'] = 2 * avg['FETCH_SIZE'] * 1024
             e['hbm_write_bytes_per_launch'] = avg['WRITE_SIZE'] * 1024

@@ -376,7 +376,20 @@ combine_rows_kernel(const Params p) {
         if (it < items)
             combine_item<kMode, kWeighted, kVPT, kFull, kStoreAux, kGroup>(p, it, nchunks, nvec, lane, my_slot, my_w);
     };
-    if constexpr (kPersistent) {
+    if constexpr (kPersistent && !kLDS) {
+        // per-wave items, grid-stride, with the NEXT item's slots loading while this item's rows are
+        // gathered: a wave never waits on a slot-table load between two rounds of row loads
+        const int64_t stride = static_cast<int64_t>(gridDim.x) * kWaves;
+        int64_t it = static_cast<int64_t>(blockIdx.x) * kWaves + wave;
+        int32_t next = (it < items && lane < width) ? load_slot(it / nchunks, lane) : -1;
+        for (; it < items; it += stride) {
+            const int32_t my_slot = next;
+            float my_w = 0.0f;
+            if constexpr (kWeighted) my_w = my_slot >= 0 ? p.row_weights[my_slot] : 0.0f;
+            next = (it + stride < items && lane < width) ? load_slot((it + stride) / nchunks, lane) : -1;
+            combine_item<kMode, kWeighted, kVPT, kFull, kStoreAux, kGroup>(p, it, nchunks, nvec, lane, my_slot, my_w);
+        }
+    } else if constexpr (kPersistent) {
         for (int64_t vb = blockIdx.x; vb < nblocks; vb += gridDim.x) block(vb);
     } else {
         block(blockIdx.x);                          // one virtual block per workgroup

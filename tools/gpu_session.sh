@@ -40,6 +40,7 @@ for step in "$@"; do
                 run kplacetlb2 300 rocprofv3 --kernel-trace --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum GRBM_UTCL2_BUSY GRBM_GUI_ACTIVE -d $OUT/kplacetlb2 -o pmc --output-format csv -- python3 tools/kplace.py
                 unset KPLACE_ITERS KPLACE_WARM KPLACE_ROUNDS ;;
         kphase) run kphase 300 python tools/kphase.py ;;
+        profphase) run profphase 300 rocprofv3 --kernel-trace --stats -d $OUT/profphase -o prof --output-format csv -- python3 tools/kphase_prof.py ;;
         kcu)    run kcu 300 python tools/kcu.py ;;
         cumask) run cumask 120 python tools/probe_cumask.py ;;
         probeld) run probeld 300 python tools/probe_ld.py ;;

@@ -384,7 +384,13 @@ class ElasticBuffer(ExchangeMixin):
                  do_expand: bool = False,
                  do_zero_padding: bool = False,
                  use_tma_aligned_col_major_sf: bool = False):
-        """Dispatch tokens to the ranks owning their experts (elastic.py:855-1033 contract)."""
+        """Dispatch tokens to the ranks owning their experts (elastic.py:855-1033 contract).
+
+        A fresh handle costs one host sync (the notify counts, as the reference's do_cpu_sync=True);
+        with do_cpu_sync=False the outputs are padded to the worst case as the reference's, but this
+        build still syncs once (the RCCL all-to-all needs host split sizes).  A cached handle
+        (`handle=...`) needs no sync.  The notify also carries per-64-token-block counts, so the
+        handle's combines never sync."""
         num_topk = (handle.topk_idx if topk_idx is None else topk_idx).shape[1]
         num_sms = self.get_theoretical_num_sms(num_experts or handle.num_experts, num_topk) if num_sms == 0 else num_sms
         num_qps = self.get_theoretical_num_qps(num_sms) if num_qps == 0 else num_qps

@@ -97,6 +97,7 @@ SIGNATURES = {
     'deepep_sym_wait': (_I, [_P, _I, _I, _I, _I64, _I64, _P, _P]),
     'deepep_stream_create_cu_budget': (_I, [_I, ctypes.POINTER(ctypes.c_void_p)]),
     'deepep_stream_destroy': (_I, [_P]),
+    'deepep_stream_probe_cus': (_I, [_P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     'deepep_combine_reduce_scatter': (_I, [_I, _P, _I64, _I64, _P, _I64, _I, _P, _P, _I, _I, _P, _I64, _P, _I,
                                            _I64, _I, _P, _P]),
 }

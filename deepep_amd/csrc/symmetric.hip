@@ -199,6 +199,47 @@ int deepep_stream_create_cu_budget(int num_cus, deepep_stream_t* stream) {
     return DEEPEP_OK;
 }
 
+namespace {
+// Where the workgroups of a stream run (diagnostic for CU budgets): HW_REG_HW_ID and HW_REG_XCC_ID of
+// every workgroup's first lane.
+__global__ void where_kernel(uint32_t* out, int spin) {
+    if (threadIdx.x != 0) return;
+    const uint32_t hw = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));
+    const uint32_t xcc = __builtin_amdgcn_s_getreg(20 | (0 << 6) | (15 << 11));
+    for (volatile int i = 0; i < spin; ++i) {}
+    out[2 * blockIdx.x] = hw;
+    out[2 * blockIdx.x + 1] = xcc;
+}
+}  // namespace
+
+int deepep_stream_probe_cus(deepep_stream_t stream, int* num_cus, int* num_xcds) {
+    if (num_cus == nullptr || num_xcds == nullptr) return deepep_amd_set_error(DEEPEP_ERR_INVALID_ARG, "probe_cus: null");
+    constexpr int kBlocks = 8192;
+    uint32_t* d = nullptr;
+    hipError_t e = hipMalloc(&d, sizeof(uint32_t) * 2 * kBlocks);
+    if (e != hipSuccess) return hip_fail(e, "hipMalloc(probe)");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(where_kernel, dim3(kBlocks), dim3(64), 0, s, d, 2000);
+    static uint32_t h[2 * kBlocks];
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    (void)hipFree(d);
+    if (e != hipSuccess) return hip_fail(e, "probe_cus");
+    bool seen[16][8][2][16] = {};            // (xcc, se, sh, cu)
+    bool xcds[16] = {};
+    int n = 0, x = 0;
+    for (int i = 0; i < kBlocks; ++i) {
+        const uint32_t hw = h[2 * i], xcc = h[2 * i + 1] & 0xF;
+        const uint32_t cu = (hw >> 8) & 0xF, sh = (hw >> 12) & 0x1, se = (hw >> 13) & 0x7;
+        if (!seen[xcc][se][sh][cu]) { seen[xcc][se][sh][cu] = true; ++n; }
+        if (!xcds[xcc]) { xcds[xcc] = true; ++x; }
+    }
+    *num_cus = n;
+    *num_xcds = x;
+    return DEEPEP_OK;
+}
+
 int deepep_stream_destroy(deepep_stream_t stream) {
     if (stream == nullptr) return DEEPEP_OK;
     deepep_amd_register_budget(stream, 0);

@@ -333,6 +333,9 @@ int deepep_combine_reduce_scatter(int weighted,
  * grid with it, csrc/kernels/elastic/combine.hpp:135, elastic.py:1086-1088). */
 int deepep_stream_create_cu_budget(int num_cus, deepep_stream_t* stream);
 int deepep_stream_destroy(deepep_stream_t stream);
+/* Diagnostic: how many distinct CUs (and XCDs) a stream's workgroups run on (8192 one-wave workgroups
+ * recording their hardware ids; synchronises the stream). */
+int deepep_stream_probe_cus(deepep_stream_t stream, int* num_cus, int* num_xcds);
 
 /* ElasticBuffer::get_combine_buffer_size for one node (num_scaleout_ranks == 1). */
 int64_t deepep_combine_buffer_size(int num_max_tokens_per_rank, int hidden, int num_topk,

@@ -160,3 +160,36 @@ def test_stream_modes_ep4_pipelined(monkeypatch):
     assert len(results) == world, results
     bad = {r: f for r, f in results.items() if f}
     assert not bad, bad
+
+
+@pytest.mark.parametrize('num_sms,expect_cus', [(4, 8), (8, 8), (12, 16), (64, 64)])
+def test_cu_budget_is_honoured_and_bitwise(num_sms, expect_cus):
+    """An explicit num_sms is rounded up to whole CUs per XCD (a CU mask without bits on an XCD would
+    leave that XCD unrestricted): the budget stream's workgroups run on exactly that many CUs, spread
+    over all 8 XCDs; the combine on it -- from the default stream, and issued from the budget stream
+    itself (no stream hops) -- is bitwise the whole-chip combine."""
+    import ctypes
+    import torch.distributed as dist
+    from deepep_amd import ElasticBuffer
+    if not dist.is_initialized():
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        os.environ.setdefault('MASTER_PORT', '29563')
+        dist.init_process_group('gloo', rank=0, world_size=1)
+    T, H, K, E = 512, 2048, 8, 64
+    g = torch.Generator(device='cuda').manual_seed(num_sms)
+    w, idx = torch.topk(torch.rand((T, E), device='cuda', generator=g), K, dim=-1, sorted=False)
+    buf = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=T, hidden=H, num_topk=K)
+    _, _, ex_w, handle, _ = buf.dispatch(torch.zeros((T, H), dtype=torch.bfloat16, device='cuda'),
+                                         topk_idx=idx.to(torch.int64), topk_weights=w, num_experts=E, do_expand=True)
+    y = torch.randn((handle.num_expanded_tokens, H), device='cuda', generator=g).to(torch.bfloat16)
+    ref, ref_w, _ = buf.combine(y, handle, topk_weights=ex_w, apply_topk_weights=True)
+    bs = buf.get_cu_budget_stream(num_sms)
+    n, x = ctypes.c_int(), ctypes.c_int()
+    assert buf.kernels.lib.deepep_stream_probe_cus(ctypes.c_void_p(bs.cuda_stream), ctypes.byref(n), ctypes.byref(x)) == 0
+    assert (n.value, x.value) == (expect_cus, 8), (n.value, x.value)
+    out, out_w, _ = buf.combine(y, handle, topk_weights=ex_w, apply_topk_weights=True, num_sms=num_sms)
+    with torch.cuda.stream(bs):
+        out2, out2_w, _ = buf.combine(y, handle, topk_weights=ex_w, apply_topk_weights=True, num_sms=num_sms)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref) and torch.equal(out_w, ref_w)
+    assert torch.equal(out2, ref) and torch.equal(out2_w, ref_w)

@@ -387,3 +387,79 @@ def test_lost_peer_times_out_instead_of_hanging():
     finally:
         sym.destroy()
         _lib.check(lib.deepep_sym_free(dead), 'sym_free')
+
+
+def _full_worker(rank, world, port, queue):
+    """BASELINE config 3 at full size over the xGMI transport: 8 processes sharing the GPU, HIP-IPC
+    windows, the pipelined combine (4 chunks) -- against the RCCL-path combine of the same handle and
+    inputs (the RCCL path is checked against the oracle at this size in tests/test_fullsize_gpu.py)."""
+    sys.path.insert(0, ROOT)
+    try:
+        os.environ['MASTER_ADDR'] = '127.0.0.1'
+        os.environ['MASTER_PORT'] = str(port)
+        import torch.distributed as dist
+        torch.cuda.set_device(0)
+        dist.init_process_group('gloo', rank=rank, world_size=world)
+        from deepep_amd import ElasticBuffer
+        dev = torch.device('cuda', 0)
+        T, H, K, E = 8192, 7168, 8, 256
+        g = torch.Generator(device=dev).manual_seed(500 + rank)
+        w, idx = torch.topk(torch.rand((T, E), device=dev, generator=g), K, dim=-1, sorted=False)
+        idx = idx.to(torch.int64)
+        x = torch.randn((T, H), device=dev, generator=g).to(torch.bfloat16)
+        bias = torch.randn((T, H), device=dev, generator=g).to(torch.bfloat16)
+        bufs = {}
+        for transport in ('xgmi', 'rccl'):
+            os.environ['DEEPEP_TRANSPORT'] = transport
+            bufs[transport] = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=T, hidden=H, num_topk=K,
+                                            explicitly_destroy=True, num_gpu_timeout_secs=60)
+        failures = []
+        ex_x, _, ex_w, handle, _ = bufs['xgmi'].dispatch(x, topk_idx=idx, topk_weights=w, num_experts=E,
+                                                         do_expand=True)
+        _, _, ex_w_r, handle_r, _ = bufs['rccl'].dispatch(x, topk_idx=idx, topk_weights=w, num_experts=E,
+                                                          do_expand=True)
+        if not torch.equal(handle.recv_src_metadata, handle_r.recv_src_metadata) or not torch.equal(ex_w, ex_w_r):
+            failures.append('xgmi dispatch != rccl dispatch')
+        y = torch.randn((handle.num_expanded_tokens, H), device=dev, generator=g).to(torch.bfloat16)
+        for weighted in (False, True):
+            b = None if weighted else bias
+            outs = {t: bf.combine(y, handle, topk_weights=ex_w, bias=b, apply_topk_weights=weighted)
+                    for t, bf in bufs.items()}
+            torch.cuda.synchronize()
+            if bufs['xgmi']._num_chunks(handle) < 2:
+                failures.append('not pipelined')
+            if not torch.equal(outs['xgmi'][0], outs['rccl'][0]):
+                failures.append(f'weighted={weighted}: xgmi combined_x != rccl')
+            if not (torch.equal(outs['xgmi'][1], w) and torch.equal(outs['rccl'][1], w)):
+                failures.append(f'weighted={weighted}: weight pass-through')
+        bufs['xgmi']._sym.check()
+        for bf in bufs.values():
+            bf.destroy()
+        queue.put((rank, failures))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:
+        queue.put((rank, [traceback.format_exc()]))
+
+
+def test_xgmi_transport_full_size_config3():
+    world = 8
+    ctx = mp.get_context('spawn')
+    queue = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_full_worker, args=(r, world, port, queue)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = {}
+    try:
+        for _ in range(world):
+            rank, failures = queue.get(timeout=160)
+            results[rank] = failures
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    if len(results) != world or any(results.values()):
+        tails = {r: [f[-1500:] for f in fl] for r, fl in results.items()}
+        pytest.fail(f'{len(results)}/{world} ranks reported; failures: {tails}', pytrace=False)

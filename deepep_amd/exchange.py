@@ -197,11 +197,8 @@ class ExchangeMixin:
         source-token chunks like the RCCL path: phase A of chunk c is followed by a signal on split
         barrier c, and phase B of chunk c runs on a second stream behind the wait for every rank's
         signal c, so it overlaps phase A of the later chunks."""
-        R, r = self.num_ranks, self.rank_idx
         T_max = handle.num_max_tokens_per_rank
-        T = handle.topk_idx.shape[0]
-        rank_layout = R <= K                              # use_rank_layout, combine_utils.cuh:8-13
-        self._window_slots = min(R, K)
+        self._window_slots = min(self.num_ranks, K)       # rank layout when R <= K (combine_utils.cuh:8-13)
         row_bytes, w_off, w_pad = packed_row_layout(hidden, K)     # the weight tail is always reserved
         sym = self._window(row_bytes, rows_per_slot=T_max)
         num_chunks = min(self._num_chunks(handle), 63)
@@ -264,9 +261,7 @@ class ExchangeMixin:
         k * T_max + t (per-top-k slot layout, buffer.hpp:616-633), then one EPILOGUE reduce per token
         over its K rows (weighted: the legacy low-latency fma chain).  Chunked by source token like
         _combine_xgmi, phase B of chunk c behind the split barrier of chunk c."""
-        R, r = self.num_ranks, self.rank_idx
         T_max = handle.num_max_tokens_per_rank
-        T = handle.topk_idx.shape[0]
         with_w = topk_weights is not None
         self._window_slots = K
         # the weight tail is always reserved: one window size per buffer

@@ -6,7 +6,7 @@ same tables from their definitions with plain torch on the CPU, straight from th
 addressing rules, so that
 
 * tests/oracle_kernels.py can run the whole EP > 1 host orchestration on gloo ranks without a GPU,
-* tests/test_plan_gpu.py can check the HIP plan kernels against it bit for bit.
+* tests/test_sync_free_gpu.py can check the HIP plan kernels against it bit for bit.
 
 Reference rules restated (paths in /root/reference):
 * the partial of received token i goes to its source rank's receive slot
@@ -48,8 +48,7 @@ def route_block_counts(topk_idx, num_experts, num_ranks, num_blocks):
 def _positions(unit_src, unit_chunk, counts, R, interleave):
     """Unit index of every unit (given in receive order) inside the concatenated chunk tables:
     chunk base + position inside the chunk (grouped by source rank, or round-robin)."""
-    n = unit_src.numel()
-    C = counts.shape[0]                                        # counts [C, R]
+    n = unit_src.numel()                                       # counts: [chunks, R]
     base = torch.cumsum(counts.sum(dim=1), 0) - counts.sum(dim=1)
     # p = rank of the unit among the units of its (source, chunk) group, in receive order
     key = unit_chunk * R + unit_src

@@ -72,7 +72,7 @@ def test_plan_kernels_match_reference(kern, world, K, T, chunks):
     from deepep_amd import _lib
     from deepep_amd.handle import chunk_geometry
     E = world * max(2, (K + world - 1) // world + 1)
-    rng, idx_all, _ = _routing(world, T, K, E, seed=world * 100 + K)
+    _, idx_all, _ = _routing(world, T, K, E, seed=world * 100 + K)
     nb, bpc, _ = chunk_geometry(T, chunks)
     disp = oracle.simulate_dispatch(idx_all, E, T)
     # per-source block counts: HIP vs the restatement
@@ -275,7 +275,7 @@ def _ordering_rank(rank, world, T, H, K, E, comm, drop_wait, results):
             real = buf._a2a_async
 
             def no_wait(out, inp, os_, is_):
-                work = real(out, inp, os_, is_)
+                real(out, inp, os_, is_)                 # the exchange still runs, on its own stream
                 return sim.Work(torch.cuda.Event())      # never recorded: waiting on it orders nothing
             buf._a2a_async = no_wait
         comm.delay_cycles = 20_000_000                  # the exchange lands ~10 ms after it is queued

@@ -494,7 +494,9 @@ class ElasticBuffer(ExchangeMixin):
                                          [b[:nb] for b in recv_blk], [b[nb:] for b in recv_blk],
                                          torch.cat([blk, rb]).contiguous())
                 if offs is not None:
-                    peer_offsets = torch.tensor(offs, dtype=torch.int32).to(dev, non_blocking=True)
+                    # pinned source: an asynchronous copy from a pageable temporary may read it after it
+                    # is freed (garbage offsets -> rows pushed into the wrong window rows)
+                    peer_offsets = torch.tensor(offs, dtype=torch.int32).pin_memory().to(dev, non_blocking=True)
                 recv_counts_t = recv_notify[:, 0].contiguous()
                 send_offsets = (torch.cumsum(send_counts, 0) - send_counts).to(torch.int32)
             N = sum(recv_counts_l)

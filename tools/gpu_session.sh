@@ -49,10 +49,10 @@ for step in "$@"; do
         bench4gloo) export DEEPEP_BENCH_BACKEND=gloo; run bench4gloo 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29657 bench.py --gpus 4 --steps 4 --warmup 2; unset DEEPEP_BENCH_BACKEND ;;
         bench2gloo) export DEEPEP_BENCH_BACKEND=gloo; run bench2gloo 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29655 bench.py --gpus 2 --steps 10 --warmup 3; unset DEEPEP_BENCH_BACKEND ;;
         pmc)    for c in FETCH_SIZE WRITE_SIZE TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum; do
-                    run pmc_$c 600 rocprofv3 --pmc $c -d $OUT/pmc_$c -o pmc --output-format csv -- python3 tools/pmc_run.py
+                    run pmc_$c 300 timeout -s KILL 120 rocprofv3 --pmc $c -d $OUT/pmc_$c -o pmc --output-format csv -- python3 tools/pmc_run.py
                 done ;;
         pmcphases) for c in FETCH_SIZE WRITE_SIZE; do
-                    run pmcph_$c 300 rocprofv3 --pmc $c -d $OUT/pmcph_$c -o pmc --output-format csv -- python3 tools/pmc_phases.py
+                    run pmcph_$c 300 timeout -s KILL 120 rocprofv3 --pmc $c -d $OUT/pmcph_$c -o pmc --output-format csv -- python3 tools/pmc_phases.py
                 done ;;
         pmccal) # request-size calibration of every phase kernel (incl. the dispatch copy): 3 passes
                 run pmccal_ws 300 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE TCC_EA0_WRREQ_sum -d $OUT/pmccal_ws -o pmc --output-format csv -- python3 tools/pmc_phases.py
@@ -63,7 +63,7 @@ for step in "$@"; do
                 run pmccopy_rq 300 timeout -s KILL 120 rocprofv3 --pmc TCC_EA0_WRREQ_64B_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_DRAM_sum TCC_EA0_RDREQ_DRAM_sum -d $OUT/pmccopy_rq -o pmc --output-format csv -- python3 tools/pmc_copycal.py
                 run pmccopy_fs 300 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmccopy_fs -o pmc --output-format csv -- python3 tools/pmc_copycal.py ;;
         pmcplain) for c in FETCH_SIZE WRITE_SIZE; do
-                    run pmcp_$c 600 rocprofv3 --pmc $c -d $OUT/pmcp_$c -o pmc --output-format csv -- python3 tools/pmc_run.py --plain
+                    run pmcp_$c 300 timeout -s KILL 120 rocprofv3 --pmc $c -d $OUT/pmcp_$c -o pmc --output-format csv -- python3 tools/pmc_run.py --plain
                 done ;;
         probe)  run probe 600 python tools/probe.py ;;
         *) echo "unknown step $step" ;;

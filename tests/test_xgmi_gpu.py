@@ -429,18 +429,28 @@ def _full_worker(rank, world, port, queue):
             if bufs['xgmi']._num_chunks(handle) < 2:
                 failures.append('not pipelined')
             if not torch.equal(outs['xgmi'][0], outs['rccl'][0]):
+                flag = int(bufs['xgmi']._sym.error_flag.item())
+                bufs['xgmi']._sym.error_flag.zero_()
+                bufs['xgmi']._sym._flag_event = None
                 again = {t: bf.combine(y, handle, topk_weights=ex_w, bias=b, apply_topk_weights=weighted)[0]
                          for t, bf in bufs.items()}
                 torch.cuda.synchronize()
                 rows = (outs['xgmi'][0].float() != outs['rccl'][0].float()).any(dim=1)
+                per_chunk = [int(rows[c * 2048:(c + 1) * 2048].sum()) for c in range(T // 2048)]
                 failures.append(f'weighted={weighted}: xgmi combined_x != rccl on {int(rows.sum())} rows '
-                                f'(blocks {sorted(set((rows.nonzero().flatten() // 64).tolist()))[:8]}); '
+                                f'(per 2048-token chunk {per_chunk}); '
                                 f'repeated: xgmi stable {torch.equal(again["xgmi"], outs["xgmi"][0])}, '
-                                f'rccl stable {torch.equal(again["rccl"], outs["rccl"][0])}')
+                                f'rccl stable {torch.equal(again["rccl"], outs["rccl"][0])}, '
+                                f'repeated xgmi == rccl {torch.equal(again["xgmi"], again["rccl"])}, '
+                                f'error flag after the first combine {flag}, after the repeat '
+                                f'{int(bufs["xgmi"]._sym.error_flag.item())}')
             for t in bufs:
                 if not torch.equal(outs[t][1], w):
-                    failures.append(f'weighted={weighted}: {t} weight pass-through on '
-                                    f'{int((outs[t][1] != w).any(dim=1).sum())} tokens')
+                    bad_t = (outs[t][1] != w).any(dim=1).nonzero().flatten()
+                    t0 = int(bad_t[0])
+                    failures.append(f'weighted={weighted}: {t} weight pass-through on {bad_t.numel()} tokens, '
+                                    f'first {bad_t[:4].tolist()}; token {t0} got {outs[t][1][t0].tolist()} '
+                                    f'expected {w[t0].tolist()} routed to ranks {(idx[t0] // (E // 8)).tolist()}')
         bufs['xgmi']._sym.check()
         for bf in bufs.values():
             bf.destroy()

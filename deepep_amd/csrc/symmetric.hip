@@ -10,10 +10,11 @@
 // rank, exported with hipIpcGetMemHandle and opened by every peer with hipIpcOpenMemHandle; the
 // fabric (xGMI) makes the peer's HBM load/store addressable from kernels.  Uncached (MTYPE UC)
 // memory is used because a peer's stores land in this GPU's HBM behind its L2; nothing of the
-// window is ever cached, so no invalidation protocol is needed between the writers' kernels and
-// the reader's.  The barrier is a one-workgroup kernel: thread s publishes `epoch` into rank s's
-// flag slot [rank] with a system-scope release store and then waits, with a system-scope acquire
-// load, until its own slot [s] reaches `epoch`.  Epochs only grow, so flags never need resetting;
+// window should ever be cached; measured, one-XCD fences were not enough (below), so a publishing
+// launch first writes back the L2 of every XCD and a barrier / wait ends by invalidating every
+// XCD's L2 (writeback_all_xcds, invalidate_all_xcds).  Then thread s of the last workgroup publishes `epoch` into
+// rank s's flag slot [rank] with a system-scope release store and waits, with a system-scope
+// acquire load, until its own slot [s] reaches `epoch`.  Epochs only grow, so flags never need resetting;
 // they are counted on the device, so the barriers replay correctly inside a captured HIP graph.
 // A wall-clock timeout (the reference's num_gpu_timeout_secs, comm.cuh:30-54) sets bit 2 of the
 // error flag and lets the kernel finish instead of trapping, so a lost peer never hangs the GPU.
@@ -36,10 +37,34 @@ int hip_fail(hipError_t e, const char* what) {
 
 // Epochs counted on the device (argument <= 0): the next epoch comes from this rank's own counter
 // in its window header, so a captured HIP graph replays with fresh epochs.  Counter table: int64
-// [2][kSlots] after the flag table -- row 0 = publishes per slot (barrier = slot 0, signals),
-// row 1 = waits per slot.  Only the launching kernel touches its counter (one thread, one
-// stream-ordered kernel at a time per slot).
+// [3][kSlots] after the flag table -- row 0 = publishes per slot (barrier = slot 0, signals),
+// row 1 = waits per slot, row 2 = workgroup arrivals of the publishing launches (below).  Only the
+// launching kernel touches its counters (one stream-ordered kernel at a time per slot).
 constexpr int kSlots = DEEPEP_SYM_FLAG_SLOTS;
+
+// Every XCD takes part in a hand-off.  Publishing launches (barrier, signal) run kXcdGroups
+// workgroups -- dealt round-robin over the 8 XCDs, so every XCD gets some: each writes back its
+// XCD's L2 at system scope and waits for it, then counts its arrival, and the last to arrive
+// publishes.  After a barrier or a wait, kXcdGroups workgroups invalidate every XCD's L2 before the
+// stream's next kernel reads the window.  A single-workgroup fence covers one XCD only.  Evidence
+// (tests/test_xgmi_gpu.py config 3 after the 8-process test, 8 processes sharing one GPU): with
+// the one-XCD fences about one first dispatch / combine in five read stale rows; with the
+// write-back alone 1 in 14; with write-back and invalidate 0 in 10, as with host-synchronised
+// hand-offs (0 in 18).
+constexpr int kXcdGroups = 64;
+
+__device__ __forceinline__ bool writeback_all_xcds(const uint64_t* peer_flags, int rank, int slot) {
+    __shared__ int s_last;
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");                 // buffer_wbl2 sc0 sc1
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        int64_t* join = reinterpret_cast<int64_t*>(peer_flags[rank]) + kSlots * 64 + 2 * kSlots + slot;
+        const int64_t arrived = __hip_atomic_fetch_add(join, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1;
+        s_last = arrived % static_cast<int64_t>(gridDim.x) == 0;
+    }
+    __syncthreads();
+    return s_last != 0;
+}
 
 __device__ __forceinline__ int64_t next_epoch(const uint64_t* peer_flags, int rank, int row, int slot, int64_t given) {
     __shared__ int64_t s_epoch;
@@ -71,6 +96,7 @@ __device__ __forceinline__ void wait_slots(const int64_t* mine, int s, int64_t e
 __global__ void __launch_bounds__(64)
 sym_barrier_kernel(const uint64_t* peer_flags, int rank, int num_ranks, int64_t epoch, int64_t timeout_ticks,
                    int32_t* error_flag) {
+    if (!writeback_all_xcds(peer_flags, rank, 0)) return;
     epoch = next_epoch(peer_flags, rank, 0, 0, epoch);
     const int s = static_cast<int>(threadIdx.x);
     if (s >= num_ranks) return;
@@ -86,6 +112,7 @@ sym_barrier_kernel(const uint64_t* peer_flags, int rank, int num_ranks, int64_t 
 // table.  Flag table of a window: int64 [kSlots][64], slot 0 is the full barrier above.
 __global__ void __launch_bounds__(64)
 sym_signal_kernel(const uint64_t* peer_flags, int rank, int num_ranks, int slot, int64_t value) {
+    if (!writeback_all_xcds(peer_flags, rank, slot)) return;
     value = next_epoch(peer_flags, rank, 0, slot, value);
     const int s = static_cast<int>(threadIdx.x);
     if (s >= num_ranks) return;
@@ -103,6 +130,20 @@ sym_wait_kernel(const uint64_t* peer_flags, int rank, int num_ranks, int slot, i
     wait_slots(reinterpret_cast<const int64_t*>(peer_flags[rank]) + static_cast<int64_t>(slot) * 64, s, value,
                timeout_ticks, error_flag);
     __threadfence_system();
+}
+
+// After a barrier or a wait: every XCD invalidates its L2 (system scope) before the stream's next
+// kernel reads what the peers stored into this rank's window (one extra small launch).
+__global__ void __launch_bounds__(64) invalidate_all_xcds_kernel() {
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");                 // buffer_inv sc0 sc1
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+}
+
+hipError_t invalidate_all_xcds(hipStream_t s) {
+    hipLaunchKernelGGL(invalidate_all_xcds_kernel, dim3(kXcdGroups), dim3(64), 0, s);
+    return hipGetLastError();
 }
 
 int64_t timeout_ticks(int64_t timeout_us, int* rc) {
@@ -254,9 +295,10 @@ int deepep_sym_barrier(const uint64_t* peer_flags, int rank, int num_ranks, int6
     int rc = DEEPEP_OK;
     const int64_t ticks = timeout_ticks(timeout_us, &rc);
     if (rc != DEEPEP_OK) return rc;
-    hipLaunchKernelGGL(sym_barrier_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream),
+    hipLaunchKernelGGL(sym_barrier_kernel, dim3(kXcdGroups), dim3(64), 0, reinterpret_cast<hipStream_t>(stream),
                        peer_flags, rank, num_ranks, epoch, ticks, error_flag);
-    const hipError_t e = hipGetLastError();
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = invalidate_all_xcds(reinterpret_cast<hipStream_t>(stream));
     return e == hipSuccess ? DEEPEP_OK : hip_fail(e, "barrier launch");
 }
 
@@ -265,7 +307,7 @@ int deepep_sym_signal(const uint64_t* peer_flags, int rank, int num_ranks, int s
     if (peer_flags == nullptr || num_ranks < 1 || num_ranks > 64 || rank < 0 || rank >= num_ranks || slot < 1 ||
         slot >= DEEPEP_SYM_FLAG_SLOTS)
         return deepep_amd_set_error(DEEPEP_ERR_INVALID_ARG, "sym_signal: bad arguments");
-    hipLaunchKernelGGL(sym_signal_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream),
+    hipLaunchKernelGGL(sym_signal_kernel, dim3(kXcdGroups), dim3(64), 0, reinterpret_cast<hipStream_t>(stream),
                        peer_flags, rank, num_ranks, slot, value);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? DEEPEP_OK : hip_fail(e, "signal launch");
@@ -281,7 +323,8 @@ int deepep_sym_wait(const uint64_t* peer_flags, int rank, int num_ranks, int slo
     if (rc != DEEPEP_OK) return rc;
     hipLaunchKernelGGL(sym_wait_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream),
                        peer_flags, rank, num_ranks, slot, value, ticks, error_flag);
-    const hipError_t e = hipGetLastError();
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = invalidate_all_xcds(reinterpret_cast<hipStream_t>(stream));
     return e == hipSuccess ? DEEPEP_OK : hip_fail(e, "wait launch");
 }
 

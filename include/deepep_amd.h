@@ -287,8 +287,10 @@ int deepep_sym_import(const void* handle, void** ptr);      /* a peer's window, 
 int deepep_sym_close(void* ptr);
 
 /* Group barrier on the stream: peer_flags (device, uint64 [num_ranks]) holds the address of every
- * rank's window header (int64 flag table [DEEPEP_SYM_FLAG_SLOTS][64], then int64 epoch counters
- * [2][DEEPEP_SYM_FLAG_SLOTS]; DEEPEP_SYM_HEADER_BYTES in all, zero at allocation).  Rank r stores
+ * rank's window header (int64 flag table [DEEPEP_SYM_FLAG_SLOTS][64], then int64 counters
+ * [3][DEEPEP_SYM_FLAG_SLOTS]: publishes, waits, workgroup arrivals; DEEPEP_SYM_HEADER_BYTES in all,
+ * zero at allocation).  Every XCD's L2 is first written back (the stores into peer windows before
+ * the call may sit in any of them).  Rank r then stores
  * the epoch into entry [r] of slot 0 of every rank's table (system-scope release) and waits until
  * its own entries all reach it (system-scope acquire).  epoch <= 0: the next epoch is counted on
  * the device (this rank's counter), so a captured HIP graph replays with fresh epochs -- use it

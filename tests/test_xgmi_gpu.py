@@ -469,15 +469,25 @@ def test_xgmi_transport_full_size_config3():
     procs = [ctx.Process(target=_full_worker, args=(r, world, port, queue)) for r in range(world)]
     for p in procs:
         p.start()
+    import queue as queue_mod
+    import time
     results = {}
+    deadline = time.time() + 150
     try:
-        for _ in range(world):
-            rank, failures = queue.get(timeout=150)
+        while len(results) < world and time.time() < deadline:
+            try:
+                rank, failures = queue.get(timeout=5)
+            except queue_mod.Empty:
+                # a rank that died without reporting (its peers would wait out their barriers)
+                dead = {r: [f'exited with code {p.exitcode} before reporting'] for r, p in enumerate(procs)
+                        if p.exitcode is not None and r not in results}
+                if dead:
+                    results.update(dead)
+                    break
+                continue
             results[rank] = failures
             if failures:              # the other ranks may now wait out their barriers: stop early
                 break
-    except Exception:                 # noqa: BLE001 -- a rank that never reports is itself the failure
-        pass
     finally:
         for p in procs:
             p.join(timeout=2 if len(results) != world or any(results.values()) else 30)

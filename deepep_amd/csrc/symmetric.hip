@@ -49,7 +49,7 @@ constexpr int kSlots = DEEPEP_SYM_FLAG_SLOTS;
 // stream's next kernel reads the window.  A single-workgroup fence covers one XCD only.  Evidence
 // (tests/test_xgmi_gpu.py config 3 after the 8-process test, 8 processes sharing one GPU): with
 // the one-XCD fences about one first dispatch / combine in five read stale rows; with the
-// write-back alone 1 in 14; with write-back and invalidate 0 in 10, as with host-synchronised
+// write-back alone 1 in 14; with write-back and invalidate 0 in 22, as with host-synchronised
 // hand-offs (0 in 18).
 constexpr int kXcdGroups = 64;
 

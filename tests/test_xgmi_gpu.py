@@ -400,6 +400,7 @@ def _full_worker(rank, world, port, queue):
         import torch.distributed as dist
         torch.cuda.set_device(0)
         dist.init_process_group('gloo', rank=rank, world_size=world)
+        queue.put((rank, 'stage', 'gloo up'))
         from deepep_amd import ElasticBuffer
         dev = torch.device('cuda', 0)
         T, H, K, E = 8192, 7168, 8, 256
@@ -414,6 +415,7 @@ def _full_worker(rank, world, port, queue):
             bufs[transport] = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=T, hidden=H, num_topk=K,
                                             explicitly_destroy=True, num_gpu_timeout_secs=60)
         failures = []
+        queue.put((rank, 'stage', 'buffers built'))
         ex_x, _, ex_w, handle, _ = bufs['xgmi'].dispatch(x, topk_idx=idx, topk_weights=w, num_experts=E,
                                                          do_expand=True)
         _, _, ex_w_r, handle_r, _ = bufs['rccl'].dispatch(x, topk_idx=idx, topk_weights=w, num_experts=E,
@@ -421,11 +423,13 @@ def _full_worker(rank, world, port, queue):
         if not torch.equal(handle.recv_src_metadata, handle_r.recv_src_metadata) or not torch.equal(ex_w, ex_w_r):
             failures.append('xgmi dispatch != rccl dispatch')
         y = torch.randn((handle.num_expanded_tokens, H), device=dev, generator=g).to(torch.bfloat16)
+        queue.put((rank, 'stage', 'dispatched'))
         for weighted in (False, True):
             b = None if weighted else bias
             outs = {t: bf.combine(y, handle, topk_weights=ex_w, bias=b, apply_topk_weights=weighted)
                     for t, bf in bufs.items()}
             torch.cuda.synchronize()
+            queue.put((rank, 'stage', f'combined weighted={weighted}'))
             if bufs['xgmi']._num_chunks(handle) < 2:
                 failures.append('not pipelined')
             if not torch.equal(outs['xgmi'][0], outs['rccl'][0]):
@@ -471,12 +475,12 @@ def test_xgmi_transport_full_size_config3():
         p.start()
     import queue as queue_mod
     import time
-    results = {}
+    results, stages = {}, {}
     deadline = time.time() + 150
     try:
         while len(results) < world and time.time() < deadline:
             try:
-                rank, failures = queue.get(timeout=5)
+                msg = queue.get(timeout=5)
             except queue_mod.Empty:
                 # a rank that died without reporting (its peers would wait out their barriers)
                 dead = {r: [f'exited with code {p.exitcode} before reporting'] for r, p in enumerate(procs)
@@ -485,6 +489,10 @@ def test_xgmi_transport_full_size_config3():
                     results.update(dead)
                     break
                 continue
+            if len(msg) == 3:                 # progress marker
+                stages[msg[0]] = msg[2]
+                continue
+            rank, failures = msg
             results[rank] = failures
             if failures:              # the other ranks may now wait out their barriers: stop early
                 break
@@ -495,4 +503,5 @@ def test_xgmi_transport_full_size_config3():
                 p.kill()
     if len(results) != world or any(results.values()):
         tails = {r: [f[-1500:] for f in fl] for r, fl in results.items()}
-        pytest.fail(f'{len(results)}/{world} ranks reported; failures: {tails}', pytrace=False)
+        pytest.fail(f'{len(results)}/{world} ranks reported; last stage per rank {stages}; failures: {tails}',
+                    pytrace=False)

@@ -612,7 +612,7 @@ template <int kMode, bool kWeighted, int kVPT, bool kFull, int kAux>
 void launch_lds(const Params& p, bool lds, int waves, int group, hipStream_t stream) {
     const int nvec = p.hidden / 8;
     const int64_t items = static_cast<int64_t>(p.num_units) * ((nvec + 64 * kVPT - 1) / (64 * kVPT));
-    if constexpr (kAux == kAuxSC1) {
+    if constexpr (kAux == kAuxSC1 || kAux == kAuxSys) {
         if (lds) {
             if (waves == 8) {
                 if (group == 2) launch_shape<kMode, kWeighted, kVPT, kFull, kAux, true, 8, 2>(p, items, stream);
@@ -855,7 +855,10 @@ int launch_combine(int mode, int weighted, const Params& p_in, deepep_stream_t s
     sh.policy = p.out_rows != nullptr ? 3 : (g_config.store_policy >= 0 ? g_config.store_policy : 2);
     // units_per_block 4 / 8 forces the workgroup shape; 0 = automatic
     sh.waves = p.units_per_block == 4 ? 4 : (p.units_per_block == 8 ? 8 : (mode == DEEPEP_MODE_LOCAL ? 4 : 8));
-    sh.group = g_config.rows_in_flight > 0 ? g_config.rows_in_flight : 8;
+    // rows in flight per lane: 8 for the fused / epilogue reduces (8 rows per token at EP = 1), 4 for
+    // phase A (about 1.5 local rows per received token at EP = 8: 64 VGPRs and 8 waves per SIMD beat
+    // deeper per-wave loads, tools/kphase.py 252-254 vs 256-260 us, tools/kphase_cu.py)
+    sh.group = g_config.rows_in_flight > 0 ? g_config.rows_in_flight : (mode == DEEPEP_MODE_LOCAL ? 4 : 8);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     // A forced streaming kernel (one wave per unit, chunks pipelined) applies only when the shape is
     // automatic: an explicit units_per_block / LDS / rows-in-flight setting selects the item kernel
@@ -894,19 +897,25 @@ int launch_combine(int mode, int weighted, const Params& p_in, deepep_stream_t s
     // on every measurement (config 2 188.4 vs 175.3 us, EP = 8 phase A 318 vs 301, phase B 126 vs
     // 115): neighbouring items spread over all XCDs stream better
     // 5: the item kernel on a persistent grid (as many workgroups as the chip holds at once)
-    // On a CU-budget stream every candidate takes a persistent grid sized to the budget.
+    // 6: the item kernel on its full grid (what the default does on a CU-budget stream too)
+    // On a CU-budget stream the item kernel keeps its full grid (the CU mask alone holds it to the
+    // budget) with 4 rows in flight per lane: 64 VGPRs, 8 waves per SIMD, so a budgeted CU keeps more
+    // bytes in flight than with 8 rows at 5 waves (config 2, tools/kcu2.py, profiles/r02n_kcu2.jsonl:
+    // 128 CUs 208 vs 235 us on a persistent grid, 32 CUs 603 vs 661 us; the whole chip is unchanged);
+    // the streaming kernels and the forced persistent item kernel take a persistent grid sized to it.
     const int budget = budget_cus_of(s);
+    if (budget > 0 && g_config.rows_in_flight == 0) sh.group = 4;
     auto launch_choice = [&](int c) {
         p.xcd_blocks = c == 4 ? 1 : 0;
-        p.cap_cus = budget > 0 ? budget : (c == 5 ? device_cus() : 0);
+        p.cap_cus = (c == 0 || c == 4 || c == 6) ? 0 : (budget > 0 ? budget : (c == 5 ? device_cus() : 0));
         // a persistent grid stages slots per wave (no workgroup barrier between a wave's items), so
         // each wave streams at its own pace
         sh.lds = g_config.stage_lds >= 0 ? g_config.stage_lds != 0 : p.cap_cus == 0;
-        if (c == 0 || c == 4 || c == 5) launch_items();
+        if (c == 0 || c == 4 || c == 5 || c == 6) launch_items();
         else launch_streaming(c == 2 ? 1 : sh.vpt, c == 3);
     };
     const int forced = g_kernel_choice;
-    const int choice = forced == 5 ? 5 : ((stream_ok && forced >= 0) ? forced : 0);
+    const int choice = (forced == 5 || forced == 6) ? forced : ((stream_ok && forced >= 0) ? forced : 0);
     g_last_choice = choice;
     launch_choice(choice);
     const hipError_t err = hipGetLastError();
@@ -953,7 +962,7 @@ int deepep_build_local_plan(const int32_t* src_metadata, int num_recv_tokens, in
 }
 
 int deepep_set_kernel_choice(int choice) {
-    if (choice < -1 || choice > 5) return set_error(DEEPEP_ERR_INVALID_ARG, "kernel choice must be -1 or 0..5");
+    if (choice < -1 || choice > 6) return set_error(DEEPEP_ERR_INVALID_ARG, "kernel choice must be -1 or 0..6");
     g_kernel_choice = choice;
     return DEEPEP_OK;
 }

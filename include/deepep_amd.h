@@ -132,7 +132,9 @@ int deepep_build_local_plan(const int32_t* src_metadata, int num_recv_tokens, in
  *   vec_per_lane   16-byte vectors each lane loads per source row and item (1 or 2)
  *   stage_lds      1: stage the slot table / weights per workgroup in LDS; 0: per wave in registers
  *   store_policy   output store cache policy: 0 plain, 1 nt, 2 sc1 (write-through)
- *   rows_in_flight source rows each lane loads before accumulating them (2, 4 or 8; sc1 + LDS only)
+ *   rows_in_flight source rows each lane loads before accumulating them (2, 4 or 8; LDS staging with
+ *                  sc1 or system-scope stores only).  Automatic: 8 for the fused / epilogue reduces,
+ *                  4 for phase A (DEEPEP_MODE_LOCAL) and for every launch on a CU-budget stream.
  * The results are identical for every configuration; only the speed changes.
  */
 int deepep_set_launch_config(int vec_per_lane, int stage_lds, int store_policy, int rows_in_flight);
@@ -148,6 +150,9 @@ int deepep_set_launch_config(int vec_per_lane, int stage_lds, int store_policy, 
  *      once, units strided over the waves;
  *   4  the item kernel with XCD-contiguous workgroup order (each of the 8 XCDs takes one
  *      contiguous eighth of the items; measured slower, so only when forced);
+ *   5  the item kernel on a persistent grid (as many workgroups as the chip or the CU budget holds);
+ *   6  the item kernel on its full grid (one workgroup per virtual block) even on a CU-budget stream,
+ *      where the default is the persistent grid (the hardware keeps the workgroups on the budget);
  *  -1  (default) the item kernel.  Nothing is timed or synchronised inside a call.
  * All of them produce identical bits.  deepep_last_kernel_choice() says which one the last launch used.
  */

@@ -69,12 +69,12 @@ def test_invalid_arguments_are_rejected_without_a_gpu(lib):
     # zero units: nothing to do, success without a launch
     assert lib.deepep_combine_reduce(1, 0, 16, 1, 8, None, 0, 1, None, None, None, 48, 8, 0, 8,
                                      None, 0, None, None, 0, 0, 0, 0, None, None) == 0
-    # kernel choice: -1 (default: the item kernel), 0-5; anything else is rejected with a message
-    assert lib.deepep_set_kernel_choice(6) == -1 and b'kernel choice' in lib.deepep_amd_last_error()
+    # kernel choice: -1 (default: the item kernel), 0-6; anything else is rejected with a message
+    assert lib.deepep_set_kernel_choice(7) == -1 and b'kernel choice' in lib.deepep_amd_last_error()
     assert lib.deepep_set_kernel_choice(-2) == -1
-    for c in (0, 1, 2, 3, 4, 5, -1):
+    for c in (0, 1, 2, 3, 4, 5, 6, -1):
         assert lib.deepep_set_kernel_choice(c) == 0
-    assert lib.deepep_last_kernel_choice() in (0, 1, 2, 3, 4, 5)
+    assert lib.deepep_last_kernel_choice() in (0, 1, 2, 3, 4, 5, 6)
     # launch configuration knobs out of range
     assert lib.deepep_set_launch_config(3, -1, -1, 0) == -1
     assert lib.deepep_set_launch_config(0, -1, -1, 3) == -1

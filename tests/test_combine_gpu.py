@@ -403,8 +403,9 @@ def test_config2_full_size_bitwise(weighted, T, skew):
     ref, _ = oracle.phase_b(recv, None, idx.cpu().numpy(), E, 1, True, True)
     lib = buf.kernels.lib
     try:
-        # the item kernel, the streaming kernel (2 and 1 vectors per lane, persistent), XCD order, persistent, default
-        for choice in (0, 1, 2, 3, 4, 5, -1):
+        # the item kernel, the streaming kernel (2 and 1 vectors per lane, persistent), XCD order, persistent,
+        # full grid, default
+        for choice in (0, 1, 2, 3, 4, 5, 6, -1):
             assert lib.deepep_set_kernel_choice(choice) == 0
             out, out_w, _ = buf.combine(y, handle, topk_weights=ex_w, apply_topk_weights=weighted)
             torch.cuda.synchronize()

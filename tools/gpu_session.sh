@@ -42,7 +42,10 @@ for step in "$@"; do
         kphase) run kphase 300 python tools/kphase.py ;;
         profphase) run profphase 300 rocprofv3 --kernel-trace --stats -d $OUT/profphase -o prof --output-format csv -- python3 tools/kphase_prof.py ;;
         kcu)    run kcu 300 python tools/kcu.py ;;
+        kcu2)   run kcu2 300 python tools/kcu2.py ;;
+        kphasecu) run kphasecu 300 python tools/kphase_cu.py ;;
         cumask) run cumask 120 python tools/probe_cumask.py ;;
+        cubw)   run cubw 300 python tools/probe_cubw.py ;;
         probeld) run probeld 300 python tools/probe_ld.py ;;
         pmclist) run pmclist 120 rocprofv3 --list-avail ;;
         smi)    run smi 60 rocm-smi --showclocks --showpower --showtemp ;;

@@ -1,11 +1,13 @@
 """Combine time under a CU budget (ElasticBuffer.combine(num_sms=n): kernels on a
-hipExtStreamCreateWithCUMask stream, persistent grid sized to the budget), BASELINE config 2 at
-EP = 1: what the combine costs when it leaves CUs to overlapping compute.
+hipExtStreamCreateWithCUMask stream), BASELINE config 2 at EP = 1: what the combine costs when it
+leaves CUs to overlapping compute.
 
 Per budget: `api` = combine(num_sms=n) from the default stream (two cross-stream hops per call),
 `api_on_budget_stream` = the same call issued from the budget stream itself (no hops), `kernel` = the
-fused launch alone on the budget stream (item kernel, persistent), `kernel_stream` = the streaming
-kernel forced (deepep_set_kernel_choice(3), persistent)."""
+fused launch alone on the budget stream (the default: item kernel on its full grid, 4 rows in flight
+per lane on a budget), `kernel_stream` = the streaming kernel forced (deepep_set_kernel_choice(3),
+persistent grid), `kernel_persistent` = the item kernel on a persistent grid sized to the budget
+(choice 5, round 2's budget default), `kernel_r8` = the full grid with 8 rows in flight per lane."""
 import json
 import os
 import sys
@@ -70,13 +72,16 @@ def main():
             row['bitwise'] = bool(torch.equal(out, ref) and torch.equal(res['o'], ref))
             lib.deepep_set_kernel_choice(3)
             row['kernel_stream_us'] = round(timed(kern, bs), 1)
+            lib.deepep_set_kernel_choice(5)                    # the item kernel on a persistent grid
+            row['kernel_persistent_us'] = round(timed(kern, bs), 1)
             lib.deepep_set_kernel_choice(-1)
-            lib.deepep_set_launch_config(0, 1, -1, 0)          # persistent item kernel with LDS staging
-            row['kernel_lds_us'] = round(timed(kern, bs), 1)
+            lib.deepep_set_launch_config(0, -1, -1, 8)         # full grid, 8 rows in flight per lane
+            row['kernel_r8_us'] = round(timed(kern, bs), 1)
             lib.deepep_set_launch_config(0, -1, -1, 0)
             torch.cuda.synchronize()
             row['bitwise'] = row['bitwise'] and bool(torch.equal(out, ref))
-        for k in ('api_us', 'api_on_budget_stream_us', 'kernel_us', 'kernel_stream_us', 'kernel_lds_us'):
+        for k in ('api_us', 'api_on_budget_stream_us', 'kernel_us', 'kernel_stream_us', 'kernel_persistent_us',
+                  'kernel_r8_us'):
             row[k.replace('_us', '_tbps')] = round(nbytes / row[k] / 1e6, 2)
         print(json.dumps(row), flush=True)
     dist.destroy_process_group()

@@ -11,8 +11,8 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def main():
-    torch.cuda.set_device(0)
+def setup():
+    """The phase A / phase B launches of one rank's share of config 3: (launch_a, launch_b, bytes_a, bytes_b)."""
     from deepep_amd.handle import packed_row_layout
     from deepep_amd.kernels import HipKernels, MODE_EPILOGUE, MODE_LOCAL
     from tests.plan_ref import epilogue_tables
@@ -43,32 +43,42 @@ def main():
                            torch.full_like(row_of_lane, -1)).to(torch.int32).contiguous()
     out = torch.empty((T, H), dtype=torch.bfloat16, device='cuda')
     out_w = torch.empty((T, K), dtype=torch.float32, device='cuda')
+    bytes_a = n_exp * H * 2 + n_recv * (H * 2 + K * 4)
+    bytes_b = int((table_b >= 0).sum()) * H * 2 + T * H * 2 + T * K * 4
+
+    def launch_a(stream):
+        kern.combine_reduce(MODE_LOCAL, y, packed[:, :H], n_recv, table=table_a, row_weights=w, wtable=table_a, wsrc=w,
+                            out_weights=pw, weights_pad=w_pad, stream=stream)
+
+    def launch_b(stream):
+        kern.combine_reduce(MODE_EPILOGUE, recv[:, :H], out, T, table=table_b, wtable=wtable_b,
+                            wsrc=recv.view(torch.float32).view(-1), out_weights=out_w, stream=stream)
+    return launch_a, launch_b, bytes_a, bytes_b, dict(units_a=n_recv, rows_a=n_exp)
+
+
+def main():
+    torch.cuda.set_device(0)
+    launch_a, launch_b, bytes_a, bytes_b, info = setup()
     s = torch.cuda.current_stream()
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
     for _ in range(3):
-        kern.combine_reduce(MODE_LOCAL, y, packed[:, :H], n_recv, table=table_a, row_weights=w, wtable=table_a, wsrc=w,
-                            out_weights=pw, weights_pad=w_pad, stream=s)
+        launch_a(s)
     ev[0].record(s)
     for _ in range(50):
-        kern.combine_reduce(MODE_LOCAL, y, packed[:, :H], n_recv, table=table_a, row_weights=w, wtable=table_a, wsrc=w,
-                            out_weights=pw, weights_pad=w_pad, stream=s)
+        launch_a(s)
     ev[1].record(s)
     for _ in range(3):
-        kern.combine_reduce(MODE_EPILOGUE, recv[:, :H], out, T, table=table_b, wtable=wtable_b,
-                            wsrc=recv.view(torch.float32).view(-1), out_weights=out_w, stream=s)
+        launch_b(s)
     ev[2].record(s)
     for _ in range(50):
-        kern.combine_reduce(MODE_EPILOGUE, recv[:, :H], out, T, table=table_b, wtable=wtable_b,
-                            wsrc=recv.view(torch.float32).view(-1), out_weights=out_w, stream=s)
+        launch_b(s)
     ev[3].record(s)
     torch.cuda.synchronize()
     a_us = ev[0].elapsed_time(ev[1]) * 1e3 / 50
     b_us = ev[2].elapsed_time(ev[3]) * 1e3 / 50
-    bytes_a = n_exp * H * 2 + n_recv * (H * 2 + K * 4)
-    bytes_b = int((table_b >= 0).sum()) * H * 2 + T * H * 2 + T * K * 4
     print(json.dumps(dict(phase_a_us=round(a_us, 1), phase_a_bytes=bytes_a, phase_a_gbps=round(bytes_a / a_us / 1e3, 1),
                           phase_b_us=round(b_us, 1), phase_b_bytes=bytes_b, phase_b_gbps=round(bytes_b / b_us / 1e3, 1),
-                          units_a=n_recv, rows_a=n_exp)), flush=True)
+                          **info)), flush=True)
 
 
 if __name__ == '__main__':

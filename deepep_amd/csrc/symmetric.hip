@@ -56,7 +56,9 @@ constexpr int kXcdGroups = 64;
 __device__ __forceinline__ bool writeback_all_xcds(const uint64_t* peer_flags, int rank, int slot) {
     __shared__ int s_last;
     if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");                 // buffer_wbl2 sc0 sc1
+        // buffer_wbl2 sc0 sc1, then buffer_inv sc0 sc1: this XCD's dirty lines reach memory and its
+        // copies of window lines are dropped, so the last workgroup reads its epoch counter fresh
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         int64_t* join = reinterpret_cast<int64_t*>(peer_flags[rank]) + kSlots * 64 + 2 * kSlots + slot;
         const int64_t arrived = __hip_atomic_fetch_add(join, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1;
@@ -71,6 +73,7 @@ __device__ __forceinline__ int64_t next_epoch(const uint64_t* peer_flags, int ra
     if (threadIdx.x == 0) {
         int64_t e = given;
         if (e <= 0) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");             // no stale copy of the counter
             int64_t* cnt = reinterpret_cast<int64_t*>(peer_flags[rank]) + kSlots * 64 + row * kSlots + slot;
             e = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
             __hip_atomic_store(cnt, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -83,6 +86,10 @@ __device__ __forceinline__ int64_t next_epoch(const uint64_t* peer_flags, int ra
 
 __device__ __forceinline__ void wait_slots(const int64_t* mine, int s, int64_t epoch, int64_t timeout_ticks,
                                            int32_t* error_flag) {
+    // An acquire load invalidates this XCD's L2 only AFTER it has read: a stale copy of the flag line
+    // left in that L2 (window memory freed by an earlier process and reallocated here still holds
+    // that process's epochs) would let the very first poll pass early.  Drop such copies first.
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");                     // buffer_inv sc0 sc1
     const uint64_t t0 = wall_clock64();
     while (__hip_atomic_load(mine + s, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
         if (static_cast<int64_t>(wall_clock64() - t0) > timeout_ticks) {

@@ -54,6 +54,13 @@ for step in "$@"; do
         pmc)    for c in FETCH_SIZE WRITE_SIZE TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum; do
                     run pmc_$c 300 timeout -s KILL 120 rocprofv3 --pmc $c -d $OUT/pmc_$c -o pmc --output-format csv -- python3 tools/pmc_run.py
                 done ;;
+        pmcfold) # fold this build's PMC passes (the `pmc` step) into profiles/pmc_traffic.json, so the bench
+                 # line run after it in the same call carries measured traffic; the file comes back in $OUT
+                run pmcfold 120 python tools/summarize_prof.py pmc profiles/pmc_traffic.json \
+                    combine_fused_weighted_t8192_h7168_k8 1057488896 \
+                    $(find $OUT/pmc_FETCH_SIZE $OUT/pmc_WRITE_SIZE $OUT/pmc_TCC_EA0_RDREQ_sum $OUT/pmc_TCC_EA0_WRREQ_sum -name '*counter_collection.csv')
+                cp profiles/pmc_traffic.json $OUT/pmc_traffic.json ;;
+        benchjson) run bench 600 python bench.py && grep '^{' $OUT/bench.log | tail -1 > $OUT/bench.json ;;
         pmcphases) for c in FETCH_SIZE WRITE_SIZE; do
                     run pmcph_$c 300 timeout -s KILL 120 rocprofv3 --pmc $c -d $OUT/pmcph_$c -o pmc --output-format csv -- python3 tools/pmc_phases.py
                 done ;;

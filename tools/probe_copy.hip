@@ -135,6 +135,48 @@ __global__ void __launch_bounds__(256) seq_write_only(int N, int xb, uint8_t* ou
     __builtin_amdgcn_raw_buffer_store_b128(a, rs, v1 * 16, 0, 16);
 }
 
+// One wave per token, its 2 KiB chunks in order with the next kAhead chunks' loads in flight while the
+// current chunk is stored to every destination (the read latency hidden behind the store stream).
+template <int kWaves, int kAhead>
+__global__ void __launch_bounds__(64 * kWaves) scatter_copy_pf(const uint8_t* x, const int32_t* dst, int T, int K,
+                                                               int xb, uint8_t* out) {
+    const int lane = threadIdx.x & 63;
+    const int nvec = xb / 16, nch = (nvec + 127) / 128;
+    const int64_t t = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+    if (t >= T) return;
+    int32_t my = lane < K ? dst[t * K + lane] : -1;
+    const uint64_t m0 = __ballot(my >= 0);
+    const u32x4 z = {0u, 0u, 0u, 0u};
+    const u32x4* src = (const u32x4*)(x + t * xb);
+    u32x4 a[kAhead + 1][2];
+#pragma unroll
+    for (int j = 0; j <= kAhead; ++j) {
+        const int v0 = j * 128 + lane, v1 = v0 + 64;
+        a[j][0] = (j < nch && v0 < nvec) ? __builtin_nontemporal_load(src + v0) : z;
+        a[j][1] = (j < nch && v1 < nvec) ? __builtin_nontemporal_load(src + v1) : z;
+    }
+    for (int c = 0; c < nch; ++c) {
+        const int v0 = c * 128 + lane, v1 = v0 + 64;
+        for (uint64_t m = m0; m; m &= m - 1) {
+            const int64_t d = __builtin_amdgcn_readlane(my, __builtin_ctzll(m));
+            auto rs = __builtin_amdgcn_make_buffer_rsrc(out + d * xb, 0, xb, 0x00020000);
+            __builtin_amdgcn_raw_buffer_store_b128(a[0][0], rs, v0 * 16, 0, 16);
+            __builtin_amdgcn_raw_buffer_store_b128(a[0][1], rs, v1 * 16, 0, 16);
+        }
+#pragma unroll
+        for (int j = 0; j < kAhead; ++j) { a[j][0] = a[j + 1][0]; a[j][1] = a[j + 1][1]; }
+        const int n = c + kAhead + 1, w0 = n * 128 + lane, w1 = w0 + 64;
+        a[kAhead][0] = (n < nch && w0 < nvec) ? __builtin_nontemporal_load(src + w0) : z;
+        a[kAhead][1] = (n < nch && w1 < nvec) ? __builtin_nontemporal_load(src + w1) : z;
+    }
+}
+
+template <int kWaves, int kAhead>
+static void launch_pf(const uint8_t* x, const int32_t* dst, int T, int K, int xb, uint8_t* o, hipStream_t s) {
+    hipLaunchKernelGGL((scatter_copy_pf<kWaves, kAhead>), dim3((unsigned)((T + kWaves - 1) / kWaves)),
+                       dim3(64 * kWaves), 0, s, x, dst, T, K, xb, o);
+}
+
 extern "C" int probe_copy(int variant, const void* x, const int32_t* dst, const int32_t* inv, int T, int K, int N,
                           int xb, void* out, hipStream_t s) {
     const int nch = (xb / 16 + 127) / 128;
@@ -161,6 +203,11 @@ extern "C" int probe_copy(int variant, const void* x, const int32_t* dst, const 
         case 109: launch_t<4, 1, 16>(xx, dst, T, K, xb, o, s); break;
         case 110: launch_t<16, 2, 16>(xx, dst, T, K, xb, o, s); break;
         case 111: launch_t<8, 7, 16>(xx, dst, T, K, xb, o, s); break;
+        case 300: launch_pf<4, 1>(xx, dst, T, K, xb, o, s); break;
+        case 301: launch_pf<4, 2>(xx, dst, T, K, xb, o, s); break;
+        case 302: launch_pf<2, 1>(xx, dst, T, K, xb, o, s); break;
+        case 303: launch_pf<1, 1>(xx, dst, T, K, xb, o, s); break;
+        case 304: launch_pf<1, 3>(xx, dst, T, K, xb, o, s); break;
         case 200: hipLaunchKernelGGL(scatter_write_only, grid((int64_t)T * nch), dim3(256), 0, s, dst, T, K, xb, o); break;
         case 201: hipLaunchKernelGGL(seq_write_only, grid((int64_t)N * nch), dim3(256), 0, s, N, xb, o); break;
         default: return -1;

@@ -41,7 +41,7 @@ def main():
     s = torch.cuda.current_stream()
     xb = H * 2
     nbytes = T * xb + N * xb
-    for v in (0, 200, 201, 1, 0, 200, 201):
+    for v in (0, 300, 301, 302, 303, 304, 104, 105, 111, 0, 300, 201):
         out.zero_()
         fn = lambda: lib.probe_copy(v, x.data_ptr(), dst.data_ptr(), inv.data_ptr(), T, K, N, xb, out.data_ptr(),
                                     s.cuda_stream)

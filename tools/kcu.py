@@ -51,7 +51,7 @@ def main():
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) * 1e3 / n
 
-    for n in (0, 224, 192, 160, 128, 96, 64, 32, 16):
+    for n in (0, 224, 192, 160, 128, 96, 64, 32, 24, 16, 8):
         row = dict(num_sms=n)
         s0 = torch.cuda.current_stream()
         row['api_us'] = round(timed(lambda: buf.combine(y, handle, topk_weights=ex_w, apply_topk_weights=True,

@@ -386,11 +386,12 @@ class ElasticBuffer(ExchangeMixin):
                  use_tma_aligned_col_major_sf: bool = False):
         """Dispatch tokens to the ranks owning their experts (elastic.py:855-1033 contract).
 
-        A fresh handle costs one host sync (the notify counts, as the reference's do_cpu_sync=True);
-        with do_cpu_sync=False the outputs are padded to the worst case as the reference's, but this
-        build still syncs once (the RCCL all-to-all needs host split sizes).  A cached handle
-        (`handle=...`) needs no sync.  The notify also carries per-64-token-block counts, so the
-        handle's combines never sync."""
+        A fresh handle costs one host sync (the notify counts, as the reference's do_cpu_sync=True).
+        With do_cpu_sync=False the outputs are padded to the worst case as the reference's
+        (buffer.hpp:1065-1070); on one rank that call then issues kernels only (launches sized for all
+        tokens, bounded on the device by the received count; graph-capturable), while EP > 1 still syncs
+        once (the all-to-all needs host split sizes).  A cached handle (`handle=...`) needs no sync.
+        The notify also carries per-64-token-block counts, so the handle's combines never sync."""
         num_topk = (handle.topk_idx if topk_idx is None else topk_idx).shape[1]
         num_sms = self.get_theoretical_num_sms(num_experts or handle.num_experts, num_topk) if num_sms == 0 else num_sms
         num_qps = self.get_theoretical_num_qps(num_sms) if num_qps == 0 else num_qps
@@ -438,6 +439,9 @@ class ElasticBuffer(ExchangeMixin):
             # and, over xGMI, at EP > 1),
             # as the reference's cached mode skips its notify phase (elastic.py:855-1033).
             cached = handle if handle is not None and handle._send_counts is not None else None
+            # dispatch(do_cpu_sync=False) on one rank issues kernels only (the reference's no-sync mode,
+            # buffer.hpp:1065-1070); EP > 1 still syncs once (the all-to-all needs host split sizes)
+            sync_free = cached is None and not do_cpu_sync and R == 1
             # EP > 1 over xGMI: the pack kernel stores every row straight into its destination's
             # symmetric window (dispatch.cuh:373-392's push), no RCCL exchange for the rows
             use_xgmi = R > 1 and self.transport == 'xgmi' and self.use_cuda
@@ -480,12 +484,17 @@ class ElasticBuffer(ExchangeMixin):
                 else:
                     recv_notify = torch.empty_like(notify)
                     self._a2a(recv_notify, notify)
-                host = [int(v) for v in torch.cat([send_counts, blk.view(-1), (everyone if R > 1 and use_xgmi else
-                                                                               recv_notify).reshape(-1)]).tolist()]   # host sync
-                send_counts_l = host[:R]
-                own_blk = host[R:R + 2 * R * nb]
-                _, recv_counts_l, expert_counts_l, offs, recv_blk = notify_layout(
-                    host[R + 2 * R * nb:], R, r, epr, all_gathered=R > 1 and use_xgmi, num_blocks=nb)
+                if sync_free:
+                    # one rank, no CPU sync: every receive-side launch is sized for all T tokens and bounded
+                    # on the device by the received count (psum of the notify); outputs are worst-case
+                    send_counts_l, recv_counts_l, expert_counts_l, offs = [T], [T], None, None
+                else:
+                    host = [int(v) for v in torch.cat([send_counts, blk.view(-1), (everyone if R > 1 and use_xgmi else
+                                                                                   recv_notify).reshape(-1)]).tolist()]   # host sync
+                    send_counts_l = host[:R]
+                    own_blk = host[R:R + 2 * R * nb]
+                    _, recv_counts_l, expert_counts_l, offs, recv_blk = notify_layout(
+                        host[R + 2 * R * nb:], R, r, epr, all_gathered=R > 1 and use_xgmi, num_blocks=nb)
                 counts = None
                 if R > 1:
                     rb = recv_notify[:, 1 + epr:].reshape(R, 2, nb).transpose(0, 1)
@@ -549,7 +558,8 @@ class ElasticBuffer(ExchangeMixin):
                 psum_expert = torch.empty((epr,), dtype=torch.int32, device=dev)
                 kern.dispatch_scan(block_counts, epr, expert_alignment, do_expand, expert_counts, psum_expert,
                                    stream=stream)
-                aligned_l = [align(c, expert_alignment) for c in expert_counts_l]      # known since notify
+                # known since the notify; [] without a CPU sync (as the reference's handle)
+                aligned_l = [] if sync_free else [align(c, expert_alignment) for c in expert_counts_l]
                 if cumulative_local_expert_recv_stats is not None:
                     cumulative_local_expert_recv_stats += expert_counts.to(cumulative_local_expert_recv_stats.dtype)
                 self._before_epilogue(previous_event_before_epilogue)
@@ -558,7 +568,17 @@ class ElasticBuffer(ExchangeMixin):
                 else:
                     meta[:, 2:] = -1
             num_unaligned = expert_counts
-            if do_expand:
+            if do_expand and cached is not None:
+                num_expanded = cached.num_expanded_tokens
+                alloc = torch.zeros if do_zero_padding else torch.empty
+                n_rows = num_expanded
+            elif do_expand and sync_free:
+                # worst case of buffer.hpp:1067-1069: every token in min(K, local experts) experts
+                num_expanded = align(num_max_tokens_per_rank * R * min(K, epr) + (expert_alignment - 1) * epr,
+                                     expert_alignment)
+                alloc = torch.zeros if do_zero_padding else torch.empty
+                n_rows = num_expanded
+            elif do_expand:
                 num_expanded = sum(aligned_l)
                 alloc = torch.zeros if do_zero_padding else torch.empty
                 n_rows = num_expanded

@@ -205,7 +205,10 @@ __device__ __forceinline__ int local_expert(int64_t e, int rank, int epr) {
 }
 
 // One thread per received row, 256 rows per workgroup: metadata columns 0-1, the local top-k
-// indices (non-expanded recv_topk_idx) and per-workgroup expert histograms.
+// indices (non-expanded recv_topk_idx) and per-workgroup expert histograms.  N is the host's row
+// count; the rows actually received are rank_psum[R - 1] (the same number after a host-synced notify;
+// fewer when the host sized the launch for the worst case, dispatch(do_cpu_sync=False)).  Rows past
+// the received ones get metadata -1 (and recv_topk_idx -1): the later kernels skip them.
 __global__ void __launch_bounds__(256)
 count_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int idx_off, int src_off, int N, int K,
              int rank, int epr, const int32_t* __restrict__ rank_psum, int R,
@@ -214,7 +217,15 @@ count_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int idx_off,
     for (int e = threadIdx.x; e < epr; e += 256) s_hist[e] = 0;
     __syncthreads();
     const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i < N) {
+    const int received = min(N, rank_psum[R - 1]);
+    if (i >= received && i < N) {
+        const int64_t mrow = static_cast<int64_t>(i) * (K + 2);
+        meta[mrow] = -1;
+        meta[mrow + 1] = -1;
+        if (recv_topk_idx != nullptr)
+            for (int k = 0; k < K; ++k) recv_topk_idx[static_cast<int64_t>(i) * K + k] = -1;
+    }
+    if (i < received) {
         const uint8_t* row = packed + static_cast<int64_t>(i) * row_bytes;
         const int64_t* idx = reinterpret_cast<const int64_t*>(row + idx_off);
         int src_rank = 0;
@@ -287,7 +298,8 @@ scan_kernel(int32_t* __restrict__ block_counts, int nblocks, int epr, int align,
 
 // Expanded slot of every (row, local lane): the expert group's offset for this workgroup plus the
 // number of earlier rows of the workgroup holding the same expert (per-wave 64-bit ballot masks in
-// LDS).  A token never holds one expert twice, so this is the ascending-token order.
+// LDS).  A token never holds one expert twice, so this is the ascending-token order.  Rows whose
+// metadata count_kernel marked -1 (past the received rows) get no slots.
 __global__ void __launch_bounds__(256)
 slots_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int idx_off, int N, int K, int rank, int epr,
              const int32_t* __restrict__ block_offsets, int32_t* __restrict__ meta) {
@@ -297,7 +309,8 @@ slots_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int idx_off,
     const int i = blockIdx.x * 256 + threadIdx.x;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t* idx = reinterpret_cast<const int64_t*>(packed + static_cast<int64_t>(i) * row_bytes + idx_off);
-    if (i < N)
+    const bool valid = i < N && meta[static_cast<int64_t>(i) * (K + 2)] >= 0;
+    if (valid)
         for (int k = 0; k < K; ++k) {
             const int le = local_expert(idx[k], rank, epr);
             if (le >= 0) atomicOr(reinterpret_cast<unsigned long long*>(&s_bits[le * 4 + wave]), 1ull << lane);
@@ -306,7 +319,7 @@ slots_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int idx_off,
     if (i >= N) return;
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     for (int k = 0; k < K; ++k) {
-        const int le = local_expert(idx[k], rank, epr);
+        const int le = valid ? local_expert(idx[k], rank, epr) : -1;
         int slot = -1;
         if (le >= 0) {
             slot = block_offsets[static_cast<int64_t>(blockIdx.x) * epr + le];
@@ -341,6 +354,7 @@ copy_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int x_bytes, 
     if (it >= static_cast<int64_t>(N) * nchunks) return;
     const int64_t i = it / nchunks;
     const int c = static_cast<int>(it - i * nchunks);
+    if (meta[i * (K + 2)] < 0) return;                     // past the received rows (count_kernel)
     const uint8_t* row = packed + i * row_bytes;
     const uint8_t* xs = row;
     const uint8_t* sfs = row + sf_off;

@@ -198,7 +198,9 @@ int deepep_dispatch_pack(const void* x, int64_t x_row_stride_bytes, int x_bytes,
 /* Receive side, pass 1: src_metadata columns 0-1 ({src_global_idx, src_rank * K + master lane}),
  * recv_topk_idx (local expert or -1, int64 [num_recv][K], may be NULL) and per-256-row expert
  * histograms block_counts [ceil(num_recv / 256)][num_local_experts]. recv_rank_psum is the
- * inclusive prefix sum of rows per source rank. */
+ * inclusive prefix sum of rows per source rank (device memory).  Rows from recv_rank_psum[num_ranks-1]
+ * up to num_recv (a launch sized for the worst case, dispatch(do_cpu_sync=False)) get src_metadata
+ * columns 0-1 = -1 and recv_topk_idx -1; passes 3 and 4 skip them. */
 int deepep_dispatch_count(const void* packed, int64_t row_bytes, int idx_off, int src_off, int num_recv, int num_topk,
                           int rank, int num_local_experts, const int32_t* recv_rank_psum, int num_ranks,
                           int32_t* src_metadata, int64_t* recv_topk_idx, int32_t* block_counts,
@@ -210,7 +212,8 @@ int deepep_dispatch_count(const void* packed, int64_t row_bytes, int idx_off, in
 int deepep_dispatch_scan(int32_t* block_counts, int num_blocks, int num_local_experts, int expert_alignment,
                          int expanded, int32_t* expert_counts, int32_t* psum_expert, deepep_stream_t stream);
 
-/* Pass 3 (expanded only): src_metadata columns 2.. = expanded row of every local slot, -1 elsewhere. */
+/* Pass 3 (expanded only): src_metadata columns 2.. = expanded row of every local slot, -1 elsewhere
+ * (all -1 for a row whose column 0 is -1). */
 int deepep_dispatch_slots(const void* packed, int64_t row_bytes, int idx_off, int num_recv, int num_topk,
                           int rank, int num_local_experts, const int32_t* block_offsets, int32_t* src_metadata,
                           deepep_stream_t stream);
@@ -220,7 +223,8 @@ int deepep_dispatch_slots(const void* packed, int64_t row_bytes, int idx_off, in
  * (one rank: nothing was exchanged, the packed rows carry only metadata) the x / sf bytes of row i
  * are read from x_direct / sf_direct at row src_metadata[i][0] % num_max_tokens.  Destination rows
  * >= num_out_rows (the rows recv_x holds) are skipped and set bit 1 of error_flag (device int or
- * NULL); once bit 2 is set (a timed-out window barrier) nothing is stored. */
+ * NULL); once bit 2 is set (a timed-out window barrier) nothing is stored.  Rows whose
+ * src_metadata[i][0] is -1 (past the received rows, pass 1) are skipped. */
 int deepep_dispatch_copy(const void* packed, int64_t row_bytes, int x_bytes, int sf_off, int sf_bytes, int w_off,
                          int num_recv, int num_topk, const int32_t* src_metadata, int expanded,
                          const void* x_direct, int64_t x_direct_stride_bytes,

@@ -158,4 +158,17 @@ def dispatch_mode_checks(buf, x, topk_idx, topk_weights, num_experts: int, num_m
             break
     if ex_handle.recv_src_metadata.shape[0] != (n if do_cpu_sync else num_max_tokens * buf.num_ranks):
         fails.append('expanded metadata rows')
+    if not do_cpu_sync:
+        # a handle made without a CPU sync combines exactly like a host-synced one (same slots, same rows)
+        s_ex_x, _, s_ex_w, s_handle, _ = buf.dispatch(x, do_expand=True, **dict(args, do_cpu_sync=True))
+        if not torch.equal(s_handle.recv_src_metadata, ex_handle.recv_src_metadata[:s_handle.recv_src_metadata.shape[0]]):
+            fails.append('no-CPU-sync expanded metadata differs from the synced one')
+        g = torch.Generator(device=rows(ex_x).device).manual_seed(3)
+        y = torch.randn((ex_handle.num_expanded_tokens, rows(ex_x).shape[1]), generator=g,
+                        device=rows(ex_x).device).to(torch.bfloat16)
+        n_ex = s_handle.num_expanded_tokens
+        out_f, w_f, _ = buf.combine(y, ex_handle, topk_weights=ex_w)
+        out_s, w_s, _ = buf.combine(y[:n_ex].contiguous(), s_handle, topk_weights=s_ex_w)
+        if not (torch.equal(out_f.view(torch.int16), out_s.view(torch.int16)) and torch.equal(w_f, w_s)):
+            fails.append('combine over a no-CPU-sync handle differs')
     return fails

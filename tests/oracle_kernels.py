@@ -45,15 +45,16 @@ class OracleKernels:
                          plan, num_tokens, topk_idx=None, wtable=None, stream=None):
         meta = src_metadata[:num_recv_tokens]
         plan.fill_(-1)
-        t = (meta[:, 0] % num_max_tokens_per_rank).long()
+        rows = (meta[:, 0] >= 0).nonzero(as_tuple=True)[0]     # metadata -1: not a received row (C: -1 % n < 0)
+        t = (meta[rows, 0] % num_max_tokens_per_rank).long()
         if expanded:
-            plan[t] = meta[:, 2:2 + plan.shape[1]]
+            plan[t] = meta[rows, 2:2 + plan.shape[1]]
         else:
-            plan[t, 0] = torch.arange(num_recv_tokens, dtype=torch.int32)
+            plan[t, 0] = rows.to(torch.int32)
         if wtable is not None:
             wtable.fill_(-1)
             inv = torch.full((num_tokens,), -1, dtype=torch.int64)
-            inv[t] = torch.arange(num_recv_tokens)
+            inv[t] = rows
             k = torch.arange(num_topk).view(1, -1)
             ok = (topk_idx >= 0) & (inv.view(-1, 1) >= 0)
             wtable.copy_(torch.where(ok, inv.view(-1, 1) * num_topk + k, torch.full_like(topk_idx, -1)).to(torch.int32))
@@ -112,7 +113,11 @@ class OracleKernels:
 
     def dispatch_count(self, packed, layout, num_recv, rank, num_local_experts, rank_psum, meta, recv_topk_idx,
                        block_counts, stream=None):
-        N, K, epr = num_recv, layout.num_topk, num_local_experts
+        K, epr = layout.num_topk, num_local_experts
+        N = min(num_recv, int(rank_psum[-1]))          # rows received; the rest get metadata -1
+        meta[N:num_recv, :2] = -1
+        if recv_topk_idx is not None:
+            recv_topk_idx[N:num_recv] = -1
         le = self._local(packed, layout, N, rank, epr)
         src = packed[:N, layout.src_off:layout.src_off + 4].contiguous().view(torch.int32).view(N)
         src_rank = torch.searchsorted(rank_psum.to(torch.int64), torch.arange(N), right=True).clamp(max=rank_psum.numel() - 1)
@@ -120,7 +125,7 @@ class OracleKernels:
         meta[:N, 0] = src
         meta[:N, 1] = (src_rank * K + master).to(torch.int32)
         if recv_topk_idx is not None:
-            recv_topk_idx.copy_(le)
+            recv_topk_idx[:N].copy_(le)
         block_counts.zero_()
         for b in range(block_counts.shape[0]):
             chunk = le[b * 256:(b + 1) * 256]
@@ -143,6 +148,8 @@ class OracleKernels:
         for b in range(block_offsets.shape[0]):
             run = block_offsets[b].clone()
             for i in range(b * 256, min(num_recv, (b + 1) * 256)):
+                if int(meta[i, 0]) < 0:                  # past the received rows
+                    continue
                 for k in range(layout.num_topk):
                     e = int(le[i, k])
                     if e >= 0:
@@ -151,7 +158,8 @@ class OracleKernels:
 
     def dispatch_copy(self, packed, layout, num_recv, meta, expanded, recv_x_bytes, recv_sf_bytes, recv_w,
                       x_direct=None, sf_direct=None, num_max_tokens=0, error_flag=None, stream=None):
-        N, K = num_recv, layout.num_topk
+        K = layout.num_topk
+        N = int((meta[:num_recv, 0] >= 0).sum())         # the received rows come first
         if x_direct is not None:
             t = (meta[:N, 0].long() % num_max_tokens)
             xs = x_direct[t]

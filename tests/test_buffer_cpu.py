@@ -295,6 +295,8 @@ def _modes_worker(rank, world, port, alignment, do_cpu_sync, do_handle_copy, que
         w, idx = torch.topk(scores, K, dim=-1, sorted=False)
         idx = idx.to(torch.int64)
         idx[torch.rand(idx.shape, generator=g) < 0.2] = -1
+        idx[0] = -1                                        # tokens routed nowhere: fewer rows received than T
+        idx[T // 2] = -1
         w = w.masked_fill(idx < 0, 0)
         x = torch.randn((T, H), generator=g).to(torch.bfloat16)
         buf = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=T, hidden=H, num_topk=K)
@@ -306,20 +308,22 @@ def _modes_worker(rank, world, port, alignment, do_cpu_sync, do_handle_copy, que
         queue.put((rank, [traceback.format_exc()]))
 
 
-@pytest.mark.parametrize('alignment,do_cpu_sync,do_handle_copy', [(1, True, True), (4, True, False), (8, False, True)])
-def test_dispatch_modes_world2(alignment, do_cpu_sync, do_handle_copy):
+@pytest.mark.parametrize('world,alignment,do_cpu_sync,do_handle_copy', [
+    (2, 1, True, True), (2, 4, True, False), (2, 8, False, True), (1, 8, False, True), (1, 1, False, False)])
+def test_dispatch_modes(world, alignment, do_cpu_sync, do_handle_copy):
     """Cached / cached-expanded-zero-padded / deterministic / counter / no-CPU-sync dispatch
-    (tests/elastic/test_ep.py:143-177, 355-466) over 2 gloo ranks."""
+    (tests/elastic/test_ep.py:143-177, 355-466) over 1 and 2 gloo ranks (one rank without a CPU sync
+    sizes its launches for all tokens and bounds them by the device count)."""
     ctx = mp.get_context('spawn')
     queue = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_modes_worker, args=(r, 2, port, alignment, do_cpu_sync, do_handle_copy, queue))
-             for r in range(2)]
+    procs = [ctx.Process(target=_modes_worker, args=(r, world, port, alignment, do_cpu_sync, do_handle_copy, queue))
+             for r in range(world)]
     for p in procs:
         p.start()
     results = {}
     try:
-        for _ in range(2):
+        for _ in range(world):
             rank, failures = queue.get(timeout=240)
             results[rank] = failures
     finally:
@@ -327,7 +331,7 @@ def test_dispatch_modes_world2(alignment, do_cpu_sync, do_handle_copy):
             p.join(timeout=30)
             if p.is_alive():
                 p.kill()
-    assert len(results) == 2 and not any(results.values()), results
+    assert len(results) == world and not any(results.values()), results
 
 
 def _empty_rank_worker(rank, world, port, queue):

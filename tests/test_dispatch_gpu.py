@@ -159,7 +159,8 @@ def test_dispatch_direct_copy_one_rank(hip, K, E, T, H, expanded, fp8):
 
 
 @pytest.mark.parametrize('alignment,do_cpu_sync,do_handle_copy,fp8', [
-    (1, True, True, False), (128, True, False, False), (4, False, True, False), (1, True, True, True)])
+    (1, True, True, False), (128, True, False, False), (4, False, True, False), (1, True, True, True),
+    (1, False, False, True), (128, False, True, False)])
 def test_dispatch_modes_on_gpu(alignment, do_cpu_sync, do_handle_copy, fp8):
     """ElasticBuffer.dispatch modes with the HIP kernels (EP = 1): cached, cached expanded with zero
     padding, handle copy, deterministic repeat, the per-expert counter, no CPU sync
@@ -179,6 +180,8 @@ def test_dispatch_modes_on_gpu(alignment, do_cpu_sync, do_handle_copy, fp8):
     w, idx = torch.topk(scores, K, dim=-1, sorted=False)
     idx = idx.to(torch.int64)
     idx[torch.rand(idx.shape, device='cuda', generator=g) < 0.1] = -1
+    idx[0] = -1                                            # tokens routed nowhere: fewer rows received than T
+    idx[T - 300] = -1
     w = w.masked_fill(idx < 0, 0)
     x = torch.randn((T, H), device='cuda', generator=g).to(torch.bfloat16)
     if fp8:

@@ -251,6 +251,69 @@ def test_first_combine_captured_into_a_graph():
     assert torch.equal(eager, out) and torch.equal(eager_w, out_w)
 
 
+def _dispatch_combine_free(buf, x, idx, w, E, y, bias):
+    """A fresh dispatch without CPU sync (EP = 1) and the first combine over its handle."""
+    _, _, ex_w, handle, _ = buf.dispatch(x, topk_idx=idx, topk_weights=w, num_experts=E, do_expand=True,
+                                         do_cpu_sync=False)
+    out, out_w, _ = buf.combine(y, handle, topk_weights=ex_w, bias=bias, apply_topk_weights=True)
+    return out, out_w, handle
+
+
+@pytest.mark.parametrize('capture', [False, True])
+def test_dispatch_without_cpu_sync_then_combine(capture):
+    """dispatch(do_cpu_sync=False) on one rank issues kernels only (the reference's no-sync mode,
+    csrc/elastic/buffer.hpp:1065-1070): with its first combine it runs under
+    set_sync_debug_mode('error') and, with no eager call before it, inside a HIP graph capture.
+    Tokens routed nowhere make the received count smaller than the launches' worst case; the
+    combined rows are bitwise equal to the oracle and to a host-synced dispatch's."""
+    from deepep_amd import ElasticBuffer
+    T, H, K, E = 768, 1024, 8, 64
+    rng, idx_all, w_all = _routing(1, T, K, E, seed=17)
+    idx_all[0][[0, 5, T - 1]] = -1                       # three tokens routed nowhere
+    w_all[0][[0, 5, T - 1]] = 0
+    buf = ElasticBuffer(_group1(), num_max_tokens_per_rank=T, hidden=H, num_topk=K)
+    idx, w = torch.from_numpy(idx_all[0]).cuda(), torch.from_numpy(w_all[0]).cuda()
+    x = _bf16(oracle.f32_to_bf16(rng.standard_normal((T, H)).astype(np.float32)))
+    worst = T * min(K, E)
+    y = _bf16(oracle.f32_to_bf16(rng.standard_normal((worst, H)).astype(np.float32)))
+    bias = _bf16(oracle.f32_to_bf16(rng.standard_normal((T, H)).astype(np.float32)))
+    torch.cuda.synchronize()
+    if capture:
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            out, out_w, handle = _dispatch_combine_free(buf, x, idx, w, E, y, bias)
+        graph.replay()
+    else:
+        torch.cuda.set_sync_debug_mode('error')
+        try:
+            out, out_w, handle = _dispatch_combine_free(buf, x, idx, w, E, y, bias)
+        finally:
+            torch.cuda.set_sync_debug_mode(0)
+    torch.cuda.synchronize()
+    assert handle.num_expanded_tokens == worst and handle.recv_src_metadata.shape[0] == T
+    assert handle.num_recv_tokens_per_expert_list == []
+    meta = handle.recv_src_metadata.cpu().numpy()
+    n = int(handle.psum_num_recv_tokens_per_scaleup_rank[-1].item())
+    assert n == T - 3 and (meta[n:] == -1).all()
+    # the same batch through a host-synced dispatch: same metadata rows, same combine bits
+    _, _, s_w, s_handle, _ = buf.dispatch(x, topk_idx=idx, topk_weights=w, num_experts=E, do_expand=True)
+    assert np.array_equal(s_handle.recv_src_metadata.cpu().numpy(), meta[:n])
+    s_out, s_out_w, _ = buf.combine(y[:s_handle.num_expanded_tokens].contiguous(), s_handle, topk_weights=s_w,
+                                    bias=bias, apply_topk_weights=True)
+    torch.cuda.synchronize()
+    assert torch.equal(s_out, out) and torch.equal(s_out_w, out_w)
+    ex_w = np.zeros((worst,), np.float32)
+    slots = meta[:n, 2:]
+    tok = meta[:n, 0] % T
+    ex_w[slots[slots >= 0]] = w_all[0][tok][slots >= 0]
+    part, _ = oracle.phase_a(_u16(y), meta[:n], K, True, ex_w, weighted=True)
+    recv = np.zeros((1, T, H), np.uint16)
+    recv[0, tok] = part
+    ref, _ = oracle.phase_b(recv, None, idx_all[0], E, 1, True, True, _u16(bias))
+    assert np.array_equal(_u16(out), ref)
+    assert np.array_equal(out_w.cpu().numpy(), w_all[0])
+
+
 # ----------------------------------------------------------------------------- stream ordering
 def _ordering_rank(rank, world, T, H, K, E, comm, drop_wait, results):
     try:
@@ -288,14 +351,51 @@ def _ordering_rank(rank, world, T, H, K, E, comm, drop_wait, results):
         comm.bar.abort()
 
 
+def _ordering_child(queue):
+    """Both schedules in a fresh process (see the test): {drop_wait: {rank: bool or traceback}}."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    try:
+        T, H, K, E, world = 1024, 256, 8, 32, 4
+        out = {}
+        for drop_wait in (False, True):
+            comm = ThreadComm(world)
+            out[drop_wait] = run_threads(world, _ordering_rank, (world, T, H, K, E, comm, drop_wait))
+        queue.put(out)
+    except Exception:
+        import traceback
+        queue.put(traceback.format_exc())
+
+
 def test_pipelined_schedule_is_ordered_by_its_stream_waits():
     """EP = 4, 4 chunks, the exchange delayed on its own stream: the real schedule is bitwise right;
     the same schedule with the exchange's wait dropped is caught (phase B reads receive rows that
-    have not landed)."""
-    T, H, K, E, world = 1024, 256, 8, 32, 4
-    for drop_wait in (False, True):
-        comm = ThreadComm(world)
-        results = run_threads(world, _ordering_rank, (world, T, H, K, E, comm, drop_wait))
+    have not landed).  The 4 simulated ranks use 12 streams; HIP deals streams round-robin onto
+    GPU_MAX_HW_QUEUES hardware queues (4 by default), and a phase-B stream that shares a queue with a
+    delayed exchange stream is serialised behind it, which would hide the race.  So the schedules
+    run in a fresh process with 16 hardware queues: every stream of it gets its own."""
+    import multiprocessing as mp
+    ctx = mp.get_context('spawn')
+    queue = ctx.Queue()
+    saved = os.environ.get('GPU_MAX_HW_QUEUES')
+    os.environ['GPU_MAX_HW_QUEUES'] = '16'
+    try:
+        proc = ctx.Process(target=_ordering_child, args=(queue,))
+        proc.start()
+    finally:
+        if saved is None:
+            os.environ.pop('GPU_MAX_HW_QUEUES')
+        else:
+            os.environ['GPU_MAX_HW_QUEUES'] = saved
+    try:
+        out = queue.get(timeout=150)
+    finally:
+        proc.join(timeout=30)
+        if proc.is_alive():
+            proc.kill()
+    assert isinstance(out, dict), out
+    world = 4
+    for drop_wait, results in out.items():
         assert len(results) == world and all(isinstance(v, bool) for v in results.values()), results
         if drop_wait:
             assert not all(results.values()), 'a schedule without the exchange wait went undetected'

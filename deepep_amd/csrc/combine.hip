@@ -203,6 +203,10 @@ __device__ __forceinline__ void combine_item(const Params& p, int64_t it, int nc
     //      written once per unit by the wave owning chunk 0: gathered here, stored after the row
     uint16_t* const out_row = p.out_rows != nullptr ? reinterpret_cast<uint16_t*>(p.out_rows[u])
                                                      : p.out + u * p.out_stride;
+    if (out_row == nullptr) {                            // no window row (plan_expert rejected the unit)
+        if (lane == 0 && c == 0 && p.error_flag != nullptr) atomicOr(p.error_flag, 1);
+        return;
+    }
     const bool wlane = c == 0 && p.num_weights > 0 && lane < p.weights_pad;
     const float wv = wlane ? pass_through_weight<kWeighted>(p, u, lane, my_slot, my_w) : 0.0f;
 
@@ -436,6 +440,10 @@ combine_stream_kernel(const Params p) {
 
     uint16_t* const out_row = p.out_rows != nullptr ? reinterpret_cast<uint16_t*>(p.out_rows[u])
                                                      : p.out + u * p.out_stride;
+    if (out_row == nullptr) {                            // no window row (plan_expert rejected the unit)
+        if (lane == 0 && p.error_flag != nullptr) atomicOr(p.error_flag, 1);
+        continue;
+    }
     const bool wlane = p.num_weights > 0 && lane < p.weights_pad;     // top-k weight pass-through, once per unit
     const float wv = wlane ? pass_through_weight<kWeighted>(p, u, lane, my_slot, my_w) : 0.0f;
 

@@ -128,7 +128,11 @@ plan_expert_kernel(const int32_t* __restrict__ meta, int K, int R, int rank, int
         }
         if (out_rows != nullptr) {
             const int src = m[1] / K, slot = rank_layout ? rank : m[1] % K, st = m[0] % t_max;
-            out_rows[u] = bases[src] + static_cast<uint64_t>(static_cast<int64_t>(slot) * t_max + st) * row_bytes;
+            // metadata that cannot come from a correct dispatch never becomes a window address: the row
+            // is 0 (phase A skips the unit and flags the call) instead of a store anywhere in memory
+            const bool ok = m[0] >= 0 && m[1] >= 0 && src < R;
+            out_rows[u] = ok ? bases[src] + static_cast<uint64_t>(static_cast<int64_t>(slot) * t_max + st) * row_bytes
+                             : 0ull;
         }
         return;
     }
@@ -146,7 +150,9 @@ plan_expert_kernel(const int32_t* __restrict__ meta, int K, int R, int rank, int
         table_a[u] = slot;
         if (out_rows != nullptr) {
             const int src = m[1] / K, st = m[0] % t_max;
-            out_rows[u] = bases[src] + static_cast<uint64_t>(static_cast<int64_t>(k) * t_max + st) * row_bytes;
+            const bool ok = m[0] >= 0 && m[1] >= 0 && src < R;
+            out_rows[u] = ok ? bases[src] + static_cast<uint64_t>(static_cast<int64_t>(k) * t_max + st) * row_bytes
+                             : 0ull;
         }
     }
 }

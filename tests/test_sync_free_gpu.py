@@ -314,6 +314,29 @@ def test_dispatch_without_cpu_sync_then_combine(capture):
     assert np.array_equal(out_w.cpu().numpy(), w_all[0])
 
 
+def test_plan_expert_rejects_impossible_metadata(kern):
+    """Window addresses come only from metadata a correct dispatch can produce: a received row whose
+    source index or master lane is negative, or whose source rank is out of range, gets a null window
+    row (phase A then skips it and flags the call) -- never an address computed from garbage."""
+    from deepep_amd.handle import PLAN_EXPANDED, PLAN_RANK_LAYOUT
+    R, K, T_max, rank, row_bytes = 2, 2, 64, 1, 1024
+    meta = torch.tensor([[0, 0 * K + 1, 0, -1],          # source rank 0, token 0, master lane 1: valid
+                         [-5, 0 * K + 0, 1, -1],         # negative source index
+                         [64 + 3, 1 * K + 0, 2, -1],     # source rank 1, token 3: valid
+                         [64 + 9, 7 * K + 0, 3, -1]],    # source rank 7 of 2
+                        dtype=torch.int32, device='cuda')
+    recv_tok = torch.tensor([[2], [2]], dtype=torch.int32, device='cuda')
+    bases = torch.tensor([1 << 40, 2 << 40], dtype=torch.int64, device='cuda')
+    table_a = torch.empty((4, K), dtype=torch.int32, device='cuda')
+    out_rows = torch.empty((4,), dtype=torch.int64, device='cuda')
+    kern.plan_expert(meta, K, R, rank, T_max, recv_tok, recv_tok, 1, 1, PLAN_EXPANDED | PLAN_RANK_LAYOUT,
+                     table_a, None, bases, row_bytes, out_rows)
+    torch.cuda.synchronize()
+    expect = [(1 << 40) + (rank * T_max + 0) * row_bytes, 0, (2 << 40) + (rank * T_max + 3) * row_bytes, 0]
+    assert out_rows.tolist() == expect
+    assert table_a.tolist() == meta[:, 2:].tolist()
+
+
 # ----------------------------------------------------------------------------- stream ordering
 def _ordering_rank(rank, world, T, H, K, E, comm, drop_wait, results):
     try:

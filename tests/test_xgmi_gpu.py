@@ -421,7 +421,14 @@ def _full_worker(rank, world, port, queue):
         _, _, ex_w_r, handle_r, _ = bufs['rccl'].dispatch(x, topk_idx=idx, topk_weights=w, num_experts=E,
                                                           do_expand=True)
         if not torch.equal(handle.recv_src_metadata, handle_r.recv_src_metadata) or not torch.equal(ex_w, ex_w_r):
-            failures.append('xgmi dispatch != rccl dispatch')
+            meta_x, meta_r = handle.recv_src_metadata, handle_r.recv_src_metadata
+            bad = (meta_x != meta_r).any(dim=1).nonzero().flatten() if meta_x.shape == meta_r.shape else None
+            failures.append(f'xgmi dispatch != rccl dispatch: metadata shapes {tuple(meta_x.shape)} / '
+                            f'{tuple(meta_r.shape)}, differing rows '
+                            f'{None if bad is None else (bad.numel(), bad[:4].tolist())}, error flag '
+                            f'{int(bufs["xgmi"]._sym.error_flag.item())}')
+            queue.put((rank, failures))               # the combine would run on that metadata: stop here
+            return
         y = torch.randn((handle.num_expanded_tokens, H), device=dev, generator=g).to(torch.bfloat16)
         queue.put((rank, 'stage', 'dispatched'))
         for weighted in (False, True):

@@ -492,7 +492,8 @@ int deepep_dispatch_count(const void* packed, int64_t row_bytes, int idx_off, in
                           deepep_stream_t stream) {
     if (num_recv == 0) return DEEPEP_OK;                  // a rank that receives nothing
     if (num_recv < 0 || num_topk < 1 || num_topk > 32 || num_local_experts < 1 || num_local_experts > 1024 ||
-        num_ranks < 1 || src_metadata == nullptr || block_counts == nullptr || packed == nullptr)
+        num_ranks < 1 || src_metadata == nullptr || block_counts == nullptr || packed == nullptr ||
+        recv_rank_psum == nullptr)
         return deepep_amd_set_error(DEEPEP_ERR_INVALID_ARG, "dispatch_count: invalid arguments");
     const int nblocks = (num_recv + 255) / 256;
     hipLaunchKernelGGL(count_kernel, dim3(nblocks), dim3(256), num_local_experts * 4,

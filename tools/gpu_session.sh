@@ -47,6 +47,7 @@ for step in "$@"; do
         kphasecu) run kphasecu 300 python tools/kphase_cu.py ;;
         cumask) run cumask 120 python tools/probe_cumask.py ;;
         cubw)   run cubw 300 python tools/probe_cubw.py ;;
+        cubwspread) export CUBW_SPREAD=1; run cubwspread 300 python tools/probe_cubw.py; unset CUBW_SPREAD ;;
         probeld) run probeld 300 python tools/probe_ld.py ;;
         pmclist) run pmclist 120 rocprofv3 --list-avail ;;
         smi)    run smi 60 rocm-smi --showclocks --showpower --showtemp ;;

@@ -55,6 +55,10 @@ void launch(int grid, int scattered, hipStream_t s) {
 }
 }  // namespace
 
+int g_spread = 0;   // 0: the first `cus` bits; 1: per XCD, CU slots spread evenly over the XCD's CUs
+
+extern "C" void probe_cubw_set_spread(int spread) { g_spread = spread; }
+
 // cus: the first `cus` mask bits (bit b = CU b / 8 of XCD b % 8), 0 = the whole chip unmasked.
 // Returns the average microseconds per launch in *us, GB/s in *gbps.
 extern "C" int probe_cubw(int cus, int wg_per_cu, int L, int lds, int scattered, int iters, float* us, float* gbps) {
@@ -69,7 +73,16 @@ extern "C" int probe_cubw(int cus, int wg_per_cu, int L, int lds, int scattered,
     hipStream_t s = nullptr;
     if (cus > 0 && cus < n) {
         uint32_t mask[64] = {};
-        for (int b = 0; b < cus; ++b) mask[b / 32] |= 1u << (b % 32);
+        if (g_spread) {
+            const int per_xcd = n / 8, k = (cus + 7) / 8;         // CU slots per XCD in the mask, wanted
+            for (int x = 0; x < 8; ++x)
+                for (int j = 0; j < k; ++j) {
+                    const int b = (j * per_xcd / k) * 8 + x;
+                    mask[b / 32] |= 1u << (b % 32);
+                }
+        } else {
+            for (int b = 0; b < cus; ++b) mask[b / 32] |= 1u << (b % 32);
+        }
         if (hipExtStreamCreateWithCUMask(&s, (n + 31) / 32, mask) != hipSuccess) return -2;
     } else {
         cus = n;

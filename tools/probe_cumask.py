@@ -32,6 +32,18 @@ def main():
             per_xcc[x] = per_xcc.get(x, 0) + 1
         print(json.dumps(dict(tag=tag, bits=len(bits), distinct_cus=len(slots),
                               cus_per_xcc=dict(sorted(per_xcc.items())))), flush=True)
+        return slots
+
+    # which (shader engine, shader array, CU) each mask bit of XCD 0 selects (bit b = CU slot b // 8)
+    topo = {}
+    for b in range(0, n, 8):
+        mask = (ctypes.c_uint32 * words)()
+        mask[b // 32] |= 1 << (b % 32)
+        out = (ctypes.c_uint32 * (2 * 256))()
+        assert lib.probe_cumask(mask, words, 256, out) == 0
+        hw = out[0]
+        topo[b // 8] = [(hw >> 13) & 0x7, (hw >> 12) & 0x1, (hw >> 8) & 0xF]
+    print(json.dumps(dict(tag='xcd0_slot_to_se_sh_cu', map=topo)), flush=True)
 
     run(range(n), 'all')
     for k in (8, 16, 32, 64, 96, 128):

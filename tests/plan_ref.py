@@ -86,7 +86,9 @@ def plan_expert(meta, num_topk, num_ranks, rank, num_max_tokens, recv_tok, recv_
         table_a[u, 0] = m[ii, 2 + kk].to(torch.int32)
         if out_rows is not None:
             bases = window_bases.long().cpu()
-            out_rows[u] = (bases[src[ii]] + (kk * T_max + st[ii]) * window_row_bytes).to(out_rows.dtype)
+            ok = (m[ii, 0] >= 0) & (m[ii, 1] >= 0) & (src[ii] < R)        # else a null row (plan.hip)
+            addr = bases[src[ii].clamp(0, R - 1)] + (kk * T_max + st[ii]) * window_row_bytes
+            out_rows[u] = torch.where(ok, addr, torch.zeros_like(addr)).to(out_rows.dtype)
         return
     u = _positions(src, chunk, counts, R, bool(flags & INTERLEAVE))
     rows = torch.arange(n_recv)
@@ -99,7 +101,9 @@ def plan_expert(meta, num_topk, num_ranks, rank, num_max_tokens, recv_tok, recv_
     if out_rows is not None:
         slot = torch.full_like(src, rank) if flags & RANK_LAYOUT else m[:, 1] % K
         bases = window_bases.long().cpu()
-        out_rows[u] = (bases[src] + (slot * T_max + st) * window_row_bytes).to(out_rows.dtype)
+        ok = (m[:, 0] >= 0) & (m[:, 1] >= 0) & (src < R)                 # else a null row (plan.hip)
+        addr = bases[src.clamp(0, R - 1)] + (slot * T_max + st) * window_row_bytes
+        out_rows[u] = torch.where(ok, addr, torch.zeros_like(addr)).to(out_rows.dtype)
 
 
 def plan_source(topk_idx, num_experts, num_ranks, num_max_tokens, dst_slot, send_tok, send_pairs, num_blocks,

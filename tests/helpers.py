@@ -115,6 +115,7 @@ def dispatch_mode_checks(buf, x, topk_idx, topk_weights, num_experts: int, num_m
         worst = num_max_tokens * buf.num_ranks
         if rows(recv_x).shape[0] != worst or handle.recv_src_metadata.shape[0] != worst:
             fails.append('do_cpu_sync=False shapes are not worst-case')
+    recv_w_full = recv_w
     recv_x, recv_idx, recv_w = head(recv_x, n), recv_idx[:n], recv_w[:n]
     meta, ex_meta = handle.recv_src_metadata[:n], ex_handle.recv_src_metadata[:n]
     if not (same(head(c_x, n), recv_x) and torch.equal(c_idx[:n], recv_idx) and c_w is None):
@@ -171,4 +172,13 @@ def dispatch_mode_checks(buf, x, topk_idx, topk_weights, num_experts: int, num_m
         out_s, w_s, _ = buf.combine(y[:n_ex].contiguous(), s_handle, topk_weights=s_ex_w)
         if not (torch.equal(out_f.view(torch.int16), out_s.view(torch.int16)) and torch.equal(w_f, w_s)):
             fails.append('combine over a no-CPU-sync handle differs')
+        # the same for the received-token layout: one row per received token, worst-case padded
+        s_x, _, s_w, s_rhandle, _ = buf.dispatch(x, **dict(args, do_cpu_sync=True))
+        n_s = s_rhandle.recv_src_metadata.shape[0]
+        y_r = torch.randn((handle.recv_src_metadata.shape[0], rows(ex_x).shape[1]), generator=g,
+                          device=rows(ex_x).device).to(torch.bfloat16)
+        out_f, w_f, _ = buf.combine(y_r, handle, topk_weights=recv_w_full)
+        out_s, w_s, _ = buf.combine(y_r[:n_s].contiguous(), s_rhandle, topk_weights=s_w)
+        if not (torch.equal(out_f.view(torch.int16), out_s.view(torch.int16)) and torch.equal(w_f, w_s)):
+            fails.append('non-expanded combine over a no-CPU-sync handle differs')
     return fails

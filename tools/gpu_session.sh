@@ -78,6 +78,7 @@ for step in "$@"; do
                     run pmcp_$c 300 timeout -s KILL 120 rocprofv3 --pmc $c -d $OUT/pmcp_$c -o pmc --output-format csv -- python3 tools/pmc_run.py --plain
                 done ;;
         probe)  run probe 600 python tools/probe.py ;;
+        probeburst) export PROBE_BURST=1; run probeburst 600 python tools/probe.py; unset PROBE_BURST ;;
         *) echo "unknown step $step" ;;
     esac
 done

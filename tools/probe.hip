@@ -211,6 +211,80 @@ __global__ void __launch_bounds__(256) gather_store(const uint16_t* src, const i
     }
 }
 
+// ---- write-burst probe: a workgroup of 8 waves reduces 8 consecutive items (16 KiB of contiguous
+//      output at H = 7168: items are row-major chunks) into LDS, then stores the 16 KiB as one burst
+//      with all 512 threads (sc1), instead of each wave storing its 2 KiB as soon as it is done.
+//      kRounds > 1: a persistent workgroup buffers kRounds such groups (kRounds x 16 KiB) per burst.
+template <int kRounds>
+__global__ void __launch_bounds__(512) gather_burst(const uint16_t* src, const int32_t* table, uint16_t* out,
+                                                    int T, int hidden) {
+    constexpr int K = 8;
+    __shared__ u32x4 s_out[kRounds][8][128];                 // [round][wave][2 x 64 lanes]
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int nvec = hidden / 8;
+    const int nchunks = nvec / 128;
+    const int64_t items = (int64_t)T * nchunks;
+    for (int64_t g0 = (int64_t)blockIdx.x * 8 * kRounds; g0 < items; g0 += (int64_t)gridDim.x * 8 * kRounds) {
+#pragma unroll
+        for (int r = 0; r < kRounds; ++r) {
+            const int64_t it = g0 + r * 8 + wave;
+            if (it >= items) continue;
+            const int64_t t = it / nchunks;
+            const int c = (int)(it - t * nchunks);
+            float a[2][8] = {};
+            u32x4 v[K][2];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int64_t srow = __builtin_amdgcn_readfirstlane(table[t * K + k]);
+                const u32x4* row = reinterpret_cast<const u32x4*>(src + srow * hidden) + c * 128 + lane;
+                v[k][0] = __builtin_nontemporal_load(row);
+                v[k][1] = __builtin_nontemporal_load(row + 64);
+            }
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+#pragma unroll
+                    for (int d = 0; d < 4; ++d) {
+                        a[h][2 * d] += lo(v[k][h][d]);
+                        a[h][2 * d + 1] += hi(v[k][h][d]);
+                    }
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                u32x4 q;
+#pragma unroll
+                for (int d = 0; d < 4; ++d) q[d] = pack(a[h][2 * d], a[h][2 * d + 1]);
+                s_out[r][wave][h * 64 + lane] = q;
+            }
+        }
+        __syncthreads();
+        // the group's items are consecutive, so its output is one contiguous run of 8 x kRounds x 2 KiB
+        const int64_t n_it = min((int64_t)8 * kRounds, items - g0);
+        const u32x4* flat = &s_out[0][0][0];
+        u32x4* dst = reinterpret_cast<u32x4*>(out) + g0 * 128;
+        __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(dst, 0, (int)(n_it * 2048), 0x00020000);
+        for (int i = threadIdx.x; i < 8 * kRounds * 128; i += 512)
+            __builtin_amdgcn_raw_buffer_store_b128(flat[i], rsrc, i * 16, 0, 16);
+        __syncthreads();
+    }
+}
+
+static int g_lds_pad = 0;      // extra dynamic LDS per workgroup (caps workgroups per CU: occupancy probe)
+extern "C" void probe_set_lds_pad(int bytes) { g_lds_pad = bytes; }
+
+extern "C" int probe_gather_burst(int rounds, int grid, const void* src, const int32_t* table, void* out, int T,
+                                  int hidden, hipStream_t s) {
+    const uint16_t* x = (const uint16_t*)src;
+    uint16_t* o = (uint16_t*)out;
+    const int64_t items = (int64_t)T * (hidden / 8 / 128);
+    if (grid <= 0) grid = (int)((items + 8 * rounds - 1) / (8 * rounds));
+    if (rounds == 1) hipLaunchKernelGGL((gather_burst<1>), dim3(grid), dim3(512), g_lds_pad, s, x, table, o, T, hidden);
+    else if (rounds == 2) hipLaunchKernelGGL((gather_burst<2>), dim3(grid), dim3(512), g_lds_pad, s, x, table, o, T, hidden);
+    else if (rounds == 4) hipLaunchKernelGGL((gather_burst<4>), dim3(grid), dim3(512), g_lds_pad, s, x, table, o, T, hidden);
+    else return -1;
+    return hipGetLastError();
+}
+
 extern "C" int probe_gather_store(int policy, int region, int noload, const void* src, const int32_t* table,
                                   void* out, int T, int hidden, hipStream_t s) {
     const uint16_t* x = (const uint16_t*)src;

@@ -78,6 +78,36 @@ def main():
             name = ('store ' if variant & 1 else 'nostore ') + ('seq ' if variant & 2 else 'table ') + \
                    ('nt ' if variant & 4 else 'plain ') + ('pipe' if variant & 8 else 'flat')
             res.append(dict(probe=f'gather {name} grid{grid}', us=round(us, 1), gbps=round(nbytes / us / 1e3, 1)))
+    if os.environ.get('PROBE_BURST'):
+        from deepep_amd.kernels import MODE_FUSED
+        res = []
+        lib.probe_gather_burst.argtypes = [I, I, P, P, P, I, I, P]
+        ref = torch.empty_like(out)
+        lib.probe_gather_store(16, 0, 0, y.data_ptr(), table.data_ptr(), ref.data_ptr(), T, H, st)
+        for rep in range(2):
+            for name, fn in [('gather_store sc1 (per-wave stores)',
+                              lambda: lib.probe_gather_store(16, 0, 0, y.data_ptr(), table.data_ptr(), out.data_ptr(),
+                                                             T, H, st))] + \
+                            [(f'gather_burst rounds{r} grid{g}',
+                              (lambda r=r, g=g: lib.probe_gather_burst(r, g, y.data_ptr(), table.data_ptr(),
+                                                                       out.data_ptr(), T, H, st)))
+                             for r, g in ((1, 0), (4, 0), (4, 512))] + \
+                            [(f'gather_burst rounds1 grid0 lds_pad{pad}',
+                              (lambda pad=pad: (lib.probe_set_lds_pad(pad), lib.probe_gather_burst(
+                                  1, 0, y.data_ptr(), table.data_ptr(), out.data_ptr(), T, H, st))[1]))
+                             for pad in (32768, 49152, 65536, 98304)] + \
+                            [('gather_burst rounds4 grid0 lds_pad0', (lambda: (lib.probe_set_lds_pad(0), lib.probe_gather_burst(
+                                  4, 0, y.data_ptr(), table.data_ptr(), out.data_ptr(), T, H, st))[1]))] + \
+                            [('product fused kernel, plain sum (8-wave workgroups, per-wave stores)',
+                              lambda: buf.kernels.combine_reduce(MODE_FUSED, y, out, T, table=table,
+                                                                 stream=torch.cuda.current_stream()) or 0)]:
+                out.zero_()
+                assert fn() == 0
+                torch.cuda.synchronize()
+                same = bool(torch.equal(out, ref)) if not name.startswith('product') else None
+                us = timeit(fn)
+                res.append(dict(probe=name, rep=rep, us=round(us, 1), gbps=round((gb_read + T * H * 2) / us / 1e3, 1),
+                                equal=same))
     for r in res:
         print(json.dumps(r), flush=True)
     dist.destroy_process_group()

@@ -12,7 +12,7 @@ from typing import Optional
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('DEEPEP_AMD_LIB', os.path.join(_HERE, 'libdeepep_amd.so'))
-SOURCES = [os.path.join(_HERE, 'csrc', f) for f in ('combine.hip', 'dispatch.hip', 'symmetric.hip', 'plan.hip')]
+SOURCES = [os.path.join(_HERE, 'csrc', f) for f in ('combine.hip', 'dispatch.hip', 'symmetric.hip', 'plan.hip', 'fault.h')]
 HEADER = os.path.join(os.path.dirname(_HERE), 'include', 'deepep_amd.h')
 HIPCC_FLAGS = ['--offload-arch=gfx950', '-O3', '-fPIC', '-std=c++17', '-Wall']
 
@@ -38,9 +38,28 @@ def binary_build_id(path: str) -> Optional[str]:
         data = f.read()
     i = data.find(b'DEEPEP_BUILD_ID=')
     return data[i + 16:i + 32].decode(errors='replace') if i >= 0 else None
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 MODE_LOCAL, MODE_EPILOGUE, MODE_FUSED = 0, 1, 2
+
+# error record of the window paths (DEEPEP_ERROR_RECORD_INTS, DEEPEP_FLAG_*, DEEPEP_FAULT_*)
+ERROR_RECORD_INTS = 8
+FLAG_BAD_SLOT, FLAG_TIMEOUT, FLAG_BAD_ADDRESS = 1, 2, 4
+FAULT_NAMES = {1: 'scatter row outside every window', 2: 'plan window row past its window',
+               3: 'plan unit / received row out of range', 4: 'dispatch row past its destination buffer'}
+
+
+def describe_error_record(rec) -> str:
+    """Human-readable text of an error record (a sequence of DEEPEP_ERROR_RECORD_INTS ints)."""
+    rec = [int(v) for v in rec]
+    bits = [n for b, n in ((FLAG_BAD_SLOT, 'rejected slot / unit'), (FLAG_TIMEOUT, 'barrier timeout'),
+                           (FLAG_BAD_ADDRESS, 'address outside every window')) if rec[0] & b]
+    text = f'error flag {rec[0]} ({", ".join(bits) or "none"})'
+    if len(rec) > 6 and rec[1]:
+        addr = (rec[5] & 0xffffffff) << 32 | (rec[4] & 0xffffffff)
+        text += (f'; first fault: {FAULT_NAMES.get(rec[1], rec[1])}, unit/row {rec[2]}, rank/lane {rec[3]}, '
+                 f'address {addr:#x}, extent {rec[6]}')
+    return text
 
 # deepep_plan_* (include/deepep_amd.h)
 PLAN_BLOCK_TOKENS = 64
@@ -78,14 +97,14 @@ SIGNATURES = {
     'deepep_dispatch_route': (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P]),
     'deepep_dispatch_expert_counts': (_I, [_P, _I, _I, _I, _P, _P]),
     'deepep_dispatch_pack': (_I, [_P, _I64, _I, _P, _I64, _I, _P, _P, _I, _I, _I, _P, _P, _I,
-                                  _P, _P, _I64, _I, _I, _I, _I, _P, _P]),
+                                  _P, _P, _I64, _I64, _I, _I, _I, _I, _P, _P]),
     'deepep_dispatch_count': (_I, [_P, _I64, _I, _I, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P]),
     'deepep_dispatch_scan': (_I, [_P, _I, _I, _I, _I, _P, _P, _P]),
     'deepep_dispatch_slots': (_I, [_P, _I64, _I, _I, _I, _I, _I, _P, _P, _P]),
     'deepep_dispatch_copy': (_I, [_P, _I64, _I, _I, _I, _I, _I, _I, _P, _I, _P, _I64, _P, _I64, _I,
                                   _P, _P, _P, _I64, _P, _P]),
     'deepep_route_block_counts': (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P]),
-    'deepep_plan_expert': (_I, [_P, _I, _I, _I, _I, _P, _P, _I, _I, _I, _P, _P, _P, _I64, _P, _P]),
+    'deepep_plan_expert': (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _I, _I, _I, _P, _P, _P, _I64, _I64, _P, _P, _P]),
     'deepep_plan_source': (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I64, _I64, _P, _I, _P, _P]),
     'deepep_sym_alloc': (_I, [_I64, ctypes.POINTER(ctypes.c_void_p)]),
     'deepep_sym_free': (_I, [_P]),
@@ -99,7 +118,7 @@ SIGNATURES = {
     'deepep_stream_destroy': (_I, [_P]),
     'deepep_stream_probe_cus': (_I, [_P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     'deepep_combine_reduce_scatter': (_I, [_I, _P, _I64, _I64, _P, _I64, _I, _P, _P, _I, _I, _P, _I64, _P, _I,
-                                           _I64, _I, _P, _P]),
+                                           _I64, _I, _P, _I, _I64, _P, _P]),
 }
 
 

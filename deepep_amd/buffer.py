@@ -521,7 +521,8 @@ class ElasticBuffer(ExchangeMixin):
                 sym.barrier(stream)                               # peers finished reading their windows
                 kern.dispatch_pack(x_bytes, sf_bytes, idx64, w, r * num_max_tokens_per_rank, dst_slot,
                                    peer_offsets, None, layout, dest_bases=sym.data_bases_dev,
-                                   error_flag=sym.error_flag, stream=stream)
+                                   dest_rows=sym.data_bytes // layout.row_bytes, error_flag=sym.error_flag,
+                                   stream=stream)
                 sym.barrier(stream)                               # every row landed
                 if not self._capturing:
                     sym.publish(stream)

@@ -29,6 +29,7 @@
 #include <mutex>
 
 #include "../../include/deepep_amd.h"
+#include "fault.h"
 
 namespace {
 
@@ -100,7 +101,28 @@ struct Params {
     int64_t weights_offset;      // scatter: byte offset of the weights inside the output row
     int xcd_blocks;              // item kernel: 1 = XCD-contiguous workgroup order (see xcd_block)
     int cap_cus;                 // > 0: persistent grid, at most the workgroups this many CUs hold at once
+    const uint64_t* win_bases;   // scatter: the windows every out_rows[u] must lie in (lane l < win_count: window l)
+    int win_count;
+    uint64_t win_limit;          // scatter: largest offset of a row start inside a window (extent - row bytes)
 };
+
+// Scatter (phase A into the owners' windows): the byte address of unit u's row, or 0 when the unit must
+// not be stored -- a row plan_expert rejected (0, bit 1) or one not wholly inside any window (bit 4 and
+// the error record: a wild store through a bad address is never issued).  Wave-uniform.
+__device__ __forceinline__ uint64_t checked_row(const Params& p, int64_t u, int lane, bool report) {
+    const uint64_t a = p.out_rows[u];
+    if (a == 0ull) {
+        if (report && lane == 0 && p.error_flag != nullptr) atomicOr(p.error_flag, DEEPEP_FLAG_BAD_SLOT);
+        return 0ull;
+    }
+    const uint64_t base = lane < p.win_count ? p.win_bases[lane] : 0ull;
+    const bool inside = lane < p.win_count && (a & 15ull) == 0ull && a >= base && a - base <= p.win_limit;
+    if (__ballot(inside) != 0ull) return a;
+    if (report && lane == 0)
+        deepep::record_fault(p.error_flag, DEEPEP_FLAG_BAD_ADDRESS, DEEPEP_FAULT_SCATTER_ROW, u, -1, a,
+                             static_cast<int64_t>(p.win_limit >> 4));
+    return 0ull;
+}
 
 // Workgroups are dealt round-robin to the 8 XCDs (workgroup b runs on XCD b % 8).  With
 // xcd_blocks, workgroup b takes block xcd_block(b) instead, so each XCD works through one
@@ -201,12 +223,9 @@ __device__ __forceinline__ void combine_item(const Params& p, int64_t it, int nc
 
     // ---- top-k weight pass-through (combine.cuh:215-226, combine_reduce_epilogue.cuh:127-141),
     //      written once per unit by the wave owning chunk 0: gathered here, stored after the row
-    uint16_t* const out_row = p.out_rows != nullptr ? reinterpret_cast<uint16_t*>(p.out_rows[u])
+    uint16_t* const out_row = p.out_rows != nullptr ? reinterpret_cast<uint16_t*>(checked_row(p, u, lane, c == 0))
                                                      : p.out + u * p.out_stride;
-    if (out_row == nullptr) {                            // no window row (plan_expert rejected the unit)
-        if (lane == 0 && c == 0 && p.error_flag != nullptr) atomicOr(p.error_flag, 1);
-        return;
-    }
+    if (out_row == nullptr) return;                      // rejected / outside every window: flagged above
     const bool wlane = c == 0 && p.num_weights > 0 && lane < p.weights_pad;
     const float wv = wlane ? pass_through_weight<kWeighted>(p, u, lane, my_slot, my_w) : 0.0f;
 
@@ -438,12 +457,10 @@ combine_stream_kernel(const Params p) {
     const uint64_t valid = __ballot(my_slot >= 0);
     const int n = __popcll(valid);
 
-    uint16_t* const out_row = p.out_rows != nullptr ? reinterpret_cast<uint16_t*>(p.out_rows[u])
+    uint16_t* const out_row = p.out_rows != nullptr ? reinterpret_cast<uint16_t*>(checked_row(p, u, lane, true))
                                                      : p.out + u * p.out_stride;
-    if (out_row == nullptr) {                            // no window row (plan_expert rejected the unit)
-        if (lane == 0 && p.error_flag != nullptr) atomicOr(p.error_flag, 1);
-        continue;
-    }
+    if (out_row == nullptr) continue;                    // rejected / outside every window: flagged
+
     const bool wlane = p.num_weights > 0 && lane < p.weights_pad;     // top-k weight pass-through, once per unit
     const float wv = wlane ? pass_through_weight<kWeighted>(p, u, lane, my_slot, my_w) : 0.0f;
 
@@ -787,6 +804,9 @@ int deepep_combine_reduce(int mode, int weighted,
     p.weights_offset = 0;
     p.xcd_blocks = 0;
     p.cap_cus = 0;
+    p.win_bases = nullptr;
+    p.win_count = 0;
+    p.win_limit = 0;
 
     return launch_combine(mode, weighted, p, stream);
 }
@@ -798,6 +818,7 @@ int deepep_combine_reduce_scatter(int weighted,
                                   const uint64_t* out_rows, int num_units, int hidden,
                                   const int32_t* wtable, int64_t wtable_stride,
                                   const float* wsrc, int num_weights, int64_t weights_offset, int weights_pad,
+                                  const uint64_t* window_bases, int num_windows, int64_t window_bytes,
                                   int32_t* error_flag, deepep_stream_t stream) {
     if (num_units < 0 || hidden < 0)
         return set_error(DEEPEP_ERR_INVALID_ARG, "negative size (num_units=%d, hidden=%d)", num_units, hidden);
@@ -817,6 +838,12 @@ int deepep_combine_reduce_scatter(int weighted,
         return set_error(DEEPEP_ERR_INVALID_ARG, "weights need wsrc, num_weights <= %d and an offset past the row", kMaxWidth);
     if (weights_pad < num_weights) weights_pad = num_weights;
     if (weights_pad > 64) return set_error(DEEPEP_ERR_INVALID_ARG, "weights_pad > 64");
+    // the bytes one unit stores: the bf16 row, then (with weights) weights_pad floats at weights_offset
+    const int64_t row_extent = num_weights > 0 ? std::max<int64_t>(int64_t(hidden) * 2, weights_offset + 4 * weights_pad)
+                                               : int64_t(hidden) * 2;
+    if (window_bases == nullptr || num_windows < 1 || num_windows > 64 || window_bytes < row_extent)
+        return set_error(DEEPEP_ERR_INVALID_ARG, "scatter needs 1..64 windows of at least one row (%lld bytes)",
+                         static_cast<long long>(row_extent));
     Params p;
     p.src = static_cast<const uint16_t*>(src);
     p.num_src_rows = num_src_rows;
@@ -844,6 +871,9 @@ int deepep_combine_reduce_scatter(int weighted,
     p.weights_offset = weights_offset;
     p.xcd_blocks = 0;
     p.cap_cus = 0;
+    p.win_bases = window_bases;
+    p.win_count = num_windows;
+    p.win_limit = static_cast<uint64_t>(window_bytes - row_extent);
     return launch_combine(DEEPEP_MODE_LOCAL, weighted, p, stream);
 }
 

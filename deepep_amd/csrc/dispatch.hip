@@ -22,6 +22,7 @@
 #include <algorithm>
 
 #include "../../include/deepep_amd.h"
+#include "fault.h"
 
 extern "C" __attribute__((visibility("hidden"))) int deepep_amd_set_error(int code, const char* msg);
 
@@ -149,7 +150,7 @@ pack_kernel(const uint8_t* __restrict__ x, int64_t x_stride, int x_bytes,
             const int64_t* __restrict__ topk_idx, const float* __restrict__ topk_weights, int K,
             int32_t src_base, const int32_t* __restrict__ dst_slot, const int32_t* __restrict__ send_offsets, int R,
             uint8_t* __restrict__ packed, const uint64_t* __restrict__ dest_bases, int64_t row_bytes,
-            int sf_off, int idx_off, int w_off, int src_off, const int32_t* __restrict__ error_flag) {
+            int64_t dest_rows, int sf_off, int idx_off, int w_off, int src_off, int32_t* __restrict__ error_flag) {
     const int t = blockIdx.x, lane = threadIdx.x;
     // the window barrier before this push timed out (bit 2): the peers may still read their
     // windows, so nothing is stored into them (the call's results are invalid and the next call raises)
@@ -157,12 +158,19 @@ pack_kernel(const uint8_t* __restrict__ x, int64_t x_stride, int x_bytes,
         (__hip_atomic_load(error_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 2))
         return;
     // lane r holds the byte address of the destination row for rank r (0: not routed to r)
+    // (a row index outside the destination buffer -- offsets or slots that disagree with its size -- is
+    // never stored: bit 4 and the error record instead of a write past a window)
     uint64_t my_row = 0;
     if (lane < R) {
         const int32_t s = dst_slot[static_cast<int64_t>(t) * R + lane];
         if (s >= 0) {
             const uint64_t base = kPeer ? dest_bases[lane] : reinterpret_cast<uint64_t>(packed);
-            my_row = base + static_cast<uint64_t>(static_cast<int64_t>(send_offsets[lane]) + s) * row_bytes;
+            const int64_t row = static_cast<int64_t>(send_offsets[lane]) + s;
+            if (row >= 0 && row < dest_rows)
+                my_row = base + static_cast<uint64_t>(row) * row_bytes;
+            else
+                deepep::record_fault(error_flag, DEEPEP_FLAG_BAD_ADDRESS, DEEPEP_FAULT_PACK_ROW, t, lane,
+                                     base + static_cast<uint64_t>(row) * row_bytes, dest_rows);
         }
     }
     const uint64_t dmask = __ballot(my_row != 0);
@@ -461,11 +469,12 @@ int deepep_dispatch_pack(const void* x, int64_t x_row_stride_bytes, int x_bytes,
                          const void* sf, int64_t sf_row_stride_bytes, int sf_bytes,
                          const int64_t* topk_idx, const float* topk_weights, int num_tokens, int num_topk,
                          int32_t src_base, const int32_t* dst_slot, const int32_t* send_offsets, int num_ranks,
-                         void* packed, const uint64_t* dest_bases, int64_t row_bytes,
-                         int sf_off, int idx_off, int w_off, int src_off, const int32_t* error_flag,
+                         void* packed, const uint64_t* dest_bases, int64_t row_bytes, int64_t dest_rows,
+                         int sf_off, int idx_off, int w_off, int src_off, int32_t* error_flag,
                          deepep_stream_t stream) {
     if (num_tokens == 0) return DEEPEP_OK;
     if (num_tokens < 0 || num_topk < 1 || num_topk > 32 || num_ranks < 1 || num_ranks > 64 || x_bytes % 16 ||
+        dest_rows < 0 || row_bytes < src_off + 4 ||
         sf_bytes % 4 || row_bytes % 16 || !a16(x) || (dest_bases == nullptr && !a16(packed)) ||
         x_row_stride_bytes % 16 || idx_off % 8 || w_off % 4 || src_off % 4 || (sf_bytes > 0 && sf == nullptr) ||
         (dest_bases == nullptr && packed == nullptr))
@@ -476,13 +485,15 @@ int deepep_dispatch_pack(const void* x, int64_t x_row_stride_bytes, int x_bytes,
                            static_cast<const uint8_t*>(x), x_row_stride_bytes, x_bytes,
                            static_cast<const uint8_t*>(sf), sf_row_stride_bytes, sf_bytes,
                            topk_idx, topk_weights, num_topk, src_base, dst_slot, send_offsets, num_ranks,
-                           static_cast<uint8_t*>(packed), dest_bases, row_bytes, sf_off, idx_off, w_off, src_off, error_flag);
+                           static_cast<uint8_t*>(packed), dest_bases, row_bytes, dest_rows, sf_off, idx_off, w_off, src_off,
+                           error_flag);
     else
         hipLaunchKernelGGL(pack_kernel<false>, dim3(num_tokens), dim3(64), 0, s,
                            static_cast<const uint8_t*>(x), x_row_stride_bytes, x_bytes,
                            static_cast<const uint8_t*>(sf), sf_row_stride_bytes, sf_bytes,
                            topk_idx, topk_weights, num_topk, src_base, dst_slot, send_offsets, num_ranks,
-                           static_cast<uint8_t*>(packed), dest_bases, row_bytes, sf_off, idx_off, w_off, src_off, error_flag);
+                           static_cast<uint8_t*>(packed), dest_bases, row_bytes, dest_rows, sf_off, idx_off, w_off, src_off,
+                           error_flag);
     return launch_status("dispatch_pack");
 }
 

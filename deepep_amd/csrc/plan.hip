@@ -18,6 +18,7 @@
 #include <stdio.h>
 
 #include "../../include/deepep_amd.h"
+#include "fault.h"
 
 extern "C" __attribute__((visibility("hidden"))) int deepep_amd_set_error(int code, const char* msg);
 
@@ -75,10 +76,11 @@ block_counts_kernel(const int64_t* __restrict__ topk_idx, int T, int K, int epr,
 // the xGMI stores then reach every peer at once) -- unit p of source s goes to position
 // sum_{s'} min(n_{s'}, p + [s' < s]), the stable sort of (p * R + s).
 __global__ void __launch_bounds__(64)
-plan_expert_kernel(const int32_t* __restrict__ meta, int K, int R, int rank, int t_max,
+plan_expert_kernel(const int32_t* __restrict__ meta, int num_recv, int K, int R, int rank, int t_max,
                    const int32_t* __restrict__ recv_tok, const int32_t* __restrict__ recv_pairs, int nb, int bpc,
                    int flags, int32_t* __restrict__ table_a, int32_t* __restrict__ wtable_a,
-                   const uint64_t* __restrict__ bases, int64_t row_bytes, uint64_t* __restrict__ out_rows) {
+                   const uint64_t* __restrict__ bases, int64_t row_bytes, int64_t window_bytes,
+                   uint64_t* __restrict__ out_rows, int32_t* __restrict__ err) {
     __shared__ int s_n[kMaxRanks];
     const int lane = threadIdx.x;
     const int s = blockIdx.x / nb, b = blockIdx.x - s * nb;
@@ -105,6 +107,7 @@ plan_expert_kernel(const int32_t* __restrict__ meta, int K, int R, int rank, int
     __syncthreads();
     const int seg_row0 = wave_sum(lane < s ? rows_l : 0) + __shfl(rows_s_before, s, 64);
     const int chunk_base = wave_sum(before_l);
+    const int chunk_units = wave_sum(n_l);                      // units of the whole chunk
     const int grouped_base = wave_sum(lane < s ? n_l : 0);
     p0 = __shfl(p0, s, 64);
     auto position = [&](int p) -> int {                         // unit p of source s inside the chunk
@@ -114,11 +117,38 @@ plan_expert_kernel(const int32_t* __restrict__ meta, int K, int R, int rank, int
         return pos;
     };
     const int i = seg_row0 + lane;                              // this lane's received row
-    const bool active = lane < seg_len;
-    const int32_t* m = meta + static_cast<int64_t>(i) * (K + 2);
+    // counts that disagree with the metadata (a row past the received ones) write nothing for the lane:
+    // its units keep the caller's -1 / 0 fill and are skipped by phase A.  The lane stays in the wave
+    // (the single reduction's scan below needs every lane).
+    const bool past_recv = lane < seg_len && i >= num_recv;
+    if (past_recv) deepep::record_fault(err, DEEPEP_FLAG_BAD_SLOT, DEEPEP_FAULT_PLAN_UNIT, i, s, 0, num_recv);
+    const bool active = lane < seg_len && !past_recv;
+    const int32_t* m = meta + static_cast<int64_t>(active ? i : 0) * (K + 2);
+    // the window row of (source, slot, token), or 0 unless all of its bytes lie inside that window
+    auto window_row = [&](int64_t u, int slot) -> uint64_t {
+        const int src = m[1] / K, st = m[0] % t_max;
+        if (m[0] < 0 || m[1] < 0 || src >= R) {                 // metadata no correct dispatch produces
+            deepep::record_fault(err, DEEPEP_FLAG_BAD_SLOT, DEEPEP_FAULT_PLAN_ROW, u, src, 0, m[0]);
+            return 0ull;
+        }
+        const int64_t off = (static_cast<int64_t>(slot) * t_max + st) * row_bytes;
+        if (slot < 0 || off + row_bytes > window_bytes) {
+            deepep::record_fault(err, DEEPEP_FLAG_BAD_SLOT, DEEPEP_FAULT_PLAN_ROW, u, src, bases[src] + off,
+                                 window_bytes >> 4);
+            return 0ull;
+        }
+        return bases[src] + static_cast<uint64_t>(off);
+    };
+    auto in_chunk = [&](int64_t pos) -> bool {
+        if (pos >= 0 && pos < chunk_units) return true;
+        deepep::record_fault(err, DEEPEP_FLAG_BAD_SLOT, DEEPEP_FAULT_PLAN_UNIT, chunk_base + pos, s, 0, chunk_units);
+        return false;
+    };
     if (!single) {
         if (!active) return;
-        const int64_t u = chunk_base + position(p0 + lane);
+        const int pos = position(p0 + lane);
+        if (!in_chunk(pos)) return;
+        const int64_t u = chunk_base + pos;
         if (expanded) {
             for (int k = 0; k < K; ++k) table_a[u * K + k] = m[2 + k];
         } else {
@@ -126,14 +156,8 @@ plan_expert_kernel(const int32_t* __restrict__ meta, int K, int R, int rank, int
             if (wtable_a != nullptr)
                 for (int k = 0; k < K; ++k) wtable_a[u * K + k] = i * K + k;
         }
-        if (out_rows != nullptr) {
-            const int src = m[1] / K, slot = rank_layout ? rank : m[1] % K, st = m[0] % t_max;
-            // metadata that cannot come from a correct dispatch never becomes a window address: the row
-            // is 0 (phase A skips the unit and flags the call) instead of a store anywhere in memory
-            const bool ok = m[0] >= 0 && m[1] >= 0 && src < R;
-            out_rows[u] = ok ? bases[src] + static_cast<uint64_t>(static_cast<int64_t>(slot) * t_max + st) * row_bytes
-                             : 0ull;
-        }
+        // a row that is not provably inside its window is 0: phase A skips the unit and flags the call
+        if (out_rows != nullptr) out_rows[u] = window_row(u, rank_layout ? rank : m[1] % K);
         return;
     }
     // single reduction: one unit per valid (row, lane), (row, lane) order
@@ -146,14 +170,11 @@ plan_expert_kernel(const int32_t* __restrict__ meta, int K, int R, int rank, int
     for (int k = 0; k < K; ++k) {
         const int32_t slot = m[2 + k];
         if (slot < 0) continue;
-        const int64_t u = chunk_base + position(p++);
+        const int pos = position(p++);
+        if (!in_chunk(pos)) return;
+        const int64_t u = chunk_base + pos;
         table_a[u] = slot;
-        if (out_rows != nullptr) {
-            const int src = m[1] / K, st = m[0] % t_max;
-            const bool ok = m[0] >= 0 && m[1] >= 0 && src < R;
-            out_rows[u] = ok ? bases[src] + static_cast<uint64_t>(static_cast<int64_t>(k) * t_max + st) * row_bytes
-                             : 0ull;
-        }
+        if (out_rows != nullptr) out_rows[u] = window_row(u, k);
     }
 }
 
@@ -271,22 +292,25 @@ int deepep_route_block_counts(const int64_t* topk_idx, int num_tokens, int num_t
     return launch_status("route_block_counts");
 }
 
-int deepep_plan_expert(const int32_t* src_metadata, int num_topk, int num_ranks, int rank, int num_max_tokens,
-                       const int32_t* recv_tok, const int32_t* recv_pairs, int num_blocks, int blocks_per_chunk,
-                       int flags, int32_t* table_a, int32_t* wtable_a, const uint64_t* window_bases,
-                       int64_t window_row_bytes, uint64_t* out_rows, deepep_stream_t stream) {
+int deepep_plan_expert(const int32_t* src_metadata, int num_recv, int num_topk, int num_ranks, int rank,
+                       int num_max_tokens, const int32_t* recv_tok, const int32_t* recv_pairs, int num_blocks,
+                       int blocks_per_chunk, int flags, int32_t* table_a, int32_t* wtable_a,
+                       const uint64_t* window_bases, int64_t window_row_bytes, int64_t window_bytes,
+                       uint64_t* out_rows, int32_t* error_flag, deepep_stream_t stream) {
     const bool single = flags & DEEPEP_PLAN_SINGLE;
-    if (num_topk < 1 || num_topk > kMaxTopk || num_ranks < 1 || num_ranks > kMaxRanks || rank < 0 ||
+    if (num_recv < 0 || num_topk < 1 || num_topk > kMaxTopk || num_ranks < 1 || num_ranks > kMaxRanks || rank < 0 ||
         rank >= num_ranks || num_max_tokens < 1 || num_blocks < 0 || blocks_per_chunk < 1 ||
         (num_blocks > 0 && (recv_tok == nullptr || (single && recv_pairs == nullptr))) ||
-        (out_rows != nullptr && (window_bases == nullptr || window_row_bytes <= 0 || window_row_bytes % 16)) ||
+        (num_recv > 0 && src_metadata == nullptr) ||
+        (out_rows != nullptr && (window_bases == nullptr || window_row_bytes <= 0 || window_row_bytes % 16 ||
+                                 window_bytes < window_row_bytes)) ||
         (single && (flags & DEEPEP_PLAN_EXPANDED) == 0))
         return deepep_amd_set_error(DEEPEP_ERR_INVALID_ARG, "plan_expert: invalid arguments");
     if (num_blocks == 0) return DEEPEP_OK;
     hipLaunchKernelGGL(plan_expert_kernel, dim3(num_ranks * num_blocks), dim3(64), 0,
-                       reinterpret_cast<hipStream_t>(stream), src_metadata, num_topk, num_ranks, rank,
+                       reinterpret_cast<hipStream_t>(stream), src_metadata, num_recv, num_topk, num_ranks, rank,
                        num_max_tokens, recv_tok, recv_pairs, num_blocks, blocks_per_chunk, flags, table_a, wtable_a,
-                       window_bases, window_row_bytes, out_rows);
+                       window_bases, window_row_bytes, window_bytes, out_rows, error_flag);
     return launch_status("plan_expert");
 }
 

@@ -22,6 +22,15 @@ from .kernels import MODE_EPILOGUE, MODE_LOCAL
 _WINDOW_IDS = itertools.count(1)            # symmetric windows created by this process
 
 
+def _require_weight_index(plan) -> None:
+    """The weight pass-through reads each lane's weight through int32 float indices into the packed
+    receive rows (handle.build_ep_plan leaves wtable_b None when they would overflow int32): raise
+    instead of reading the wrong floats (not an assert, so `python -O` keeps the check)."""
+    if any(ch.wtable_b is None for ch in plan.chunks):
+        raise RuntimeError('Assertion failed: the receive rows are too large for int32 weight indices '
+                           '(num_max_tokens_per_rank * hidden too large for the weight pass-through)')
+
+
 class ExchangeMixin:
     """EP > 1 exchange paths; uses the host attributes of ElasticBuffer (group, ranks, streams,
     kernels, _mark, _before_epilogue, _all_to_all)."""
@@ -46,7 +55,7 @@ class ExchangeMixin:
         row_elems = row_bytes // 2
         pipelined = len(plan.chunks) > 1 and self.use_cuda
         if with_w:
-            assert all(ch.wtable_b is not None for ch in plan.chunks), 'receive rows too large for int32 weight indices'
+            _require_weight_index(plan)
         if pipelined:
             if getattr(self, '_stream_b', None) is None:
                 self._stream_b = torch.cuda.Stream(device=self.device)
@@ -204,6 +213,9 @@ class ExchangeMixin:
         num_chunks = min(self._num_chunks(handle), 63)
         plan = self._plan(handle, False, num_chunks, hidden, window=sym)
         kern = self.kernels
+        if topk_weights is not None:
+            _require_weight_index(plan)
+        windows = (sym.data_bases_dev, sym.data_bytes)
         n_rows = self._window_slots * T_max
         rows = sym.data[:n_rows * row_bytes].view(torch.bfloat16).view(n_rows, row_bytes // 2)
         recv_wsrc = sym.data[:n_rows * row_bytes].view(torch.float32) if topk_weights is not None else None
@@ -227,7 +239,8 @@ class ExchangeMixin:
             kern.combine_reduce_scatter(x, ch.out_rows.shape[0], ch.out_rows, table=ch.table_a, row_weights=row_w,
                                         wtable=ch.wtable_a, wsrc=wsrc,
                                         num_weights=K if topk_weights is not None else 0,
-                                        weights_offset=w_off, weights_pad=w_pad, error_flag=err, stream=sa)
+                                        weights_offset=w_off, weights_pad=w_pad, error_flag=err, windows=windows,
+                                        stream=sa)
             self._mark(sa)
             sym.signal(1 + c, sa)
         if sa is not stream:
@@ -288,7 +301,7 @@ class ExchangeMixin:
             kern.combine_reduce_scatter(x, ch.out_rows.shape[0], ch.out_rows, table=ch.table_a,
                                         wtable=ch.table_a if with_w else None, wsrc=wsrc if with_w else None,
                                         num_weights=1 if with_w else 0, weights_offset=w_off, weights_pad=w_pad,
-                                        error_flag=err,
+                                        error_flag=err, windows=(sym.data_bases_dev, sym.data_bytes),
                                         stream=stream)
             self._mark(stream)
             sym.signal(1 + c, stream)

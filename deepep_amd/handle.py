@@ -126,16 +126,19 @@ def build_ep_plan(kern, handle: 'EPHandle', *, num_ranks: int, rank: int, single
     flags = ((PLAN_EXPANDED if expanded else 0) | (PLAN_SINGLE if single else 0) |
              (PLAN_RANK_LAYOUT if rank_layout and not single else 0) | (PLAN_INTERLEAVE if window is not None else 0))
     width_a = K if expanded and not single else 1
-    table_a = torch.empty((total, width_a), dtype=torch.int32, device=dev)
-    wtable_a = torch.empty((total, K), dtype=torch.int32, device=dev) if not expanded else None
+    # Pre-filled, so a unit the plan kernel does not write (counts that disagree with the metadata) is a
+    # skipped slot (-1) and a null window row (0) -- never stale allocator bytes used as an address.
+    table_a = torch.full((total, width_a), -1, dtype=torch.int32, device=dev)
+    wtable_a = torch.full((total, K), -1, dtype=torch.int32, device=dev) if not expanded else None
     if window is not None:
         row_bytes = packed_row_layout(hidden, K, True, single)[0]
-        out_rows = torch.empty((total,), dtype=torch.int64, device=dev)
-        bases = window.data_bases_dev
+        out_rows = torch.zeros((total,), dtype=torch.int64, device=dev)
+        bases, win_bytes, err = window.data_bases_dev, window.data_bytes, window.error_flag
     else:
-        row_bytes, out_rows, bases = 0, None, None
+        row_bytes, out_rows, bases, win_bytes, err = 0, None, None, 0, None
     kern.plan_expert(handle.recv_src_metadata, K, R, rank, T_max, cnt.dev[2], cnt.dev[3], nb, bpc, flags,
-                     table_a, wtable_a, bases, row_bytes, out_rows, stream=stream)
+                     table_a, wtable_a, bases, row_bytes, out_rows, window_bytes=win_bytes, error_flag=err,
+                     stream=stream)
     # ---- source side: the rows phase B reduces per owned token
     back = _chunk_sums(cnt.send_pairs if single else cnt.send_tok, bpc, C)       # [c][expert rank]
     width_b = K if single else min(R, K)

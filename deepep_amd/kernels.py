@@ -122,12 +122,19 @@ class HipKernels:
                                table: Optional[torch.Tensor] = None, row_weights: Optional[torch.Tensor] = None,
                                wtable: Optional[torch.Tensor] = None, wsrc: Optional[torch.Tensor] = None,
                                num_weights: int = 0, weights_offset: int = 0, weights_pad: int = 0,
-                               error_flag: Optional[torch.Tensor] = None, stream=None) -> None:
-        """Phase A storing unit u's row at byte address out_rows[u] (a peer window over xGMI)."""
+                               error_flag: Optional[torch.Tensor] = None, *, windows, stream=None) -> None:
+        """Phase A storing unit u's row at byte address out_rows[u] (a peer window over xGMI).
+        windows = (bases, bytes): int64 [n] device tensor of window data addresses and the extent of each;
+        a row not wholly inside one of them is skipped and flagged (error_flag: an error record of
+        _lib.ERROR_RECORD_INTS ints)."""
         _require(src.is_cuda and src.dtype == torch.bfloat16 and src.dim() == 2 and
                  (src.numel() == 0 or src.stride(1) == 1), 'combine rows must be 2-D bf16 on the GPU with unit column stride')
         _require(out_rows.is_cuda and out_rows.dtype == torch.int64 and out_rows.is_contiguous() and
                  out_rows.shape[0] >= num_units, 'out_rows must be int64 [num_units] on the GPU')
+        win_bases, win_bytes = windows
+        _require(win_bases.is_cuda and win_bases.dtype == torch.int64 and win_bases.is_contiguous() and
+                 win_bases.dim() == 1, 'window bases must be int64 [num_windows] on the GPU')
+        _require(error_flag is None or error_flag.numel() >= 1, 'error flag')
         t, t_stride, t_width = _table_view(table)
         w, w_stride, _ = _table_view(wtable)
         if num_weights:
@@ -138,8 +145,8 @@ class HipKernels:
         rc = self.lib.deepep_combine_reduce_scatter(
             int(row_weights is not None), ptr(src), src.shape[0], src.stride(0) if src.shape[0] > 0 else hidden,
             ptr(t), t_stride, t_width, ptr(row_weights), ptr(out_rows), num_units, hidden,
-            ptr(w), w_stride, ptr(wsrc), num_weights, weights_offset, weights_pad, ptr(error_flag),
-            _stream_handle(stream))
+            ptr(w), w_stride, ptr(wsrc), num_weights, weights_offset, weights_pad,
+            ptr(win_bases), win_bases.shape[0], int(win_bytes), ptr(error_flag), _stream_handle(stream))
         _lib.check(rc, 'combine_reduce_scatter')
 
     def build_local_plan(self, src_metadata: torch.Tensor, num_recv_tokens: int, num_topk: int,
@@ -187,16 +194,20 @@ class HipKernels:
 
     def plan_expert(self, meta, num_topk, num_ranks, rank, num_max_tokens, recv_tok, recv_pairs, num_blocks,
                     blocks_per_chunk, flags, table_a, wtable_a, window_bases, window_row_bytes, out_rows,
-                    stream=None):
+                    window_bytes: int = 0, error_flag=None, stream=None):
+        """window_bytes: the data extent of every window (out_rows rows are bounded by it); error_flag:
+        an error record (_lib.ERROR_RECORD_INTS ints) or None.  table_a / wtable_a / out_rows should be
+        pre-filled with -1 / -1 / 0: a unit the kernel rejects is left as it was."""
         _require(meta.is_cuda and meta.dtype == torch.int32 and meta.is_contiguous(), 'recv_src_metadata int32')
         _require(table_a.dtype == torch.int32 and table_a.is_contiguous(), 'table_a int32')
         _require(wtable_a is None or (wtable_a.dtype == torch.int32 and wtable_a.is_contiguous()), 'wtable_a int32')
         _require(out_rows is None or (out_rows.dtype == torch.int64 and out_rows.is_contiguous() and
-                                      window_bases is not None), 'out_rows int64 with window bases')
-        rc = self.lib.deepep_plan_expert(ptr(meta), num_topk, num_ranks, rank, num_max_tokens, ptr(recv_tok),
-                                         ptr(recv_pairs), num_blocks, blocks_per_chunk, flags, ptr(table_a),
-                                         ptr(wtable_a), ptr(window_bases), window_row_bytes, ptr(out_rows),
-                                         _stream_handle(stream))
+                                      window_bases is not None and window_bytes > 0),
+                 'out_rows int64 with window bases and extent')
+        rc = self.lib.deepep_plan_expert(ptr(meta), meta.shape[0], num_topk, num_ranks, rank, num_max_tokens,
+                                         ptr(recv_tok), ptr(recv_pairs), num_blocks, blocks_per_chunk, flags,
+                                         ptr(table_a), ptr(wtable_a), ptr(window_bases), window_row_bytes,
+                                         int(window_bytes), ptr(out_rows), ptr(error_flag), _stream_handle(stream))
         _lib.check(rc, 'plan_expert')
 
     def plan_source(self, topk_idx, num_experts, num_ranks, num_max_tokens, dst_slot, send_tok, send_pairs,
@@ -212,18 +223,25 @@ class HipKernels:
         _lib.check(rc, 'plan_source')
 
     def dispatch_pack(self, x_bytes, sf_bytes, topk_idx, topk_weights, src_base, dst_slot, send_offsets,
-                      packed, layout: RowLayout, dest_bases=None, error_flag=None, stream=None):
+                      packed, layout: RowLayout, dest_bases=None, dest_rows: Optional[int] = None, error_flag=None,
+                      stream=None):
         """x_bytes / sf_bytes: [T, bytes] uint8 views (rows may be strided).  dest_bases: optional
-        int64 [R] device tensor of per-destination buffer addresses (peer windows) instead of `packed`."""
+        int64 [R] device tensor of per-destination buffer addresses (peer windows) instead of `packed`;
+        dest_rows: the rows each destination holds (default: the rows of `packed`); a row past it is
+        not stored (flagged in error_flag, an error record of _lib.ERROR_RECORD_INTS ints)."""
         T, K = topk_idx.shape
         if dest_bases is not None:
             _require(dest_bases.is_cuda and dest_bases.dtype == torch.int64 and dest_bases.is_contiguous() and
                      dest_bases.numel() == dst_slot.shape[1], 'dest_bases must be int64 [num_ranks] on the GPU')
+            _require(dest_rows is not None, 'dest_rows (rows per destination window) is required with dest_bases')
+        else:
+            dest_rows = packed.shape[0] if dest_rows is None else min(dest_rows, packed.shape[0])
         rc = self.lib.deepep_dispatch_pack(
             ptr(x_bytes), x_bytes.stride(0) if T else layout.x_bytes, layout.x_bytes,
             ptr(sf_bytes), sf_bytes.stride(0) if sf_bytes is not None and T else 0, layout.sf_bytes,
             ptr(topk_idx), ptr(topk_weights), T, K, src_base, ptr(dst_slot), ptr(send_offsets),
-            dst_slot.shape[1], ptr(packed), ptr(dest_bases), layout.row_bytes, layout.sf_off, layout.idx_off,
+            dst_slot.shape[1], ptr(packed), ptr(dest_bases), layout.row_bytes, int(dest_rows), layout.sf_off,
+            layout.idx_off,
             layout.w_off, layout.src_off, ptr(error_flag), _stream_handle(stream))
         _lib.check(rc, 'dispatch_pack')
 

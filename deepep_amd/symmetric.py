@@ -59,7 +59,10 @@ class SymmetricBuffer:
         self.bases_dev = torch.tensor(bases, dtype=torch.int64, device=device)     # flags live at offset 0
         self.data_bases_dev = self.bases_dev + HEADER_BYTES
         self.data = torch.as_tensor(_DeviceArray(self.base + HEADER_BYTES, self.data_bytes), device=device)
-        self.error_flag = torch.zeros((1,), dtype=torch.int32, device=device)
+        # error record (_lib.ERROR_RECORD_INTS ints): [0] the flag bits every window kernel reads / sets,
+        # [1..] the first bad-address fault; error_flag is a view of [0] whose pointer is the record's
+        self.error_record = torch.zeros((_lib.ERROR_RECORD_INTS,), dtype=torch.int32, device=device)
+        self.error_flag = self.error_record[:1]
         self.epoch = 0
         self._slot_epoch = [0] * 64                 # split-barrier counters (slot 0 = the full barrier)
 
@@ -107,8 +110,8 @@ class SymmetricBuffer:
         sync); poll() reads it once it has landed.  Not for use inside a HIP-graph capture."""
         with torch.cuda.stream(stream):
             if getattr(self, '_flag_host', None) is None:
-                self._flag_host = torch.zeros((1,), dtype=torch.int32, pin_memory=True)
-            self._flag_host.copy_(self.error_flag, non_blocking=True)
+                self._flag_host = torch.zeros((_lib.ERROR_RECORD_INTS,), dtype=torch.int32, pin_memory=True)
+            self._flag_host.copy_(self.error_record, non_blocking=True)
             self._flag_event = torch.cuda.Event()
             self._flag_event.record(stream)
 
@@ -118,16 +121,23 @@ class SymmetricBuffer:
         ev = getattr(self, '_flag_event', None)
         if ev is not None and ev.query():
             self._flag_event = None
-            v = int(self._flag_host[0])
-            if v:
-                raise RuntimeError(f'deepep_amd: symmetric buffer error flag {v} (2 = barrier timeout): a peer '
-                                   f'did not arrive within num_gpu_timeout_secs; the last results are invalid')
+            rec = self._flag_host.tolist()
+            if rec[0]:
+                why = ('a peer did not arrive within num_gpu_timeout_secs' if rec[0] & _lib.FLAG_TIMEOUT else
+                       'a window address or plan entry was rejected (nothing was stored through it)')
+                raise RuntimeError(f'deepep_amd: symmetric buffer {_lib.describe_error_record(rec)}: {why}; '
+                                   f'the last results are invalid')
 
     def check(self) -> None:
-        """Raise if a barrier timed out (host sync)."""
-        v = int(self.error_flag.item())
-        if v:
-            raise RuntimeError(f'deepep_amd: symmetric buffer error flag {v} (2 = barrier timeout)')
+        """Raise if a barrier timed out or a window address was rejected (host sync)."""
+        rec = self.error_record.tolist()
+        if rec[0]:
+            raise RuntimeError(f'deepep_amd: symmetric buffer {_lib.describe_error_record(rec)}')
+
+    def reset_error(self) -> None:
+        """Clear the flag and the fault record (stream-ordered on the current stream)."""
+        self.error_record.zero_()
+        self._flag_event = None
 
     def destroy(self) -> None:
         if self.base is None:

@@ -48,12 +48,29 @@ extern "C" {
 
 typedef struct ihipStream_t* deepep_stream_t;   /* == hipStream_t */
 
-#define DEEPEP_AMD_ABI_VERSION 10
+#define DEEPEP_AMD_ABI_VERSION 11
 
 #define DEEPEP_OK               0
 #define DEEPEP_ERR_INVALID_ARG  (-1)
 #define DEEPEP_ERR_UNSUPPORTED  (-2)
 #define DEEPEP_ERR_HIP          (-3)
+
+/* Error record: the error_flag of the window paths (the scatter, plan_expert, the xGMI dispatch pack)
+ * points at DEEPEP_ERROR_RECORD_INTS device ints.  [0] = flag bits: 1 = a slot / unit was rejected
+ * (skipped, never dereferenced), 2 = a window barrier timed out, 4 = a computed window address fell
+ * outside every window (nothing stored there).  [1..7] = the first fault with bit 4 or a rejected plan
+ * entry: [1] kind (DEEPEP_FAULT_*), [2] unit / token / row, [3] rank / lane, [4] address low 32 bits,
+ * [5] address high 32 bits, [6] an extra value (the extent it exceeded, in 16-byte units).  The host
+ * layer raises RuntimeError with this record at the next call.  The other entry points that take an
+ * error_flag use [0] only. */
+#define DEEPEP_ERROR_RECORD_INTS 8
+#define DEEPEP_FLAG_BAD_SLOT     1
+#define DEEPEP_FLAG_TIMEOUT      2
+#define DEEPEP_FLAG_BAD_ADDRESS  4
+#define DEEPEP_FAULT_SCATTER_ROW 1   /* deepep_combine_reduce_scatter: out_rows[u] outside every window  */
+#define DEEPEP_FAULT_PLAN_ROW    2   /* deepep_plan_expert: window row past the window's data extent     */
+#define DEEPEP_FAULT_PLAN_UNIT   3   /* deepep_plan_expert: unit position / received row out of range     */
+#define DEEPEP_FAULT_PACK_ROW    4   /* deepep_dispatch_pack: destination row past the destination buffer */
 
 /* Reduction modes of deepep_combine_reduce. */
 #define DEEPEP_MODE_LOCAL     0   /* phase A: copy if 1 valid slot, hadd if 2, else fp32 sum   */
@@ -185,14 +202,17 @@ int deepep_dispatch_expert_counts(const int64_t* topk_idx, int num_tokens, int n
  * (dest_bases NULL: one local buffer for an all-to-all) or in rank r's buffer at dest_bases[r] (device
  * uint64 [num_ranks]: the peers' symmetric windows, system-scope stores -- the xGMI push of
  * dispatch.cuh:373-392); src_global_idx = src_base + t.  topk_weights may be NULL (zeros are sent).
- * error_flag (device int or NULL): with dest_bases, nothing is stored once bit 2 is set (the window
- * barrier before the push timed out). */
+ * dest_rows: rows every destination buffer holds (`packed`, or each peer window); a row index
+ * send_offsets[r] + dst_slot[t][r] outside [0, dest_rows) is not stored: bit 4 of error_flag is set and
+ * the fault recorded (DEEPEP_FAULT_PACK_ROW).  error_flag (device, DEEPEP_ERROR_RECORD_INTS ints, or
+ * NULL): with dest_bases, nothing is stored once bit 2 is set (the window barrier before the push timed
+ * out). */
 int deepep_dispatch_pack(const void* x, int64_t x_row_stride_bytes, int x_bytes,
                          const void* sf, int64_t sf_row_stride_bytes, int sf_bytes,
                          const int64_t* topk_idx, const float* topk_weights, int num_tokens, int num_topk,
                          int32_t src_base, const int32_t* dst_slot, const int32_t* send_offsets, int num_ranks,
-                         void* packed, const uint64_t* dest_bases, int64_t row_bytes,
-                         int sf_off, int idx_off, int w_off, int src_off, const int32_t* error_flag,
+                         void* packed, const uint64_t* dest_bases, int64_t row_bytes, int64_t dest_rows,
+                         int sf_off, int idx_off, int w_off, int src_off, int32_t* error_flag,
                          deepep_stream_t stream);
 
 /* Receive side, pass 1: src_metadata columns 0-1 ({src_global_idx, src_rank * K + master lane}),
@@ -262,11 +282,18 @@ int deepep_route_block_counts(const int64_t* topk_idx, int num_tokens, int num_t
  * may be NULL).  Single reduction: one unit per valid (row, lane) in (row, lane) order, table_a[u] =
  * the expanded row (1 wide).  out_rows (optional, the xGMI transport): byte address of unit u's row,
  * window_bases[src_rank] + (slot * num_max_tokens + src_token) * window_row_bytes, slot = rank (rank
- * layout) or the master lane (multiple reduction), the lane (single reduction) -- combine.cuh:96-106. */
-int deepep_plan_expert(const int32_t* src_metadata, int num_topk, int num_ranks, int rank, int num_max_tokens,
-                       const int32_t* recv_tok, const int32_t* recv_pairs, int num_blocks, int blocks_per_chunk,
-                       int flags, int32_t* table_a, int32_t* wtable_a, const uint64_t* window_bases,
-                       int64_t window_row_bytes, uint64_t* out_rows, deepep_stream_t stream);
+ * layout) or the master lane (multiple reduction), the lane (single reduction) -- combine.cuh:96-106.
+ * Bounds: a received row index >= num_recv (src_metadata rows) or a unit position past its chunk's unit
+ * count (counts that disagree with the metadata) writes nothing for that unit (DEEPEP_FAULT_PLAN_UNIT);
+ * a window row whose bytes do not lie inside [0, window_bytes) of its window, or metadata no correct
+ * dispatch produces, gives out_rows[u] = 0 (DEEPEP_FAULT_PLAN_ROW), which the scatter skips.  Callers
+ * pre-fill table_a / wtable_a with -1 and out_rows with 0, so an unwritten unit is never an address.
+ * error_flag: DEEPEP_ERROR_RECORD_INTS device ints or NULL (bit 1 and the record are set on a fault). */
+int deepep_plan_expert(const int32_t* src_metadata, int num_recv, int num_topk, int num_ranks, int rank,
+                       int num_max_tokens, const int32_t* recv_tok, const int32_t* recv_pairs, int num_blocks,
+                       int blocks_per_chunk, int flags, int32_t* table_a, int32_t* wtable_a,
+                       const uint64_t* window_bases, int64_t window_row_bytes, int64_t window_bytes,
+                       uint64_t* out_rows, int32_t* error_flag, deepep_stream_t stream);
 
 /* Source side, per owned token t (chunk c = t / B).  Multiple reduction: table_b [T][min(R, K)] = the
  * rows of t's partials in ascending dedup-master-lane order (a rank's master is its highest top-k
@@ -327,7 +354,12 @@ int deepep_sym_wait(const uint64_t* peer_flags, int rank, int num_ranks, int slo
  * with unit u's bf16 row stored at byte address out_rows[u] (any rank's window, 16-byte aligned)
  * and, when num_weights > 0, its top-k weights (the wtable / wsrc pass-through rule above, weights_pad
  * floats) at out_rows[u] + weights_offset.  All these stores are system-scope write-through (sc0 sc1),
- * so they are visible to the owning GPU once the kernel has completed. */
+ * so they are visible to the owning GPU once the kernel has completed.
+ * Windows: window_bases (device uint64 [num_windows]) and window_bytes, the data extent of each.  Every
+ * row is checked before it is stored: unless all its bytes (the bf16 row and, with weights, the weight
+ * tail) lie inside one window, the unit is skipped, bit 4 of error_flag is set and the fault recorded
+ * (DEEPEP_FAULT_SCATTER_ROW); out_rows[u] == 0 (a unit plan_expert rejected) is skipped with bit 1.
+ * error_flag: DEEPEP_ERROR_RECORD_INTS device ints or NULL. */
 int deepep_combine_reduce_scatter(int weighted,
                                   const void* src, int64_t num_src_rows, int64_t src_row_stride,
                                   const int32_t* table, int64_t table_stride, int table_width,
@@ -335,6 +367,7 @@ int deepep_combine_reduce_scatter(int weighted,
                                   const uint64_t* out_rows, int num_units, int hidden,
                                   const int32_t* wtable, int64_t wtable_stride,
                                   const float* wsrc, int num_weights, int64_t weights_offset, int weights_pad,
+                                  const uint64_t* window_bases, int num_windows, int64_t window_bytes,
                                   int32_t* error_flag, deepep_stream_t stream);
 
 /* A CU budget: a stream whose kernels run on `num_cus` compute units only, rounded up to a multiple

@@ -66,7 +66,8 @@ class OracleKernels:
         pairs.copy_(p)
 
     def plan_expert(self, meta, num_topk, num_ranks, rank, num_max_tokens, recv_tok, recv_pairs, num_blocks,
-                    blocks_per_chunk, flags, table_a, wtable_a, window_bases, window_row_bytes, out_rows, stream=None):
+                    blocks_per_chunk, flags, table_a, wtable_a, window_bases, window_row_bytes, out_rows,
+                    window_bytes=0, error_flag=None, stream=None):
         plan_ref.plan_expert(meta, num_topk, num_ranks, rank, num_max_tokens, recv_tok, recv_pairs, num_blocks,
                              blocks_per_chunk, flags, table_a, wtable_a, window_bases, window_row_bytes, out_rows)
 
@@ -90,7 +91,7 @@ class OracleKernels:
         counts.copy_(torch.bincount(valid, minlength=num_experts)[:num_experts].to(torch.int32))
 
     def dispatch_pack(self, x_bytes, sf_bytes, topk_idx, topk_weights, src_base, dst_slot, send_offsets,
-                      packed, layout, dest_bases=None, error_flag=None, stream=None):
+                      packed, layout, dest_bases=None, dest_rows=None, error_flag=None, stream=None):
         assert dest_bases is None, 'the CPU stand-in packs into one local buffer'
         t_idx, r_idx = (dst_slot >= 0).nonzero(as_tuple=True)
         dest = (send_offsets[r_idx] + dst_slot[t_idx, r_idx]).long()

@@ -160,7 +160,8 @@ def test_kernel_reduce_scatter_rows(kern, weighted, hidden):
     g_src, g_tab = _bf16(src), torch.from_numpy(table).cuda()
     g_w = torch.from_numpy(row_w).cuda()
     kern.combine_reduce_scatter(g_src, units, addr, table=g_tab, row_weights=g_w if weighted else None,
-                                wtable=g_tab, wsrc=g_w, num_weights=K, weights_offset=hidden * 2 + 16)
+                                wtable=g_tab, wsrc=g_w, num_weights=K, weights_offset=hidden * 2 + 16,
+                                windows=(torch.tensor([win.data_ptr()], device='cuda'), win.numel()))
     torch.cuda.synchronize()
     out = torch.empty((units, hidden), dtype=torch.bfloat16)
     out_w = torch.empty((units, K))
@@ -183,12 +184,14 @@ def test_kernel_poisoned_by_timed_out_barrier(kern):
     for flag, choice in ((2, 0), (3, 1), (2, 3)):
         assert kern.lib.deepep_set_kernel_choice(choice) == 0
         try:
-            err = torch.full((1,), flag, dtype=torch.int32, device='cuda')
+            err = torch.zeros((8,), dtype=torch.int32, device='cuda')
+            err[0] = flag
             out = torch.zeros((16, 1024), dtype=torch.bfloat16, device='cuda')
             kern.combine_reduce(MODE_FUSED, src, out, 16, table=table, error_flag=err)
             win = torch.zeros((16 * 2048,), dtype=torch.uint8, device='cuda')
             addr = torch.arange(16, device='cuda', dtype=torch.int64) * 2048 + win.data_ptr()
-            kern.combine_reduce_scatter(src, 16, addr, table=table, error_flag=err)
+            kern.combine_reduce_scatter(src, 16, addr, table=table, error_flag=err,
+                                        windows=(torch.tensor([win.data_ptr()], device='cuda'), win.numel()))
             torch.cuda.synchronize()
             assert bool(torch.isnan(out.float()).all()), flag
             assert int(win.count_nonzero()) == 0, flag
@@ -228,7 +231,8 @@ def test_kernel_weights_pad_fills_the_tail_line(kern, choice):
     win = torch.full((units, H + 128), 7.0, dtype=torch.bfloat16, device='cuda')
     addr = torch.arange(units, device='cuda', dtype=torch.int64) * (2 * H + 256) + win.data_ptr()
     kern.combine_reduce_scatter(src, units, addr, table=table, wtable=table, wsrc=wsrc, num_weights=K,
-                                weights_offset=2 * H, weights_pad=32)
+                                weights_offset=2 * H, weights_pad=32,
+                                windows=(torch.tensor([win.data_ptr()], device='cuda'), win.numel() * 2))
     torch.cuda.synchronize()
     assert torch.equal(win[:, :H], packed[:, :H])
     assert torch.equal(win.view(torch.float32)[:, H // 2:], tail)

@@ -107,7 +107,7 @@ def test_plan_kernels_match_reference(kern, world, K, T, chunks):
                         args = (K, world, r, T, recv_tok.to(dev), recv_pairs.to(dev), nb, bpc, flags, ta, wa,
                                 bases.to(dev) if window else None, 14400 if window else 0, orow)
                         if dev == 'cuda':
-                            kern.plan_expert(meta, *args)
+                            kern.plan_expert(meta, *args, window_bytes=K * T * 14400 if window else 0)
                         else:
                             plan_ref.plan_expert(meta.cpu(), *args)
                         outs.append([t.cpu() if t is not None else None for t in (ta, wa, orow)])
@@ -329,12 +329,15 @@ def test_plan_expert_rejects_impossible_metadata(kern):
     bases = torch.tensor([1 << 40, 2 << 40], dtype=torch.int64, device='cuda')
     table_a = torch.empty((4, K), dtype=torch.int32, device='cuda')
     out_rows = torch.empty((4,), dtype=torch.int64, device='cuda')
+    err = torch.zeros((8,), dtype=torch.int32, device='cuda')
     kern.plan_expert(meta, K, R, rank, T_max, recv_tok, recv_tok, 1, 1, PLAN_EXPANDED | PLAN_RANK_LAYOUT,
-                     table_a, None, bases, row_bytes, out_rows)
+                     table_a, None, bases, row_bytes, out_rows, window_bytes=K * T_max * row_bytes, error_flag=err)
     torch.cuda.synchronize()
     expect = [(1 << 40) + (rank * T_max + 0) * row_bytes, 0, (2 << 40) + (rank * T_max + 3) * row_bytes, 0]
     assert out_rows.tolist() == expect
     assert table_a.tolist() == meta[:, 2:].tolist()
+    rec = err.tolist()
+    assert rec[0] == 1 and rec[1] == 2, rec                # bit 1, DEEPEP_FAULT_PLAN_ROW recorded
 
 
 # ----------------------------------------------------------------------------- stream ordering

@@ -1,0 +1,186 @@
+"""Memory safety of the window paths (the xGMI transport) on the GPU: every address the product
+computes for a store into a symmetric window is checked against the windows' extents, and a bad one
+is never stored through -- it sets a flag bit and leaves a fault record (include/deepep_amd.h,
+DEEPEP_ERROR_RECORD_INTS) that the host turns into a RuntimeError.
+
+Each case feeds deliberately inconsistent inputs -- an out-of-window row address, counts that
+disagree with the metadata, a window too small for its rows, destination offsets past the buffer --
+and checks that (1) nothing outside the windows changed (canary regions around them stay zero),
+(2) the flag and the record name the fault, (3) the consistent units are still exact.  The "windows"
+here are regions of one local allocation, so a store that escaped the check would land in a canary
+(detected), not in unmapped memory.  Reference behaviour: the NVLink push only ever addresses rows
+of the registered window (deep_ep/common/handle.cuh:64-92, impls/combine.cuh:95-106 in
+/root/reference); the reference has no recovery path -- EP_DEVICE_ASSERT traps.
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from tests.oracle_kernels import OracleKernels
+
+pytestmark = pytest.mark.gpu
+
+MODE_LOCAL = 0
+FLAG_BAD_SLOT, FLAG_BAD_ADDRESS = 1, 4
+FAULT_SCATTER_ROW, FAULT_PLAN_ROW, FAULT_PLAN_UNIT, FAULT_PACK_ROW = 1, 2, 3, 4
+
+
+@pytest.fixture(scope='module')
+def kern():
+    from deepep_amd.kernels import HipKernels
+    assert torch.cuda.is_available()
+    return HipKernels()
+
+
+def _bf16(a: np.ndarray) -> torch.Tensor:
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.int16)).view(torch.bfloat16).cuda()
+
+
+def _addr(rec) -> int:
+    return (int(rec[5]) & 0xffffffff) << 32 | (int(rec[4]) & 0xffffffff)
+
+
+@pytest.mark.parametrize('choice', [-1, 1, 3, 5])
+def test_scatter_never_stores_outside_its_windows(kern, choice):
+    """Units whose row address is in a canary region, straddles a window's end, is misaligned or is
+    null are skipped; every other unit lands exactly; the first bad unit is recorded."""
+    rng = np.random.default_rng(7)
+    H, K, units = 1024, 8, 12
+    row_bytes = 2 * H + 128                          # bf16 row + a whole weight line
+    W = 6 * row_bytes                                # one window holds 6 rows
+    src = oracle.f32_to_bf16(rng.standard_normal((units * K, H)).astype(np.float32))
+    table = rng.integers(0, units * K, size=(units, K)).astype(np.int32)
+    wsrc = torch.rand(units * K, device='cuda')
+    buf = torch.zeros((5 * W,), dtype=torch.uint8, device='cuda')   # [win0 | canary | win1 | canary | canary]
+    base = buf.data_ptr()
+    wins = torch.tensor([base, base + 2 * W], dtype=torch.int64, device='cuda')
+    good = [base + 0 * row_bytes, base + 2 * W + 1 * row_bytes, base + 3 * row_bytes, base + 2 * W + 5 * row_bytes,
+            base + 5 * row_bytes, base + 2 * W]
+    bad = {6: base + W,                              # inside the first canary
+           7: base + W - row_bytes + 16,             # starts inside window 0, ends past it
+           8: base + 8,                              # not 16-byte aligned
+           9: base + 4 * W + 4096,                   # far past both windows (the last canary)
+           10: 0}                                    # a unit plan_expert rejected
+    addr = good + [bad[u] for u in range(6, 11)] + [base + 2 * W + 3 * row_bytes]
+    err = torch.zeros((8,), dtype=torch.int32, device='cuda')
+    assert kern.lib.deepep_set_kernel_choice(choice) == 0
+    try:
+        kern.combine_reduce_scatter(_bf16(src), units, torch.tensor(addr, dtype=torch.int64, device='cuda'),
+                                    table=torch.from_numpy(table).cuda(), wtable=torch.from_numpy(table).cuda(),
+                                    wsrc=wsrc, num_weights=K, weights_offset=2 * H, weights_pad=32,
+                                    error_flag=err, windows=(wins, W))
+        torch.cuda.synchronize()
+    finally:
+        kern.lib.deepep_set_kernel_choice(-1)
+    host = buf.cpu()
+    assert int(host[W:2 * W].count_nonzero()) == 0, 'a store escaped into canary 1'
+    assert int(host[3 * W:].count_nonzero()) == 0, 'a store escaped into canary 2'
+    out = torch.empty((units, H), dtype=torch.bfloat16)
+    out_w = torch.empty((units, K))
+    OracleKernels().combine_reduce(MODE_LOCAL, _bf16(src).cpu(), out, units, table=torch.from_numpy(table),
+                                   wtable=torch.from_numpy(table), wsrc=wsrc.cpu(), out_weights=out_w)
+    for u in list(range(6)) + [11]:
+        off = addr[u] - base
+        row = host[off:off + row_bytes]
+        assert torch.equal(row[:2 * H].view(torch.bfloat16), out[u]), u
+        assert torch.equal(row[2 * H:2 * H + 4 * K].view(torch.float32), out_w[u]), u
+    rec = err.tolist()
+    assert rec[0] == FLAG_BAD_SLOT | FLAG_BAD_ADDRESS, rec
+    assert rec[1] == FAULT_SCATTER_ROW and rec[2] in (6, 7, 8, 9) and _addr(rec) == bad[rec[2]], rec
+    # the unaligned row of unit 8 must not have been stored either (window 0 bytes 8.. belong to unit 0)
+    assert torch.equal(host[:2 * H].view(torch.bfloat16), out[0])
+
+
+def test_plan_expert_rejects_inconsistent_counts_and_small_windows(kern):
+    """Counts that claim more received rows than the metadata holds, single-reduction pair counts
+    below the metadata's valid lanes, and a window too small for a row: the affected units keep the
+    caller's fill (-1 slots, 0 rows) and the fault is recorded; consistent units are unchanged."""
+    from deepep_amd.handle import PLAN_EXPANDED, PLAN_INTERLEAVE, PLAN_RANK_LAYOUT, PLAN_SINGLE
+    R, K, T_max, rank, row_bytes = 2, 2, 64, 0, 1024
+    meta = torch.tensor([[0, 0 * K + 1, 0, 1],             # rank 0 token 0: both lanes local
+                         [1, 0 * K + 0, 2, -1],            # rank 0 token 1
+                         [64 + 3, 1 * K + 1, -1, 3],       # rank 1 token 3
+                         [64 + 60, 1 * K + 0, 4, -1]],     # rank 1 token 60 (window row 60)
+                        dtype=torch.int32, device='cuda')
+    bases = torch.tensor([1 << 40, 2 << 40], dtype=torch.int64, device='cuda')
+    flags = PLAN_EXPANDED | PLAN_RANK_LAYOUT | PLAN_INTERLEAVE
+
+    def run(recv_tok, recv_pairs, fl, total, width, window_bytes):
+        table = torch.full((total, width), -1, dtype=torch.int32, device='cuda')
+        rows = torch.zeros((total,), dtype=torch.int64, device='cuda')
+        err = torch.zeros((8,), dtype=torch.int32, device='cuda')
+        kern.plan_expert(meta, K, R, rank, T_max, recv_tok, recv_pairs, 1, 1, fl, table, None, bases, row_bytes,
+                         rows, window_bytes=window_bytes, error_flag=err)
+        torch.cuda.synchronize()
+        return table.cpu(), rows.cpu(), err.tolist()
+
+    ok = torch.tensor([[2], [2]], dtype=torch.int32, device='cuda')
+    pairs = torch.tensor([[3], [3]], dtype=torch.int32, device='cuda')
+    full = K * T_max * row_bytes
+    table, rows, rec = run(ok, pairs, flags, 4, K, full)
+    assert rec[0] == 0 and (rows != 0).all() and (table != -1).any(dim=1).all(), (rec, rows, table)
+    # (1) rank 1 claims 3 rows: row 4 does not exist -> its unit is left as filled, the others are exact
+    t3, r3, rec = run(torch.tensor([[2], [3]], dtype=torch.int32, device='cuda'), pairs, flags, 5, K, full)
+    assert rec[0] == FLAG_BAD_SLOT and rec[1] == FAULT_PLAN_UNIT and rec[2] == 4 and rec[3] == 1, rec
+    assert int((r3 == 0).sum()) == 1 and int((t3 == -1).all(dim=1).sum()) == 1
+    assert sorted(r3[r3 != 0].tolist()) == sorted(rows.tolist())
+    # (2) single reduction with pair counts below the valid lanes: the excess units are not written
+    t4, r4, rec = run(ok, torch.tensor([[2], [2]], dtype=torch.int32, device='cuda'),
+                      PLAN_EXPANDED | PLAN_SINGLE | PLAN_INTERLEAVE, 4, 1, full)
+    assert rec[0] == FLAG_BAD_SLOT and rec[1] == FAULT_PLAN_UNIT, rec
+    assert int((r4 != 0).sum()) == int((t4 != -1).sum()) <= 4
+    # (3) a window that holds only 32 rows: token 60's row (and only it) becomes 0
+    t5, r5, rec = run(ok, pairs, flags, 4, K, 32 * row_bytes)
+    assert rec[0] == FLAG_BAD_SLOT and rec[1] == FAULT_PLAN_ROW and rec[3] == 1, rec
+    assert _addr(rec) == (2 << 40) + (rank * T_max + 60) * row_bytes
+    assert int((r5 == 0).sum()) == 1 and set(r5[r5 != 0].tolist()) <= set(rows.tolist())
+    assert torch.equal(t5, table)
+
+
+@pytest.mark.parametrize('peer', [False, True])
+def test_dispatch_pack_never_stores_past_its_destination(kern, peer):
+    """Destination offsets that overrun the destination buffer (dest_rows): those rows are not
+    stored (the bytes past dest_rows stay zero) and the fault is recorded; rows inside are exact."""
+    from deepep_amd.kernels import RowLayout
+    T, R, K, E, H = 40, 2, 4, 8, 256
+    g = torch.Generator().manual_seed(3)
+    idx = torch.stack([torch.randperm(E, generator=g)[:K] for _ in range(T)]).cuda()
+    w = torch.rand((T, K), generator=g).cuda()
+    x = torch.randn((T, H), generator=g).to(torch.bfloat16).cuda()
+    dst = torch.empty((T, R), dtype=torch.int32, device='cuda')
+    cnt = torch.empty((R,), dtype=torch.int32, device='cuda')
+    kern.dispatch_route(idx, E, R, dst, cnt)
+    cl = cnt.tolist()
+    layout = RowLayout.make(2 * H, 0, K)
+    xb = x.view(torch.uint8).view(T, -1)
+
+    lead = 8                                             # canary rows in front of the destination buffer
+
+    def pack(offs, dest_rows, rows_alloc):
+        big = torch.zeros((lead + rows_alloc, layout.row_bytes), dtype=torch.uint8, device='cuda')
+        packed = big[lead:]
+        err = torch.zeros((8,), dtype=torch.int32, device='cuda')
+        o = torch.tensor(offs, dtype=torch.int32, device='cuda')
+        if peer:          # every destination "window" is the same local buffer, dest_rows rows long
+            kern.dispatch_pack(xb, None, idx, w, 0, dst, o, None, layout,
+                               dest_bases=torch.tensor([packed.data_ptr()] * R, dtype=torch.int64, device='cuda'),
+                               dest_rows=dest_rows, error_flag=err)
+        else:
+            kern.dispatch_pack(xb, None, idx, w, 0, dst, o, packed, layout, dest_rows=dest_rows, error_flag=err)
+        torch.cuda.synchronize()
+        big = big.cpu()
+        assert int(big[:lead].count_nonzero()) == 0, 'a row was stored in front of the destination buffer'
+        return big[lead:], err.tolist()
+
+    n = sum(cl)
+    ref, rec = pack([0, cl[0]], n, n)
+    assert rec[0] == 0
+    cut = n - 5
+    got, rec = pack([0, cl[0]], cut, n)
+    assert int(got[cut:].count_nonzero()) == 0, 'rows past dest_rows were stored'
+    assert torch.equal(got[:cut], ref[:cut])
+    assert rec[0] == FLAG_BAD_ADDRESS and rec[1] == FAULT_PACK_ROW and rec[3] == 1, rec
+    # a negative offset is rejected the same way: nothing lands in front of the buffer
+    got, rec = pack([0, -3], n, n)
+    assert rec[0] == FLAG_BAD_ADDRESS and rec[1] == FAULT_PACK_ROW and rec[3] == 1, rec

@@ -214,6 +214,37 @@ def _worker(rank, world, port, seed, T, H, K, queue, empty_rank=-1, chunks=0):
         torch.cuda.synchronize()
         if not np.array_equal(_u16(out), expect[rank][0]):
             failures.append('xgmi combine after the poisoned call')
+        # A corrupted plan entry (a window row address pointing into local memory outside every window):
+        # phase A stores nothing through it, the window's error record names the unit and the address, and
+        # the host raises.  Every rank corrupts one unit, so every rank's check sees it at the same call.
+        key = [k for k in handle._combine_plans if k[0] == 'xgmi' and not k[1] and k[-1] == xb._sym_gen]
+        chunk = next((ch for ch in handle._combine_plans[key[0]].chunks if ch.out_rows.numel()), None) if key else None
+        if chunk is None:
+            failures.append(f'no cached xgmi plan with units to corrupt (keys {list(handle._combine_plans)})')
+        else:
+            canary = torch.zeros((4 << 20,), dtype=torch.uint8, device=dev)
+            saved = chunk.out_rows[0].clone()
+            chunk.out_rows[0] = canary.data_ptr() + (1 << 20)
+            xb.combine(g_in, handle, topk_weights=ex_w, bias=g_bias)
+            torch.cuda.synchronize()
+            chunk.out_rows[0] = saved
+            rec = xb._sym.error_record.tolist()
+            if int(canary.count_nonzero()) != 0:
+                failures.append('a phase-A store escaped through a corrupted window address')
+            addr = (rec[5] & 0xffffffff) << 32 | (rec[4] & 0xffffffff)
+            if not (rec[0] & 4 and rec[1] == 1 and addr == canary.data_ptr() + (1 << 20)):
+                failures.append(f'corrupted window address not recorded: {rec}')
+            try:
+                xb._sym.check()
+                failures.append('check() did not raise after a rejected window address')
+            except RuntimeError as e:
+                if 'outside every window' not in str(e):
+                    failures.append(f'unexpected error text: {e}')
+            xb._sym.reset_error()
+            out, _, _ = xb.combine(g_in, handle, topk_weights=ex_w, bias=g_bias)
+            torch.cuda.synchronize()
+            if not np.array_equal(_u16(out), expect[rank][0]) or xb._sym.error_record.tolist()[0]:
+                failures.append('xgmi combine after the rejected window address')
         # The FIRST combine on a fresh handle captured into a HIP graph, no eager call before it: its
         # plan (window row addresses included) is built by kernels inside the capture.
         _, _, ex_w2, handle2, _ = xb.dispatch(x, topk_idx=torch.from_numpy(idx_all[rank]).to(dev),
@@ -472,10 +503,6 @@ def _full_worker(rank, world, port, queue):
         queue.put((rank, [traceback.format_exc()]))
 
 
-@pytest.mark.skipif(os.environ.get('DEEPEP_XGMI_STRESS') != '1',
-                    reason='opt-in stress test (DEEPEP_XGMI_STRESS=1): 8 processes x 1 GB windows on ONE GPU; one run '
-                           'in about 25 ended in a GPU fault (illegal instruction during phase A window stores), '
-                           'cause not found (DESIGN.md section 5)')
 def test_xgmi_transport_full_size_config3():
     world = 8
     ctx = mp.get_context('spawn')

@@ -24,7 +24,8 @@ def main():
     kern = HipKernels()
     lib = kern.lib
     T, H, K, S = 8192, 7168, 8, 8                  # S receive slots (rank layout at EP = 8)
-    row_bytes = H * 2 + 32
+    from deepep_amd.handle import packed_row_layout
+    row_bytes = packed_row_layout(H, K)[0]         # the window's packed rows: bf16 partial + weight line
     nbytes = S * T * row_bytes
     p = ctypes.c_void_p()
     _lib.check(lib.deepep_sym_alloc(nbytes, ctypes.byref(p)), 'alloc')
@@ -49,7 +50,8 @@ def main():
     for name, buf in (('cached', cc), ('uncached', uc)):
         t = torch.arange(T, device='cuda')
         addr = (buf.data_ptr() + ((t % S) * T + t) * row_bytes).to(torch.int64).contiguous()
-        us = timeit(lambda: kern.combine_reduce_scatter(x, T, addr, stream=s), s, iters=30)
+        win = (torch.tensor([buf.data_ptr()], dtype=torch.int64, device='cuda'), nbytes)
+        us = timeit(lambda: kern.combine_reduce_scatter(x, T, addr, windows=win, stream=s), s, iters=30)
         print(json.dumps(dict(phase='A_scatter_copy', memory=name, us=round(us, 1),
                               gbps=round(2 * T * H * 2 / us / 1e3, 1))), flush=True)
     del uc

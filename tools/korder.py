@@ -54,7 +54,9 @@ def main():
         for name, perm in orders.items():
             tab = table[perm].contiguous()
             rows = (out.data_ptr() + perm.to(torch.int64) * H * 2).contiguous()
-            us = timeit(lambda: kern.combine_reduce_scatter(y, T, rows, table=tab, row_weights=ex_w, stream=s), s)
+            win = (torch.tensor([out.data_ptr()], dtype=torch.int64, device='cuda'), out.numel() * 2)
+            us = timeit(lambda: kern.combine_reduce_scatter(y, T, rows, table=tab, row_weights=ex_w, windows=win,
+                                                            stream=s), s)
             torch.cuda.synchronize()
             print(json.dumps(dict(order=name, round=rnd, us=round(us, 1), tbps=round(nbytes / us / 1e6, 3),
                                   bitwise=bool(torch.equal(out, ref)))), flush=True)

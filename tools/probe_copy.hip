@@ -171,6 +171,156 @@ __global__ void __launch_bounds__(64 * kWaves) scatter_copy_pf(const uint8_t* x,
     }
 }
 
+// Blocked destination-major: the tokens are cut into kTok-token blocks; inside a block, one wave per
+// (expert, 2 KiB chunk) copies the block's rows of that expert -- consecutive destination rows, so
+// every store run is an expert segment of the block -- reading x rows that the block keeps hot in
+// cache (kTok x 14 KiB: 3.5 MB at 256 tokens).  kXcd: each block is owned by one XCD (workgroup w runs on
+// XCD w % 8, so workgroups w = xcd (mod 8) take blocks xcd, xcd + 8, ...) and its x rows stay in
+// that XCD's L2; otherwise blocks are dealt to the grid in order (re-reads from the Infinity Cache).
+// off / cnt: [nblocks][E] first destination row and row count of expert e inside block b; inv[row] =
+// the source token of destination row `row`.
+template <int kAux, bool kXcd, bool kNT>
+__global__ void __launch_bounds__(256) blocked_copy(const uint8_t* x, const int32_t* inv, const int32_t* off,
+                                                    const int32_t* cnt, int nblocks, int E, int xb, uint8_t* out) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int nvec = xb / 16, nch = (nvec + 127) / 128;
+    const int64_t wg_per_block = ((int64_t)E * nch + 3) / 4;
+    int64_t blk, k;
+    if (kXcd) {
+        const int64_t xcd = blockIdx.x % 8, kk = blockIdx.x / 8;
+        blk = xcd + 8 * (kk / wg_per_block);
+        k = kk % wg_per_block;
+    } else {
+        blk = blockIdx.x / wg_per_block;
+        k = blockIdx.x % wg_per_block;
+    }
+    if (blk >= nblocks) return;
+    const int64_t it = k * 4 + wave;
+    const int e = (int)(it / nch), c = (int)(it - (int64_t)e * nch);
+    if (e >= E) return;
+    const int r0 = off[blk * E + e], n = cnt[blk * E + e];
+    const int v0 = c * 128 + lane, v1 = v0 + 64;
+    const u32x4 z = {0u, 0u, 0u, 0u};
+    for (int j = 0; j < n; j += 4) {
+        u32x4 a[4][2];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (j + q < n) {
+                const int64_t t = __builtin_amdgcn_readfirstlane(inv[r0 + j + q]);
+                const u32x4* src = (const u32x4*)(x + t * xb);
+                if constexpr (kNT) {
+                    a[q][0] = v0 < nvec ? __builtin_nontemporal_load(src + v0) : z;
+                    a[q][1] = v1 < nvec ? __builtin_nontemporal_load(src + v1) : z;
+                } else {
+                    a[q][0] = v0 < nvec ? src[v0] : z;
+                    a[q][1] = v1 < nvec ? src[v1] : z;
+                }
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (j + q < n) {
+                auto rs = __builtin_amdgcn_make_buffer_rsrc(out + (int64_t)(r0 + j + q) * xb, 0, xb, 0x00020000);
+                __builtin_amdgcn_raw_buffer_store_b128(a[q][0], rs, v0 * 16, 0, kAux);
+                __builtin_amdgcn_raw_buffer_store_b128(a[q][1], rs, v1 * 16, 0, kAux);
+            }
+        }
+    }
+}
+
+// Row-streaming variant of blocked_copy: one wave per (block, expert) walks the block's rows of the
+// expert, each row whole (kVec 16-byte vectors per lane: all of a 14 KiB row at kVec = 14), so a
+// wave's stores are whole consecutive rows -- one contiguous run per (block, expert).
+template <int kAux, int kVec>
+__global__ void __launch_bounds__(256) blocked_copy_rows(const uint8_t* x, const int32_t* inv, const int32_t* off,
+                                                         const int32_t* cnt, int nblocks, int E, int xb, uint8_t* out) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int nvec = xb / 16;
+    const int64_t wg_per_block = ((int64_t)E + 3) / 4;
+    const int64_t xcd = blockIdx.x % 8, kk = blockIdx.x / 8;
+    const int64_t blk = xcd + 8 * (kk / wg_per_block);
+    const int e = (int)((kk % wg_per_block) * 4 + wave);
+    if (blk >= nblocks || e >= E) return;
+    const int r0 = off[blk * E + e], n = cnt[blk * E + e];
+    const u32x4 z = {0u, 0u, 0u, 0u};
+    for (int j = 0; j < n; ++j) {
+        const int64_t t = __builtin_amdgcn_readfirstlane(inv[r0 + j]);
+        const u32x4* src = (const u32x4*)(x + t * xb);
+        u32x4 a[kVec];
+#pragma unroll
+        for (int q = 0; q < kVec; ++q) a[q] = q * 64 + lane < nvec ? src[q * 64 + lane] : z;
+        auto rs = __builtin_amdgcn_make_buffer_rsrc(out + (int64_t)(r0 + j) * xb, 0, xb, 0x00020000);
+#pragma unroll
+        for (int q = 0; q < kVec; ++q) __builtin_amdgcn_raw_buffer_store_b128(a[q], rs, (q * 64 + lane) * 16, 0, kAux);
+    }
+}
+
+// blocked_copy with kRows rows in flight per wave
+template <int kAux, int kRows>
+__global__ void __launch_bounds__(256) blocked_copy_r(const uint8_t* x, const int32_t* inv, const int32_t* off,
+                                                      const int32_t* cnt, int nblocks, int E, int xb, uint8_t* out) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int nvec = xb / 16, nch = (nvec + 127) / 128;
+    const int64_t wg_per_block = ((int64_t)E * nch + 3) / 4;
+    const int64_t xcd = blockIdx.x % 8, kk = blockIdx.x / 8;
+    const int64_t blk = xcd + 8 * (kk / wg_per_block);
+    const int64_t it = (kk % wg_per_block) * 4 + wave;
+    const int e = (int)(it / nch), c = (int)(it - (int64_t)e * nch);
+    if (blk >= nblocks || e >= E) return;
+    const int r0 = off[blk * E + e], n = cnt[blk * E + e];
+    const int v0 = c * 128 + lane, v1 = v0 + 64;
+    const u32x4 z = {0u, 0u, 0u, 0u};
+    for (int j = 0; j < n; j += kRows) {
+        u32x4 a[kRows][2];
+#pragma unroll
+        for (int q = 0; q < kRows; ++q) {
+            if (j + q < n) {
+                const int64_t t = __builtin_amdgcn_readfirstlane(inv[r0 + j + q]);
+                const u32x4* src = (const u32x4*)(x + t * xb);
+                a[q][0] = v0 < nvec ? src[v0] : z;
+                a[q][1] = v1 < nvec ? src[v1] : z;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < kRows; ++q) {
+            if (j + q < n) {
+                auto rs = __builtin_amdgcn_make_buffer_rsrc(out + (int64_t)(r0 + j + q) * xb, 0, xb, 0x00020000);
+                __builtin_amdgcn_raw_buffer_store_b128(a[q][0], rs, v0 * 16, 0, kAux);
+                __builtin_amdgcn_raw_buffer_store_b128(a[q][1], rs, v1 * 16, 0, kAux);
+            }
+        }
+    }
+}
+
+extern "C" int probe_blocked_copy(int variant, const void* x, const int32_t* inv, const int32_t* off,
+                                  const int32_t* cnt, int nblocks, int E, int xb, void* out, hipStream_t s) {
+    const int nch = (xb / 16 + 127) / 128;
+    const int64_t wg_per_block = ((int64_t)E * nch + 3) / 4;
+    const dim3 g_xcd((unsigned)(8 * wg_per_block * ((nblocks + 7) / 8))), g_lin((unsigned)(wg_per_block * nblocks));
+    const uint8_t* xx = (const uint8_t*)x;
+    uint8_t* o = (uint8_t*)out;
+    switch (variant) {
+        case 0: hipLaunchKernelGGL((blocked_copy<16, true, false>), g_xcd, dim3(256), 0, s, xx, inv, off, cnt, nblocks, E, xb, o); break;
+        case 1: hipLaunchKernelGGL((blocked_copy<16, false, false>), g_lin, dim3(256), 0, s, xx, inv, off, cnt, nblocks, E, xb, o); break;
+        case 2: hipLaunchKernelGGL((blocked_copy<0, true, false>), g_xcd, dim3(256), 0, s, xx, inv, off, cnt, nblocks, E, xb, o); break;
+        case 3: hipLaunchKernelGGL((blocked_copy<2, true, false>), g_xcd, dim3(256), 0, s, xx, inv, off, cnt, nblocks, E, xb, o); break;
+        case 4: hipLaunchKernelGGL((blocked_copy<16, true, true>), g_xcd, dim3(256), 0, s, xx, inv, off, cnt, nblocks, E, xb, o); break;
+        case 5: hipLaunchKernelGGL((blocked_copy<2, false, false>), g_lin, dim3(256), 0, s, xx, inv, off, cnt, nblocks, E, xb, o); break;
+        case 6: hipLaunchKernelGGL((blocked_copy_r<2, 8>), g_xcd, dim3(256), 0, s, xx, inv, off, cnt, nblocks, E, xb, o); break;
+        case 7: hipLaunchKernelGGL((blocked_copy_r<2, 2>), g_xcd, dim3(256), 0, s, xx, inv, off, cnt, nblocks, E, xb, o); break;
+        case 8: hipLaunchKernelGGL((blocked_copy_r<3, 4>), g_xcd, dim3(256), 0, s, xx, inv, off, cnt, nblocks, E, xb, o); break;
+        case 9: hipLaunchKernelGGL((blocked_copy_r<18, 4>), g_xcd, dim3(256), 0, s, xx, inv, off, cnt, nblocks, E, xb, o); break;
+        case 10: {
+            const dim3 g((unsigned)(8 * ((E + 3) / 4) * ((nblocks + 7) / 8)));
+            if (xb == 14336) hipLaunchKernelGGL((blocked_copy_rows<2, 14>), g, dim3(256), 0, s, xx, inv, off, cnt, nblocks, E, xb, o);
+            else return -2;
+            break;
+        }
+        default: return -1;
+    }
+    return (int)hipGetLastError();
+}
+
 template <int kWaves, int kAhead>
 static void launch_pf(const uint8_t* x, const int32_t* dst, int T, int K, int xb, uint8_t* o, hipStream_t s) {
     hipLaunchKernelGGL((scatter_copy_pf<kWaves, kAhead>), dim3((unsigned)((T + kWaves - 1) / kWaves)),

@@ -41,7 +41,29 @@ def main():
     s = torch.cuda.current_stream()
     xb = H * 2
     nbytes = T * xb + N * xb
-    for v in (0, 300, 301, 302, 303, 304, 104, 105, 111, 0, 300, 201):
+    # blocked destination-major (probe_blocked_copy): per kTok-token block and expert, the block's rows
+    lib.probe_blocked_copy.argtypes = [I, P, P, P, P, I, I, I, P, P]
+    valid = idx >= 0
+    count_e = torch.bincount(idx[valid], minlength=E)[:E]
+    start_e = torch.cumsum(count_e, 0) - count_e
+    for tok_blk in (256, 128):
+        nbk = (T + tok_blk - 1) // tok_blk
+        blk_of = (torch.arange(T, device='cuda') // tok_blk).view(T, 1).expand(T, K)
+        cnt = torch.zeros((nbk, E), dtype=torch.int64, device='cuda')
+        cnt.index_put_((blk_of[valid], idx[valid]), torch.ones_like(idx[valid]), accumulate=True)
+        off = (start_e.view(1, E) + torch.cumsum(cnt, 0) - cnt).to(torch.int32).contiguous()
+        cnt32 = cnt.to(torch.int32).contiguous()
+        for v in (3, 5, 6, 7, 8, 9, 10, 0, 3):
+            out.zero_()
+            fn = lambda: lib.probe_blocked_copy(v, x.data_ptr(), inv.data_ptr(), off.data_ptr(), cnt32.data_ptr(),
+                                                nbk, E, xb, out.data_ptr(), s.cuda_stream)
+            assert fn() == 0
+            torch.cuda.synchronize()
+            ok = bool(torch.equal(out, ref))
+            us = timeit(fn, s, iters=20)
+            print(json.dumps(dict(variant=f'blocked tok{tok_blk} v{v}', us=round(us, 1), gbps=round(nbytes / us / 1e3, 1),
+                                  equal=ok)), flush=True)
+    for v in (0, 300, 104, 0, 200, 201):
         out.zero_()
         fn = lambda: lib.probe_copy(v, x.data_ptr(), dst.data_ptr(), inv.data_ptr(), T, K, N, xb, out.data_ptr(),
                                     s.cuda_stream)

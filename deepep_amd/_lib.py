@@ -63,6 +63,7 @@ def describe_error_record(rec) -> str:
 
 # deepep_plan_* (include/deepep_amd.h)
 PLAN_BLOCK_TOKENS = 64
+DISPATCH_BLOCK_ROWS = 128          # DEEPEP_DISPATCH_BLOCK_ROWS: receive-side block of the dispatch
 PLAN_EXPANDED, PLAN_SINGLE, PLAN_INTERLEAVE, PLAN_RANK_LAYOUT, PLAN_WINDOW = 1, 2, 4, 8, 16
 
 _lib = None
@@ -100,9 +101,9 @@ SIGNATURES = {
                                   _P, _P, _I64, _I64, _I, _I, _I, _I, _P, _P]),
     'deepep_dispatch_count': (_I, [_P, _I64, _I, _I, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P]),
     'deepep_dispatch_scan': (_I, [_P, _I, _I, _I, _I, _P, _P, _P]),
-    'deepep_dispatch_slots': (_I, [_P, _I64, _I, _I, _I, _I, _I, _P, _P, _P]),
+    'deepep_dispatch_slots': (_I, [_P, _I64, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     'deepep_dispatch_copy': (_I, [_P, _I64, _I, _I, _I, _I, _I, _I, _P, _I, _P, _I64, _P, _I64, _I,
-                                  _P, _P, _P, _I64, _P, _P]),
+                                  _P, _P, _P, _I64, _P, _P, _P, _I, _P, _P]),
     'deepep_route_block_counts': (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P]),
     'deepep_plan_expert': (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _I, _I, _I, _P, _P, _P, _I64, _I64, _P, _P, _P]),
     'deepep_plan_source': (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I64, _I64, _P, _I, _P, _P]),

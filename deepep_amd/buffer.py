@@ -27,6 +27,7 @@ import torch.distributed as dist
 from .event import EventHandle, EventOverlap
 from .exchange import ExchangeMixin
 from .handle import BlockCounts, CombinePlan, EPHandle, build_ep_plan, chunk_geometry
+from ._lib import DISPATCH_BLOCK_ROWS
 from .kernels import MODE_EPILOGUE, MODE_FUSED, MODE_LOCAL, RowLayout
 from .utils import align, ceil_div, value_or
 
@@ -537,10 +538,12 @@ class ElasticBuffer(ExchangeMixin):
                 recv_packed = torch.empty((N, layout.row_bytes), dtype=torch.uint8, device=dev)
                 self._a2a(recv_packed, packed, recv_counts_l, send_counts_l)
             # --- receive side (dispatch_copy_epilogue_impl): metadata, expert layout, copies
+            inv = block_offsets = None                      # the expanded copy's tables (dispatch_copy)
             if cached is not None:
                 psum_rank = cached.psum_num_recv_tokens_per_scaleup_rank
                 psum_expert = cached.psum_num_recv_tokens_per_expert
                 meta = cached.recv_src_metadata[:N]
+                inv, block_offsets = getattr(cached, '_copy_tables', (None, None))
                 out_idx = None if do_expand else cached._recv_topk_idx.clone()
                 aligned_l = cached.num_recv_tokens_per_expert_list
                 expert_counts = cached.num_unaligned_recv_tokens_per_expert
@@ -551,7 +554,7 @@ class ElasticBuffer(ExchangeMixin):
                 psum_rank = torch.cumsum(recv_counts_t, 0).to(torch.int32)
                 meta = torch.empty((N, K + 2), dtype=torch.int32, device=dev)
                 out_idx = None if do_expand else torch.empty((N, K), dtype=torch.int64, device=dev)
-                nblocks = (N + 255) // 256
+                nblocks = (N + DISPATCH_BLOCK_ROWS - 1) // DISPATCH_BLOCK_ROWS
                 block_counts = torch.empty((nblocks, epr), dtype=torch.int32, device=dev)
                 kern.dispatch_count(recv_packed, layout, N, r, epr, psum_rank, meta, out_idx, block_counts,
                                     stream=stream)
@@ -565,7 +568,12 @@ class ElasticBuffer(ExchangeMixin):
                     cumulative_local_expert_recv_stats += expert_counts.to(cumulative_local_expert_recv_stats.dtype)
                 self._before_epilogue(previous_event_before_epilogue)
                 if do_expand:
-                    kern.dispatch_slots(recv_packed, layout, N, r, epr, block_counts, meta, stream=stream)
+                    # worst-case expanded rows (the count below is known after the notify): the inverse
+                    # map of the slots for the blocked destination-major copy
+                    inv = torch.empty((N * min(K, epr) + (expert_alignment - 1) * epr,), dtype=torch.int32,
+                                      device=dev)
+                    block_offsets = block_counts
+                    kern.dispatch_slots(recv_packed, layout, N, r, epr, block_counts, meta, inv=inv, stream=stream)
                 else:
                     meta[:, 2:] = -1
             num_unaligned = expert_counts
@@ -597,7 +605,9 @@ class ElasticBuffer(ExchangeMixin):
                                out_x.view(torch.uint8), out_sf.view(torch.uint8) if out_sf is not None else None,
                                out_w, x_direct=x_bytes if direct else None,
                                sf_direct=sf_bytes if direct else None, num_max_tokens=num_max_tokens_per_rank,
-                               error_flag=sym.error_flag if use_xgmi else None, stream=stream)
+                               error_flag=sym.error_flag if use_xgmi else None,
+                               inv=inv if do_expand else None, block_offsets=block_offsets if do_expand else None,
+                               expert_end=psum_expert if do_expand else None, stream=stream)
             recv_idx64 = out_idx
             if out_idx is not None and topk_idx.dtype != torch.int64:
                 out_idx = out_idx.to(topk_idx.dtype)
@@ -630,6 +640,7 @@ class ElasticBuffer(ExchangeMixin):
             handle._peer_offsets = peer_offsets
             handle._recv_topk_idx = recv_idx64
             handle._counts = counts
+            handle._copy_tables = (inv, block_offsets)      # reused by cached dispatches
         out_x = (out_x, out_sf) if out_sf is not None else out_x
         return out_x, out_idx, out_w, handle, EventOverlap(event)
 

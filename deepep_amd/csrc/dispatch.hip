@@ -30,6 +30,11 @@ namespace {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+// Receive-side blocks: DEEPEP_DISPATCH_BLOCK_ROWS consecutive received rows (count / slots / the expanded
+// copy).  128 rows x 14 KiB = 1.8 MB of source rows per block: what one XCD's L2 keeps for the
+// expanded copy's re-reads (below).
+constexpr int kBlockRows = DEEPEP_DISPATCH_BLOCK_ROWS;
+
 // ---------------------------------------------------------------- route: token -> destination slots
 // dst_slot[t][r] = #{t' < t : t' routed to r} or -1; send_counts[r] = #{t : t routed to r}
 // (dispatch.cuh:79-258 notify + slot assignment).  Two passes over 256-token blocks, one thread
@@ -212,19 +217,19 @@ __device__ __forceinline__ int local_expert(int64_t e, int rank, int epr) {
                ? static_cast<int>(e - static_cast<int64_t>(rank) * epr) : -1;
 }
 
-// One thread per received row, 256 rows per workgroup: metadata columns 0-1, the local top-k
+// One thread per received row, kBlockRows rows per workgroup: metadata columns 0-1, the local top-k
 // indices (non-expanded recv_topk_idx) and per-workgroup expert histograms.  N is the host's row
 // count; the rows actually received are rank_psum[R - 1] (the same number after a host-synced notify;
 // fewer when the host sized the launch for the worst case, dispatch(do_cpu_sync=False)).  Rows past
 // the received ones get metadata -1 (and recv_topk_idx -1): the later kernels skip them.
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(kBlockRows)
 count_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int idx_off, int src_off, int N, int K,
              int rank, int epr, const int32_t* __restrict__ rank_psum, int R,
              int32_t* __restrict__ meta, int64_t* __restrict__ recv_topk_idx, int32_t* __restrict__ block_counts) {
     extern __shared__ int32_t s_hist[];                 // [epr]
-    for (int e = threadIdx.x; e < epr; e += 256) s_hist[e] = 0;
+    for (int e = threadIdx.x; e < epr; e += kBlockRows) s_hist[e] = 0;
     __syncthreads();
-    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int i = blockIdx.x * kBlockRows + threadIdx.x;
     const int received = min(N, rank_psum[R - 1]);
     if (i >= received && i < N) {
         const int64_t mrow = static_cast<int64_t>(i) * (K + 2);
@@ -252,7 +257,7 @@ count_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int idx_off,
         meta[mrow + 1] = src_rank * K + master;
     }
     __syncthreads();
-    for (int e = threadIdx.x; e < epr; e += 256)
+    for (int e = threadIdx.x; e < epr; e += kBlockRows)
         block_counts[static_cast<int64_t>(blockIdx.x) * epr + e] = s_hist[e];
 }
 
@@ -307,21 +312,24 @@ scan_kernel(int32_t* __restrict__ block_counts, int nblocks, int epr, int align,
 // Expanded slot of every (row, local lane): the expert group's offset for this workgroup plus the
 // number of earlier rows of the workgroup holding the same expert (per-wave 64-bit ballot masks in
 // LDS).  A token never holds one expert twice, so this is the ascending-token order.  Rows whose
-// metadata count_kernel marked -1 (past the received rows) get no slots.
-__global__ void __launch_bounds__(256)
+// metadata count_kernel marked -1 (past the received rows) get no slots.  inv (optional): the inverse
+// map, inv[slot] = row * K + lane, read by the expanded copy.
+constexpr int kSlotWaves = kBlockRows / 64;
+
+__global__ void __launch_bounds__(kBlockRows)
 slots_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int idx_off, int N, int K, int rank, int epr,
-             const int32_t* __restrict__ block_offsets, int32_t* __restrict__ meta) {
-    extern __shared__ uint64_t s_bits[];                // [epr][4]
-    for (int j = threadIdx.x; j < epr * 4; j += 256) s_bits[j] = 0ull;
+             const int32_t* __restrict__ block_offsets, int32_t* __restrict__ meta, int32_t* __restrict__ inv) {
+    extern __shared__ uint64_t s_bits[];                // [epr][kSlotWaves]
+    for (int j = threadIdx.x; j < epr * kSlotWaves; j += kBlockRows) s_bits[j] = 0ull;
     __syncthreads();
-    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int i = blockIdx.x * kBlockRows + threadIdx.x;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t* idx = reinterpret_cast<const int64_t*>(packed + static_cast<int64_t>(i) * row_bytes + idx_off);
     const bool valid = i < N && meta[static_cast<int64_t>(i) * (K + 2)] >= 0;
     if (valid)
         for (int k = 0; k < K; ++k) {
             const int le = local_expert(idx[k], rank, epr);
-            if (le >= 0) atomicOr(reinterpret_cast<unsigned long long*>(&s_bits[le * 4 + wave]), 1ull << lane);
+            if (le >= 0) atomicOr(reinterpret_cast<unsigned long long*>(&s_bits[le * kSlotWaves + wave]), 1ull << lane);
         }
     __syncthreads();
     if (i >= N) return;
@@ -331,8 +339,9 @@ slots_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int idx_off,
         int slot = -1;
         if (le >= 0) {
             slot = block_offsets[static_cast<int64_t>(blockIdx.x) * epr + le];
-            for (int w = 0; w < wave; ++w) slot += __popcll(s_bits[le * 4 + w]);
-            slot += __popcll(s_bits[le * 4 + wave] & lt);
+            for (int w = 0; w < wave; ++w) slot += __popcll(s_bits[le * kSlotWaves + w]);
+            slot += __popcll(s_bits[le * kSlotWaves + wave] & lt);
+            if (inv != nullptr) inv[slot] = i * K + k;
         }
         meta[static_cast<int64_t>(i) * (K + 2) + 2 + k] = slot;
     }
@@ -410,6 +419,103 @@ copy_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int x_bytes, 
             if (my_dst >= 0) recv_w[my_dst] = w;
         } else {
             recv_w[i * K + lane] = w;
+        }
+    }
+}
+
+// Expanded copy, destination-major inside blocks of received rows.  The rows of
+// block b (kBlockRows received rows) that go to local expert e are the consecutive expanded rows
+// [block_offsets[b][e], block_offsets[b + 1][e]) (the slots kernel numbers them in row order), so one
+// wave per (block, expert, 2 KiB column chunk) writes a run of whole consecutive destination rows
+// and reads their sources through inv.  The block's source rows (1.8 MB) are read once from HBM and
+// re-read -- once per local expert of each row -- from the L2 of the one XCD that owns the block
+// (workgroups w = x (mod 8) run on XCD x and take blocks x, x + 8, ...).  Stores are streaming
+// write-through (sc1 nt).  Measured at BASELINE config 2 (tools/probe_copy.py, two boxes): 151.4 vs
+// 163.5 us and 182.0 vs 213.6 us for the source-major copy (one load, up to K scattered stores).
+constexpr int kCopyAux = 18;                          // sc1 | nt
+
+template <bool kDirect>
+__global__ void __launch_bounds__(256)
+copy_expanded_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int x_bytes, int sf_off, int sf_bytes,
+                     int w_off, int N, int K, const int32_t* __restrict__ meta,
+                     const uint8_t* __restrict__ x_direct, int64_t x_direct_stride,
+                     const uint8_t* __restrict__ sf_direct, int64_t sf_direct_stride, int num_max_tokens,
+                     const int32_t* __restrict__ inv, const int32_t* __restrict__ block_offsets,
+                     const int32_t* __restrict__ expert_end, int nb, int epr,
+                     uint8_t* __restrict__ recv_x, uint8_t* __restrict__ recv_sf, float* __restrict__ recv_w,
+                     int64_t num_out_rows, int32_t* __restrict__ error_flag) {
+    constexpr int kChunkVecs = 128;                        // 64 lanes x 2 x 16 B
+    constexpr int kRows = 4;                               // destination rows in flight per wave
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (error_flag != nullptr && (__hip_atomic_load(error_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 2))
+        return;                                            // a timed-out window barrier: store nothing
+    const int nvec = x_bytes / 16;
+    const int nch = max(1, (nvec + kChunkVecs - 1) / kChunkVecs);
+    const int64_t wg_per_block = (static_cast<int64_t>(epr) * nch + 3) / 4;
+    const int64_t xcd = blockIdx.x % 8, kk = blockIdx.x / 8;
+    const int64_t b = xcd + 8 * (kk / wg_per_block);
+    const int64_t it = (kk % wg_per_block) * 4 + wave;
+    const int e = static_cast<int>(it / nch), c = static_cast<int>(it - static_cast<int64_t>(e) * nch);
+    if (b >= nb || e >= epr) return;
+    const int r0 = block_offsets[b * epr + e];
+    const int r1 = b + 1 < nb ? block_offsets[(b + 1) * epr + e] : expert_end[e];
+    const int v0 = c * kChunkVecs + lane, v1 = v0 + 64;
+    const u32x4 zero = {0u, 0u, 0u, 0u};
+    for (int j = r0; j < r1; j += kRows) {
+        const uint8_t* rows[kRows];
+        int32_t src_i[kRows], src_k[kRows];
+        u32x4 a[kRows][2];
+#pragma unroll
+        for (int q = 0; q < kRows; ++q) {
+            src_i[q] = -1;
+            src_k[q] = 0;
+            rows[q] = nullptr;
+            if (j + q < r1) {
+                const int32_t code = __builtin_amdgcn_readfirstlane(inv[j + q]);
+                const int32_t i = code >= 0 ? code / K : -1;
+                if (i >= 0 && i < N) {
+                    src_i[q] = i;
+                    src_k[q] = code - i * K;
+                    if constexpr (kDirect) {
+                        const int64_t t = meta[static_cast<int64_t>(i) * (K + 2)] % num_max_tokens;
+                        rows[q] = x_direct + t * x_direct_stride;
+                    } else {
+                        rows[q] = packed + static_cast<int64_t>(i) * row_bytes;
+                    }
+                    const u32x4* xs = reinterpret_cast<const u32x4*>(rows[q]);
+                    a[q][0] = v0 < nvec ? xs[v0] : zero;
+                    a[q][1] = v1 < nvec ? xs[v1] : zero;
+                }
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < kRows; ++q) {
+            if (src_i[q] < 0) continue;
+            const int64_t d = j + q;
+            if (d >= num_out_rows) {                       // never store past the outputs
+                if (lane == 0 && error_flag != nullptr) atomicOr(error_flag, 1);
+                continue;
+            }
+            // the descriptor's range check drops the lanes past the row end
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(recv_x + d * x_bytes, 0, x_bytes,
+                                                                                0x00020000);
+            __builtin_amdgcn_raw_buffer_store_b128(a[q][0], rs, v0 * 16, 0, kCopyAux);
+            __builtin_amdgcn_raw_buffer_store_b128(a[q][1], rs, v1 * 16, 0, kCopyAux);
+            if (c != 0) continue;
+            if (recv_sf != nullptr) {
+                const uint8_t* sfs;
+                if constexpr (kDirect) {
+                    const int64_t t = meta[static_cast<int64_t>(src_i[q]) * (K + 2)] % num_max_tokens;
+                    sfs = sf_direct != nullptr ? sf_direct + t * sf_direct_stride : nullptr;
+                } else {
+                    sfs = rows[q] + sf_off;
+                }
+                if (sfs != nullptr)
+                    for (int v = lane; v < sf_bytes / 4; v += 64)
+                        reinterpret_cast<uint32_t*>(recv_sf + d * sf_bytes)[v] = reinterpret_cast<const uint32_t*>(sfs)[v];
+            }
+            if (recv_w != nullptr && lane == 0)
+                recv_w[d] = reinterpret_cast<const float*>(packed + static_cast<int64_t>(src_i[q]) * row_bytes + w_off)[src_k[q]];
         }
     }
 }
@@ -506,8 +612,8 @@ int deepep_dispatch_count(const void* packed, int64_t row_bytes, int idx_off, in
         num_ranks < 1 || src_metadata == nullptr || block_counts == nullptr || packed == nullptr ||
         recv_rank_psum == nullptr)
         return deepep_amd_set_error(DEEPEP_ERR_INVALID_ARG, "dispatch_count: invalid arguments");
-    const int nblocks = (num_recv + 255) / 256;
-    hipLaunchKernelGGL(count_kernel, dim3(nblocks), dim3(256), num_local_experts * 4,
+    const int nblocks = (num_recv + kBlockRows - 1) / kBlockRows;
+    hipLaunchKernelGGL(count_kernel, dim3(nblocks), dim3(kBlockRows), num_local_experts * 4,
                        reinterpret_cast<hipStream_t>(stream), static_cast<const uint8_t*>(packed), row_bytes,
                        idx_off, src_off, num_recv, num_topk, rank, num_local_experts, recv_rank_psum, num_ranks,
                        src_metadata, recv_topk_idx, block_counts);
@@ -527,15 +633,16 @@ int deepep_dispatch_scan(int32_t* block_counts, int num_blocks, int num_local_ex
 
 int deepep_dispatch_slots(const void* packed, int64_t row_bytes, int idx_off, int num_recv, int num_topk,
                           int rank, int num_local_experts, const int32_t* block_offsets, int32_t* src_metadata,
-                          deepep_stream_t stream) {
+                          int32_t* inv, deepep_stream_t stream) {
     if (num_recv == 0) return DEEPEP_OK;
     if (num_recv < 0 || num_topk < 1 || num_topk > 32 || num_local_experts < 1 || num_local_experts > 1024 ||
-        packed == nullptr || block_offsets == nullptr || src_metadata == nullptr)
+        packed == nullptr || block_offsets == nullptr || src_metadata == nullptr ||
+        static_cast<int64_t>(num_recv) * num_topk >= (int64_t(1) << 31))
         return deepep_amd_set_error(DEEPEP_ERR_INVALID_ARG, "dispatch_slots: invalid arguments");
-    const int nblocks = (num_recv + 255) / 256;
-    hipLaunchKernelGGL(slots_kernel, dim3(nblocks), dim3(256), num_local_experts * 4 * 8,
+    const int nblocks = (num_recv + kBlockRows - 1) / kBlockRows;
+    hipLaunchKernelGGL(slots_kernel, dim3(nblocks), dim3(kBlockRows), num_local_experts * kSlotWaves * 8,
                        reinterpret_cast<hipStream_t>(stream), static_cast<const uint8_t*>(packed), row_bytes,
-                       idx_off, num_recv, num_topk, rank, num_local_experts, block_offsets, src_metadata);
+                       idx_off, num_recv, num_topk, rank, num_local_experts, block_offsets, src_metadata, inv);
     return launch_status("dispatch_slots");
 }
 
@@ -544,14 +651,37 @@ int deepep_dispatch_copy(const void* packed, int64_t row_bytes, int x_bytes, int
                          const void* x_direct, int64_t x_direct_stride_bytes,
                          const void* sf_direct, int64_t sf_direct_stride_bytes, int num_max_tokens,
                          void* recv_x, void* recv_sf, float* recv_topk_weights, int64_t num_out_rows,
-                         int32_t* error_flag, deepep_stream_t stream) {
+                         const int32_t* inv, const int32_t* block_offsets, const int32_t* expert_end,
+                         int num_local_experts, int32_t* error_flag, deepep_stream_t stream) {
     if (num_recv == 0) return DEEPEP_OK;
     if (num_recv < 0 || num_topk < 1 || num_topk > 32 || x_bytes % 16 || row_bytes % 16 || !a16(packed) ||
         num_out_rows < 0 ||
         !a16(recv_x) || (recv_sf != nullptr && sf_bytes % 4) || src_metadata == nullptr ||
         (x_direct != nullptr && (!a16(x_direct) || x_direct_stride_bytes % 16 || num_max_tokens < 1 ||
-                                 (recv_sf != nullptr && sf_direct == nullptr))))
+                                 (recv_sf != nullptr && sf_direct == nullptr))) ||
+        (inv != nullptr && (!expanded || block_offsets == nullptr || expert_end == nullptr || num_local_experts < 1 ||
+                            num_local_experts > 1024)))
         return deepep_amd_set_error(DEEPEP_ERR_INVALID_ARG, "dispatch_copy: invalid arguments or alignment");
+    if (inv != nullptr) {
+        // the blocked destination-major copy (expanded layout)
+        const int nb = (num_recv + kBlockRows - 1) / kBlockRows;
+        const int nch = std::max(1, (x_bytes / 16 + 127) / 128);
+        const int64_t wg_per_block = (static_cast<int64_t>(num_local_experts) * nch + 3) / 4;
+        const int64_t grid = 8 * wg_per_block * ((nb + 7) / 8);
+        auto launch = [&](auto kernel) {
+            hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>(grid)), dim3(256), 0,
+                               reinterpret_cast<hipStream_t>(stream),
+                               static_cast<const uint8_t*>(packed), row_bytes, x_bytes, sf_off, sf_bytes, w_off,
+                               num_recv, num_topk, src_metadata, static_cast<const uint8_t*>(x_direct),
+                               x_direct_stride_bytes, static_cast<const uint8_t*>(sf_direct), sf_direct_stride_bytes,
+                               num_max_tokens, inv, block_offsets, expert_end, nb, num_local_experts,
+                               static_cast<uint8_t*>(recv_x), static_cast<uint8_t*>(recv_sf), recv_topk_weights,
+                               num_out_rows, error_flag);
+        };
+        if (x_direct != nullptr) launch(copy_expanded_kernel<true>);
+        else launch(copy_expanded_kernel<false>);
+        return launch_status("dispatch_copy");
+    }
     const int64_t nchunks = std::max<int64_t>(1, (x_bytes / 16 + 127) / 128);
     const int64_t items = static_cast<int64_t>(num_recv) * nchunks;
     hipLaunchKernelGGL(copy_kernel, dim3(static_cast<unsigned>((items + 3) / 4)), dim3(256), 0,

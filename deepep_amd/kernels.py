@@ -261,16 +261,26 @@ class HipKernels:
         _lib.check(rc, 'dispatch_scan')
 
     def dispatch_slots(self, packed, layout: RowLayout, num_recv, rank, num_local_experts, block_offsets, meta,
-                       stream=None):
+                       inv=None, stream=None):
+        """inv: optional int32 [expanded rows]: inv[slot] = row * K + lane (the expanded copy's map)."""
+        _require(inv is None or (inv.dtype == torch.int32 and inv.is_contiguous()), 'inv int32')
         rc = self.lib.deepep_dispatch_slots(ptr(packed), layout.row_bytes, layout.idx_off, num_recv,
                                             layout.num_topk, rank, num_local_experts, ptr(block_offsets),
-                                            ptr(meta), _stream_handle(stream))
+                                            ptr(meta), ptr(inv), _stream_handle(stream))
         _lib.check(rc, 'dispatch_slots')
 
     def dispatch_copy(self, packed, layout: RowLayout, num_recv, meta, expanded, recv_x_bytes, recv_sf_bytes,
-                      recv_w, x_direct=None, sf_direct=None, num_max_tokens: int = 0, error_flag=None, stream=None):
+                      recv_w, x_direct=None, sf_direct=None, num_max_tokens: int = 0, error_flag=None,
+                      inv=None, block_offsets=None, expert_end=None, stream=None):
         """x_direct / sf_direct: [T, bytes] uint8 views of the sender's rows (one rank: the packed rows
-        then carry only metadata and row i's x is x_direct[src_metadata[i][0] % num_max_tokens])."""
+        then carry only metadata and row i's x is x_direct[src_metadata[i][0] % num_max_tokens]).
+        inv / block_offsets / expert_end (expanded): the blocked destination-major copy (dispatch_slots'
+        inverse map, dispatch_scan's per-block offsets [blocks, local experts] and psum_expert)."""
+        if inv is not None:
+            _require(expanded and block_offsets is not None and expert_end is not None and
+                     block_offsets.dim() == 2 and block_offsets.shape[0] ==
+                     (num_recv + _lib.DISPATCH_BLOCK_ROWS - 1) // _lib.DISPATCH_BLOCK_ROWS and
+                     expert_end.numel() == block_offsets.shape[1], 'blocked copy tables')
         x_bytes = x_direct.shape[1] if x_direct is not None else layout.x_bytes
         sf_bytes = sf_direct.shape[1] if sf_direct is not None else layout.sf_bytes
         rc = self.lib.deepep_dispatch_copy(ptr(packed), layout.row_bytes, x_bytes, layout.sf_off,
@@ -280,7 +290,9 @@ class HipKernels:
                                            ptr(sf_direct), sf_direct.stride(0) if sf_direct is not None else 0,
                                            num_max_tokens,
                                            ptr(recv_x_bytes), ptr(recv_sf_bytes), ptr(recv_w),
-                                           recv_x_bytes.shape[0], ptr(error_flag), _stream_handle(stream))
+                                           recv_x_bytes.shape[0], ptr(inv), ptr(block_offsets), ptr(expert_end),
+                                           block_offsets.shape[1] if block_offsets is not None else 0,
+                                           ptr(error_flag), _stream_handle(stream))
         _lib.check(rc, 'dispatch_copy')
 
     def combine_buffer_size(self, num_max_tokens_per_rank: int, hidden: int, num_topk: int,

@@ -215,9 +215,12 @@ int deepep_dispatch_pack(const void* x, int64_t x_row_stride_bytes, int x_bytes,
                          int sf_off, int idx_off, int w_off, int src_off, int32_t* error_flag,
                          deepep_stream_t stream);
 
+/* Receive-side block: DEEPEP_DISPATCH_BLOCK_ROWS consecutive received rows. */
+#define DEEPEP_DISPATCH_BLOCK_ROWS 128
+
 /* Receive side, pass 1: src_metadata columns 0-1 ({src_global_idx, src_rank * K + master lane}),
- * recv_topk_idx (local expert or -1, int64 [num_recv][K], may be NULL) and per-256-row expert
- * histograms block_counts [ceil(num_recv / 256)][num_local_experts]. recv_rank_psum is the
+ * recv_topk_idx (local expert or -1, int64 [num_recv][K], may be NULL) and per-block expert
+ * histograms block_counts [ceil(num_recv / DEEPEP_DISPATCH_BLOCK_ROWS)][num_local_experts]. recv_rank_psum is the
  * inclusive prefix sum of rows per source rank (device memory).  Rows from recv_rank_psum[num_ranks-1]
  * up to num_recv (a launch sized for the worst case, dispatch(do_cpu_sync=False)) get src_metadata
  * columns 0-1 = -1 and recv_topk_idx -1; passes 3 and 4 skip them. */
@@ -226,17 +229,18 @@ int deepep_dispatch_count(const void* packed, int64_t row_bytes, int idx_off, in
                           int32_t* src_metadata, int64_t* recv_topk_idx, int32_t* block_counts,
                           deepep_stream_t stream);
 
-/* Pass 2: block_counts becomes each 256-row block's first slot inside its expert group (expert
+/* Pass 2: block_counts becomes each block's first slot inside its expert group (expert
  * groups start at aligned offsets); expert_counts = rows per expert; psum_expert as the reference
  * handle's psum_num_recv_tokens_per_expert (expanded: aligned start + count; else inclusive aligned). */
 int deepep_dispatch_scan(int32_t* block_counts, int num_blocks, int num_local_experts, int expert_alignment,
                          int expanded, int32_t* expert_counts, int32_t* psum_expert, deepep_stream_t stream);
 
 /* Pass 3 (expanded only): src_metadata columns 2.. = expanded row of every local slot, -1 elsewhere
- * (all -1 for a row whose column 0 is -1). */
+ * (all -1 for a row whose column 0 is -1).  inv (int32 [expanded rows], or NULL): the inverse map,
+ * inv[slot] = row * num_topk + lane for every slot written (alignment padding rows are not written). */
 int deepep_dispatch_slots(const void* packed, int64_t row_bytes, int idx_off, int num_recv, int num_topk,
                           int rank, int num_local_experts, const int32_t* block_offsets, int32_t* src_metadata,
-                          deepep_stream_t stream);
+                          int32_t* inv, deepep_stream_t stream);
 
 /* Pass 4: recv_x / recv_sf rows (row i, or every local slot when expanded) and top-k weights
  * ([num_recv][K] or, expanded, [slot]).  recv_sf / recv_topk_weights may be NULL.  With x_direct
@@ -244,13 +248,19 @@ int deepep_dispatch_slots(const void* packed, int64_t row_bytes, int idx_off, in
  * are read from x_direct / sf_direct at row src_metadata[i][0] % num_max_tokens.  Destination rows
  * >= num_out_rows (the rows recv_x holds) are skipped and set bit 1 of error_flag (device int or
  * NULL); once bit 2 is set (a timed-out window barrier) nothing is stored.  Rows whose
- * src_metadata[i][0] is -1 (past the received rows, pass 1) are skipped. */
+ * src_metadata[i][0] is -1 (past the received rows, pass 1) are skipped.
+ * inv (expanded only, or NULL): pass 3's inverse map; then the copy runs destination-major inside
+ * blocks of received rows -- expert e's rows of block b are [block_offsets[b][e], block_offsets[b+1][e])
+ * (pass 2's offsets; the last block ends at expert_end[e], pass 2's psum_expert) -- each block owned
+ * by one XCD, whose L2 serves its rows' re-reads.  Same bytes as with inv NULL
+ * (source-major: one load of each received row, a store per local slot). */
 int deepep_dispatch_copy(const void* packed, int64_t row_bytes, int x_bytes, int sf_off, int sf_bytes, int w_off,
                          int num_recv, int num_topk, const int32_t* src_metadata, int expanded,
                          const void* x_direct, int64_t x_direct_stride_bytes,
                          const void* sf_direct, int64_t sf_direct_stride_bytes, int num_max_tokens,
                          void* recv_x, void* recv_sf, float* recv_topk_weights, int64_t num_out_rows,
-                         int32_t* error_flag, deepep_stream_t stream);
+                         const int32_t* inv, const int32_t* block_offsets, const int32_t* expert_end,
+                         int num_local_experts, int32_t* error_flag, deepep_stream_t stream);
 
 /* ------------------------------------------------------------------ EP > 1 combine plan
  * The EP > 1 combine runs in pipeline chunks of source tokens: chunk c = tokens

@@ -10,6 +10,7 @@ from typing import Optional
 import torch
 
 import oracle
+from deepep_amd._lib import DISPATCH_BLOCK_ROWS
 from tests import plan_ref
 
 
@@ -128,8 +129,9 @@ class OracleKernels:
         if recv_topk_idx is not None:
             recv_topk_idx[:N].copy_(le)
         block_counts.zero_()
+        rows = DISPATCH_BLOCK_ROWS
         for b in range(block_counts.shape[0]):
-            chunk = le[b * 256:(b + 1) * 256]
+            chunk = le[b * rows:(b + 1) * rows]
             chunk = chunk[chunk >= 0]
             block_counts[b] += torch.bincount(chunk, minlength=epr).to(torch.int32)
 
@@ -143,22 +145,27 @@ class OracleKernels:
         expert_counts.copy_(counts.to(torch.int32))
         psum_expert.copy_((start + counts if expanded else start + aligned).to(torch.int32))
 
-    def dispatch_slots(self, packed, layout, num_recv, rank, num_local_experts, block_offsets, meta, stream=None):
+    def dispatch_slots(self, packed, layout, num_recv, rank, num_local_experts, block_offsets, meta, inv=None,
+                       stream=None):
         le = self._local(packed, layout, num_recv, rank, num_local_experts)
         meta[:num_recv, 2:] = -1
+        rows = DISPATCH_BLOCK_ROWS
         for b in range(block_offsets.shape[0]):
             run = block_offsets[b].clone()
-            for i in range(b * 256, min(num_recv, (b + 1) * 256)):
+            for i in range(b * rows, min(num_recv, (b + 1) * rows)):
                 if int(meta[i, 0]) < 0:                  # past the received rows
                     continue
                 for k in range(layout.num_topk):
                     e = int(le[i, k])
                     if e >= 0:
                         meta[i, 2 + k] = run[e]
+                        if inv is not None:
+                            inv[run[e]] = i * layout.num_topk + k
                         run[e] += 1
 
     def dispatch_copy(self, packed, layout, num_recv, meta, expanded, recv_x_bytes, recv_sf_bytes, recv_w,
-                      x_direct=None, sf_direct=None, num_max_tokens=0, error_flag=None, stream=None):
+                      x_direct=None, sf_direct=None, num_max_tokens=0, error_flag=None, inv=None,
+                      block_offsets=None, expert_end=None, stream=None):
         K = layout.num_topk
         N = int((meta[:num_recv, 0] >= 0).sum())         # the received rows come first
         if x_direct is not None:

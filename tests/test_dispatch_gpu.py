@@ -33,9 +33,11 @@ def _routing(T, E, K, R, masked, skew, gen):
     return idx, w
 
 
-def _run_dispatch(kern, dev, ranks, E, K, H, T_max, expanded, alignment, fp8, direct=False):
+def _run_dispatch(kern, dev, ranks, E, K, H, T_max, expanded, alignment, fp8, direct=False, blocked=True):
     """Both halves of the dispatch for every rank with `kern`; returns per-rank outputs on the CPU.
-    direct (one rank): metadata-only packed rows, the copy reads x / sf from the sender's tensors."""
+    direct (one rank): metadata-only packed rows, the copy reads x / sf from the sender's tensors.
+    blocked (expanded): the destination-major blocked copy (slots' inverse map), else source-major."""
+    from deepep_amd._lib import DISPATCH_BLOCK_ROWS
     from deepep_amd.kernels import RowLayout
     R = len(ranks)
     epr = E // R
@@ -69,16 +71,18 @@ def _run_dispatch(kern, dev, ranks, E, K, H, T_max, expanded, alignment, fp8, di
         psum = torch.tensor(np.cumsum(counts), dtype=torch.int32, device=dev)
         meta = torch.full((N, K + 2), -7, dtype=torch.int32, device=dev)
         ridx = None if expanded else torch.empty((N, K), dtype=torch.int64, device=dev)
-        nb = (N + 255) // 256
+        nb = (N + DISPATCH_BLOCK_ROWS - 1) // DISPATCH_BLOCK_ROWS
         bc = torch.empty((nb, epr), dtype=torch.int32, device=dev)
         kern.dispatch_count(recv, layout, N, r, epr, psum, meta, ridx, bc)
         ec = torch.empty((epr,), dtype=torch.int32, device=dev)
         pe = torch.empty((epr,), dtype=torch.int32, device=dev)
         kern.dispatch_scan(bc, epr, alignment, expanded, ec, pe)
         aligned = [(int(c) + alignment - 1) // alignment * alignment for c in ec.tolist()]
+        inv = None
         if expanded:
             rows = sum(aligned)
-            kern.dispatch_slots(recv, layout, N, r, epr, bc, meta)
+            inv = torch.full((max(rows, 1),), -9, dtype=torch.int32, device=dev) if blocked else None
+            kern.dispatch_slots(recv, layout, N, r, epr, bc, meta, inv=inv)
         else:
             meta[:, 2:] = -1
             rows = N
@@ -89,7 +93,8 @@ def _run_dispatch(kern, dev, ranks, E, K, H, T_max, expanded, alignment, fp8, di
         kern.dispatch_copy(recv, layout, N, meta, expanded, rx.view(torch.uint8),
                            rsf.view(torch.uint8) if rsf is not None else None, rw,
                            x_direct=sends[r][4] if direct else None, sf_direct=sends[r][5] if direct else None,
-                           num_max_tokens=T_max)
+                           num_max_tokens=T_max, inv=inv, block_offsets=bc if inv is not None else None,
+                           expert_end=pe if inv is not None else None)
         outs.append(dict(meta=meta.cpu(), ridx=None if ridx is None else ridx.cpu(), ec=ec.cpu(), pe=pe.cpu(),
                          rx=rx.cpu(), rsf=None if rsf is None else rsf.cpu(), rw=rw.cpu(), dst=sends[r][0],
                          cnt=sends[r][1],
@@ -118,6 +123,13 @@ def test_dispatch_primitives_match_cpu(hip, R, K, E, T, H, expanded, alignment, 
         ranks.append((x, sf, idx, w))
     got = _run_dispatch(hip, 'cuda', ranks, E, K, H, T, expanded, alignment, fp8)
     exp = _run_dispatch(OracleKernels(), 'cpu', ranks, E, K, H, T, expanded, alignment, fp8)
+    # the source-major copy (no inverse map) gives the same rows as the blocked destination-major one
+    src_major = _run_dispatch(hip, 'cuda', ranks, E, K, H, T, expanded, alignment, fp8, blocked=False)
+    for r in range(R):
+        assert torch.equal(got[r]['rx'].view(torch.uint8), src_major[r]['rx'].view(torch.uint8)), f'rank {r} copies'
+        assert torch.equal(got[r]['rw'], src_major[r]['rw'])
+        if fp8:
+            assert torch.equal(got[r]['rsf'], src_major[r]['rsf'])
     for r in range(R):
         g, e = got[r], exp[r]
         assert torch.equal(g['dst'], e['dst']) and g['cnt'] == e['cnt'], f'rank {r} route'

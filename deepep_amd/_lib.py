@@ -99,20 +99,22 @@ SIGNATURES = {
     'deepep_dispatch_expert_counts': (_I, [_P, _I, _I, _I, _P, _P]),
     'deepep_dispatch_pack': (_I, [_P, _I64, _I, _P, _I64, _I, _P, _P, _I, _I, _I, _P, _P, _I,
                                   _P, _P, _I64, _I64, _I, _I, _I, _I, _P, _P]),
-    'deepep_dispatch_count': (_I, [_P, _I64, _I, _I, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P]),
+    'deepep_dispatch_count': (_I, [_P, _I64, _I, _I, _I, _I, _I, _I, _P, _I, _I, _P, _P, _P, _P, _P]),
     'deepep_dispatch_scan': (_I, [_P, _I, _I, _I, _I, _P, _P, _P]),
-    'deepep_dispatch_slots': (_I, [_P, _I64, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
+    'deepep_dispatch_slots': (_I, [_P, _I64, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P]),
     'deepep_dispatch_copy': (_I, [_P, _I64, _I, _I, _I, _I, _I, _I, _P, _I, _P, _I64, _P, _I64, _I,
-                                  _P, _P, _P, _I64, _P, _P, _P, _I, _P, _P]),
+                                  _P, _P, _P, _I64, _P, _P, _P, _I, _P, _P, _P]),
     'deepep_route_block_counts': (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P]),
-    'deepep_plan_expert': (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _I, _I, _I, _P, _P, _P, _I64, _I64, _P, _P, _P]),
-    'deepep_plan_source': (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I64, _I64, _P, _I, _P, _P]),
+    'deepep_plan_expert': (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _I, _I, _I, _P, _P, _P, _I64, _I64, _P, _P, _I,
+                                _P]),
+    'deepep_plan_source': (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I64, _I64, _P, _I, _P, _I, _P]),
     'deepep_sym_alloc': (_I, [_I64, ctypes.POINTER(ctypes.c_void_p)]),
     'deepep_sym_free': (_I, [_P]),
     'deepep_sym_export': (_I, [_P, _P]),
     'deepep_sym_import': (_I, [_P, ctypes.POINTER(ctypes.c_void_p)]),
     'deepep_sym_close': (_I, [_P]),
     'deepep_sym_barrier': (_I, [_P, _I, _I, _I64, _I64, _P, _P]),
+    'deepep_sym_put': (_I, [_P, _I64, _P, _I, _I64, _P, _P]),
     'deepep_sym_signal': (_I, [_P, _I, _I, _I, _I64, _P]),
     'deepep_sym_wait': (_I, [_P, _I, _I, _I, _I64, _I64, _P, _P]),
     'deepep_stream_create_cu_budget': (_I, [_I, ctypes.POINTER(ctypes.c_void_p)]),

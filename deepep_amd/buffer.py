@@ -440,20 +440,34 @@ class ElasticBuffer(ExchangeMixin):
             # and, over xGMI, at EP > 1),
             # as the reference's cached mode skips its notify phase (elastic.py:855-1033).
             cached = handle if handle is not None and handle._send_counts is not None else None
-            # dispatch(do_cpu_sync=False) on one rank issues kernels only (the reference's no-sync mode,
-            # buffer.hpp:1065-1070); EP > 1 still syncs once (the all-to-all needs host split sizes)
-            sync_free = cached is None and not do_cpu_sync and R == 1
+            # dispatch(do_cpu_sync=False) issues kernels only, at every EP size (the reference's no-sync
+            # mode, buffer.hpp:1065-1070): every receive-side launch is sized for the worst case
+            # (R * T_max rows) and bounded on the device by the received count; over RCCL the rows travel in
+            # a worst-case-padded all-to-all (equal splits, no host sizes), over xGMI the notify and the rows
+            # go through the symmetric windows.
+            sync_free = cached is None and not do_cpu_sync
             # EP > 1 over xGMI: the pack kernel stores every row straight into its destination's
             # symmetric window (dispatch.cuh:373-392's push), no RCCL exchange for the rows
             use_xgmi = R > 1 and self.transport == 'xgmi' and self.use_cuda
+            padded = sync_free and R > 1 and not use_xgmi        # worst-case-padded RCCL exchange
             peer_offsets = None
             counts = cached._counts if cached is not None else None
+            x_bytes = x.contiguous().view(torch.uint8).view(T, H * x.element_size())
+            sf_bytes = sf.contiguous().view(torch.uint8).view(T, sf.shape[1] * sf.element_size()) if sf is not None else None
+            # One rank: nothing is exchanged, so the packed rows carry only the routing metadata and
+            # the copy reads x (and the scale factors) once, straight from the caller's tensors.
+            direct = R == 1
+            layout = (RowLayout.make(0, 0, K) if direct else
+                      RowLayout.make(x_bytes.shape[1], sf_bytes.shape[1] if sf is not None else 0, K))
+            sym = self._window(layout.row_bytes, slots=R, rows_per_slot=num_max_tokens_per_rank) if use_xgmi else None
             if cached is not None:
                 _assert(do_expand == handle.do_expand, 'do_expand must match the cached handle')
                 dst_slot = cached.dst_buffer_slot_idx
                 send_counts_l, recv_counts_l = cached._send_counts, cached._recv_counts
                 send_offsets = cached._send_offsets
                 peer_offsets = getattr(cached, '_peer_offsets', None)
+                if use_xgmi and peer_offsets is not None:
+                    sym.barrier(stream)                           # peers finished reading their windows
                 use_xgmi = use_xgmi and peer_offsets is not None      # a handle made by the RCCL path
             else:
                 # --- send side: destination slots (deterministic ranks), one packed row per (token, dest)
@@ -470,56 +484,61 @@ class ElasticBuffer(ExchangeMixin):
                 if R > 1:
                     kern.route_block_counts(idx64, num_experts, R, nb, blk[0], blk[1], stream=stream)
                 # notify (dispatch.cuh:79-258): every destination gets [tokens | tokens per local expert |
-                # block counts] from this rank; one exchange and ONE host sync size every receive-side
-                # allocation and every combine exchange.
-                # The xGMI transport pushes rows straight into the peers' windows, so every rank needs
-                # the whole [source, destination] count matrix (its rows' offset in a peer's window is
-                # what the lower source ranks send there): the notify is all-gathered instead.
+                # block counts] from this rank; one exchange sizes every receive-side allocation and every
+                # combine exchange (and, unless sync-free, ONE host sync brings them to the host).
                 notify = torch.cat([send_counts.view(R, 1), expert_hist.view(R, epr), blk[0], blk[1]], dim=1)
+                w_n = notify.shape[1]
                 if R == 1:
                     recv_notify = notify
                 elif use_xgmi:
-                    everyone = torch.empty((R * R, notify.shape[1]), dtype=notify.dtype, device=dev)
-                    self._a2a(everyone, notify.repeat(R, 1))
-                    recv_notify = everyone.view(R, R, notify.shape[1])[:, r]
+                    # Through the windows: rank r puts [tokens it sends to every rank | its record for d] into
+                    # slot r of rank d's notify area; after the barrier rank r holds every source's record for
+                    # it and the token matrix its rows' offsets in the peers' windows come from -- the
+                    # reference's notify over NVLink, with no host collective (graph-capturable).
+                    rec_w = align(R + w_n, 4)
+                    rec = torch.zeros((R, rec_w), dtype=torch.int32, device=dev)
+                    rec[:, :R] = send_counts.view(1, R)
+                    rec[:, R:R + w_n] = notify
+                    sym.barrier(stream)                           # peers finished reading their windows
+                    sym.put_notify(rec, stream)
+                    sym.barrier(stream)                           # every rank's record landed
+                    area = sym.notify_area(rec_w)                 # [source, record]
+                    recv_notify = area[:, R:R + w_n].clone()
+                    # my rows' first row in every destination's window: what the lower source ranks send there
+                    peer_offsets = (area[:r, :R].sum(dim=0, dtype=torch.int32) if r > 0 else
+                                    torch.zeros((R,), dtype=torch.int32, device=dev))
                 else:
                     recv_notify = torch.empty_like(notify)
                     self._a2a(recv_notify, notify)
                 if sync_free:
-                    # one rank, no CPU sync: every receive-side launch is sized for all T tokens and bounded
-                    # on the device by the received count (psum of the notify); outputs are worst-case
-                    send_counts_l, recv_counts_l, expert_counts_l, offs = [T], [T], None, None
+                    # no CPU sync: the sizes stay on the device; launches are sized for the worst case (one
+                    # rank: T rows both ways, which a cached dispatch over this handle reuses)
+                    send_counts_l = recv_counts_l = [T] if R == 1 else None
+                    expert_counts_l = own_blk = recv_blk = None
                 else:
-                    host = [int(v) for v in torch.cat([send_counts, blk.view(-1), (everyone if R > 1 and use_xgmi else
-                                                                                   recv_notify).reshape(-1)]).tolist()]   # host sync
+                    host = [int(v) for v in torch.cat([send_counts, blk.view(-1),
+                                                       recv_notify.reshape(-1)]).tolist()]   # host sync
                     send_counts_l = host[:R]
                     own_blk = host[R:R + 2 * R * nb]
-                    _, recv_counts_l, expert_counts_l, offs, recv_blk = notify_layout(
-                        host[R + 2 * R * nb:], R, r, epr, all_gathered=R > 1 and use_xgmi, num_blocks=nb)
+                    _, recv_counts_l, expert_counts_l, _, recv_blk = notify_layout(
+                        host[R + 2 * R * nb:], R, r, epr, all_gathered=False, num_blocks=nb)
                 counts = None
                 if R > 1:
                     rb = recv_notify[:, 1 + epr:].reshape(R, 2, nb).transpose(0, 1)
-                    counts = BlockCounts(nb, [own_blk[d * nb:(d + 1) * nb] for d in range(R)],
-                                         [own_blk[(R + d) * nb:(R + d + 1) * nb] for d in range(R)],
-                                         [b[:nb] for b in recv_blk], [b[nb:] for b in recv_blk],
-                                         torch.cat([blk, rb]).contiguous())
-                if offs is not None:
-                    # pinned source: an asynchronous copy from a pageable temporary may read it after it
-                    # is freed (garbage offsets -> rows pushed into the wrong window rows)
-                    peer_offsets = torch.tensor(offs, dtype=torch.int32).pin_memory().to(dev, non_blocking=True)
+                    dev_counts = torch.cat([blk, rb]).contiguous()
+                    if sync_free:
+                        counts = BlockCounts(nb, None, None, None, None, dev_counts)
+                    else:
+                        counts = BlockCounts(nb, [own_blk[d * nb:(d + 1) * nb] for d in range(R)],
+                                             [own_blk[(R + d) * nb:(R + d + 1) * nb] for d in range(R)],
+                                             [b[:nb] for b in recv_blk], [b[nb:] for b in recv_blk], dev_counts)
                 recv_counts_t = recv_notify[:, 0].contiguous()
                 send_offsets = (torch.cumsum(send_counts, 0) - send_counts).to(torch.int32)
-            N = sum(recv_counts_l)
-            x_bytes = x.contiguous().view(torch.uint8).view(T, H * x.element_size())
-            sf_bytes = sf.contiguous().view(torch.uint8).view(T, sf.shape[1] * sf.element_size()) if sf is not None else None
-            # One rank: nothing is exchanged, so the packed rows carry only the routing metadata and
-            # the copy reads x (and the scale factors) once, straight from the caller's tensors.
-            direct = R == 1
-            layout = (RowLayout.make(0, 0, K) if direct else
-                      RowLayout.make(x_bytes.shape[1], sf_bytes.shape[1] if sf is not None else 0, K))
+            # received rows: known on the host, or the worst case (R * T_max) without a CPU sync
+            N = num_max_tokens_per_rank * R if sync_free else sum(recv_counts_l)
+            pad_rows = num_max_tokens_per_rank if padded else 0
+            row_map = None
             if use_xgmi:
-                sym = self._window(layout.row_bytes, slots=R, rows_per_slot=num_max_tokens_per_rank)
-                sym.barrier(stream)                               # peers finished reading their windows
                 kern.dispatch_pack(x_bytes, sf_bytes, idx64, w, r * num_max_tokens_per_rank, dst_slot,
                                    peer_offsets, None, layout, dest_bases=sym.data_bases_dev,
                                    dest_rows=sym.data_bytes // layout.row_bytes, error_flag=sym.error_flag,
@@ -528,15 +547,25 @@ class ElasticBuffer(ExchangeMixin):
                 if not self._capturing:
                     sym.publish(stream)
                 recv_packed = sym.data[:N * layout.row_bytes].view(N, layout.row_bytes)
+            elif padded:
+                # worst-case-padded all-to-all: T_max rows per destination (rank d's rows at d * T_max)
+                packed = torch.empty((R * num_max_tokens_per_rank, layout.row_bytes), dtype=torch.uint8, device=dev)
+                pad_offsets = torch.arange(R, dtype=torch.int32, device=dev) * num_max_tokens_per_rank
+                kern.dispatch_pack(x_bytes, sf_bytes, idx64, w, r * num_max_tokens_per_rank, dst_slot, pad_offsets,
+                                   packed, layout, stream=stream)
+                recv_packed = torch.empty_like(packed)
+                self._a2a(recv_packed, packed)
+                row_map = torch.empty((N,), dtype=torch.int32, device=dev)
             else:
-                packed = torch.empty((sum(send_counts_l), layout.row_bytes), dtype=torch.uint8, device=dev)
+                n_send = T if sync_free else sum(send_counts_l)
+                packed = torch.empty((n_send, layout.row_bytes), dtype=torch.uint8, device=dev)
                 kern.dispatch_pack(x_bytes[:, :0] if direct else x_bytes, None if direct else sf_bytes, idx64, w,
                                    r * num_max_tokens_per_rank, dst_slot, send_offsets, packed, layout, stream=stream)
-            if R == 1:
-                recv_packed = packed
-            elif not use_xgmi:
-                recv_packed = torch.empty((N, layout.row_bytes), dtype=torch.uint8, device=dev)
-                self._a2a(recv_packed, packed, recv_counts_l, send_counts_l)
+                if R == 1:
+                    recv_packed = packed
+                else:
+                    recv_packed = torch.empty((N, layout.row_bytes), dtype=torch.uint8, device=dev)
+                    self._a2a(recv_packed, packed, recv_counts_l, send_counts_l)
             # --- receive side (dispatch_copy_epilogue_impl): metadata, expert layout, copies
             inv = block_offsets = None                      # the expanded copy's tables (dispatch_copy)
             if cached is not None:
@@ -544,6 +573,7 @@ class ElasticBuffer(ExchangeMixin):
                 psum_expert = cached.psum_num_recv_tokens_per_expert
                 meta = cached.recv_src_metadata[:N]
                 inv, block_offsets = getattr(cached, '_copy_tables', (None, None))
+                row_map = getattr(cached, '_row_map', None)
                 out_idx = None if do_expand else cached._recv_topk_idx.clone()
                 aligned_l = cached.num_recv_tokens_per_expert_list
                 expert_counts = cached.num_unaligned_recv_tokens_per_expert
@@ -557,7 +587,7 @@ class ElasticBuffer(ExchangeMixin):
                 nblocks = (N + DISPATCH_BLOCK_ROWS - 1) // DISPATCH_BLOCK_ROWS
                 block_counts = torch.empty((nblocks, epr), dtype=torch.int32, device=dev)
                 kern.dispatch_count(recv_packed, layout, N, r, epr, psum_rank, meta, out_idx, block_counts,
-                                    stream=stream)
+                                    pad_rows=pad_rows, row_map=row_map, stream=stream)
                 expert_counts = torch.empty((epr,), dtype=torch.int32, device=dev)
                 psum_expert = torch.empty((epr,), dtype=torch.int32, device=dev)
                 kern.dispatch_scan(block_counts, epr, expert_alignment, do_expand, expert_counts, psum_expert,
@@ -573,7 +603,8 @@ class ElasticBuffer(ExchangeMixin):
                     inv = torch.empty((N * min(K, epr) + (expert_alignment - 1) * epr,), dtype=torch.int32,
                                       device=dev)
                     block_offsets = block_counts
-                    kern.dispatch_slots(recv_packed, layout, N, r, epr, block_counts, meta, inv=inv, stream=stream)
+                    kern.dispatch_slots(recv_packed, layout, N, r, epr, block_counts, meta, inv=inv, row_map=row_map,
+                                        stream=stream)
                 else:
                     meta[:, 2:] = -1
             num_unaligned = expert_counts
@@ -593,39 +624,28 @@ class ElasticBuffer(ExchangeMixin):
                 n_rows = num_expanded
             else:
                 num_expanded = N
-                alloc = torch.empty
+                # without a CPU sync the rows past the received ones are zeros (never written by the copy)
+                alloc = torch.zeros if sync_free else torch.empty
                 n_rows = N
             out_x = alloc((n_rows, H), dtype=x.dtype, device=dev)
             out_sf = alloc((n_rows, sf.shape[1]), dtype=sf.dtype, device=dev) if sf is not None else None
             out_w = None
             if topk_weights is not None:
                 out_w = (torch.zeros((n_rows,), dtype=torch.float32, device=dev) if do_expand else
-                         torch.empty((N, K), dtype=torch.float32, device=dev))
+                         alloc((N, K), dtype=torch.float32, device=dev))
             kern.dispatch_copy(recv_packed, layout, N, meta, do_expand,
                                out_x.view(torch.uint8), out_sf.view(torch.uint8) if out_sf is not None else None,
                                out_w, x_direct=x_bytes if direct else None,
                                sf_direct=sf_bytes if direct else None, num_max_tokens=num_max_tokens_per_rank,
                                error_flag=sym.error_flag if use_xgmi else None,
                                inv=inv if do_expand else None, block_offsets=block_offsets if do_expand else None,
-                               expert_end=psum_expert if do_expand else None, stream=stream)
+                               expert_end=psum_expert if do_expand else None, row_map=row_map, stream=stream)
             recv_idx64 = out_idx
             if out_idx is not None and topk_idx.dtype != torch.int64:
                 out_idx = out_idx.to(topk_idx.dtype)
+            # without a CPU sync N is already the worst case (buffer.hpp:1065-1070): metadata rows past the
+            # received ones are -1 (dispatch_count), non-expanded outputs there are zeros / -1
             num_recv = N
-            if not do_cpu_sync and handle is None:
-                # Worst-case shapes, as the reference allocates without a CPU sync (buffer.hpp:1065-1070)
-                worst = num_max_tokens_per_rank * R
-                meta = torch.cat([meta, torch.full((worst - N, K + 2), -1, dtype=torch.int32, device=dev)])
-                if not do_expand:
-                    out_x = torch.cat([out_x, torch.zeros((worst - N, H), dtype=x.dtype, device=dev)])
-                    out_idx = torch.cat([out_idx, torch.full((worst - N, K), -1, dtype=out_idx.dtype, device=dev)])
-                    if out_w is not None:
-                        out_w = torch.cat([out_w, torch.zeros((worst - N, K), dtype=torch.float32, device=dev)])
-                    if out_sf is not None:
-                        out_sf = torch.cat([out_sf, torch.zeros((worst - N, out_sf.shape[1]), dtype=out_sf.dtype,
-                                                                device=dev)])
-                    num_expanded = worst
-                num_recv = worst
             cloned_idx = topk_idx.clone() if do_handle_copy else topk_idx
         event = self._epilogue([x, sf, topk_idx, topk_weights, out_x, out_sf, out_idx, out_w, meta],
                                compute_stream, allocate_on_comm_stream, async_with_compute_stream)
@@ -641,6 +661,7 @@ class ElasticBuffer(ExchangeMixin):
             handle._recv_topk_idx = recv_idx64
             handle._counts = counts
             handle._copy_tables = (inv, block_offsets)      # reused by cached dispatches
+            handle._row_map = row_map
         out_x = (out_x, out_sf) if out_sf is not None else out_x
         return out_x, out_idx, out_w, handle, EventOverlap(event)
 

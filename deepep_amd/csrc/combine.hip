@@ -111,6 +111,7 @@ struct Params {
 // the error record: a wild store through a bad address is never issued).  Wave-uniform.
 __device__ __forceinline__ uint64_t checked_row(const Params& p, int64_t u, int lane, bool report) {
     const uint64_t a = p.out_rows[u];
+    if (a == 1ull) return 0ull;                          // a padding position of a padded plan: no unit
     if (a == 0ull) {
         if (report && lane == 0 && p.error_flag != nullptr) atomicOr(p.error_flag, DEEPEP_FLAG_BAD_SLOT);
         return 0ull;

@@ -224,7 +224,8 @@ __device__ __forceinline__ int local_expert(int64_t e, int rank, int epr) {
 // the received ones get metadata -1 (and recv_topk_idx -1): the later kernels skip them.
 __global__ void __launch_bounds__(kBlockRows)
 count_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int idx_off, int src_off, int N, int K,
-             int rank, int epr, const int32_t* __restrict__ rank_psum, int R,
+             int rank, int epr, const int32_t* __restrict__ rank_psum, int R, int pad_rows,
+             int32_t* __restrict__ row_map,
              int32_t* __restrict__ meta, int64_t* __restrict__ recv_topk_idx, int32_t* __restrict__ block_counts) {
     extern __shared__ int32_t s_hist[];                 // [epr]
     for (int e = threadIdx.x; e < epr; e += kBlockRows) s_hist[e] = 0;
@@ -239,10 +240,15 @@ count_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int idx_off,
             for (int k = 0; k < K; ++k) recv_topk_idx[static_cast<int64_t>(i) * K + k] = -1;
     }
     if (i < received) {
-        const uint8_t* row = packed + static_cast<int64_t>(i) * row_bytes;
-        const int64_t* idx = reinterpret_cast<const int64_t*>(row + idx_off);
         int src_rank = 0;
         while (src_rank < R - 1 && i >= rank_psum[src_rank]) ++src_rank;
+        // padded receive buffer (a worst-case-sized exchange): source s's rows start at s * pad_rows
+        const int64_t prow = pad_rows > 0 ? static_cast<int64_t>(src_rank) * pad_rows + i -
+                                                (src_rank > 0 ? rank_psum[src_rank - 1] : 0)
+                                          : i;
+        if (row_map != nullptr) row_map[i] = static_cast<int32_t>(prow);
+        const uint8_t* row = packed + prow * row_bytes;
+        const int64_t* idx = reinterpret_cast<const int64_t*>(row + idx_off);
         int master = -1;
         for (int k = 0; k < K; ++k) {
             const int le = local_expert(idx[k], rank, epr);
@@ -318,14 +324,16 @@ constexpr int kSlotWaves = kBlockRows / 64;
 
 __global__ void __launch_bounds__(kBlockRows)
 slots_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int idx_off, int N, int K, int rank, int epr,
-             const int32_t* __restrict__ block_offsets, int32_t* __restrict__ meta, int32_t* __restrict__ inv) {
+             const int32_t* __restrict__ block_offsets, int32_t* __restrict__ meta, int32_t* __restrict__ inv,
+             const int32_t* __restrict__ row_map) {
     extern __shared__ uint64_t s_bits[];                // [epr][kSlotWaves]
     for (int j = threadIdx.x; j < epr * kSlotWaves; j += kBlockRows) s_bits[j] = 0ull;
     __syncthreads();
     const int i = blockIdx.x * kBlockRows + threadIdx.x;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t* idx = reinterpret_cast<const int64_t*>(packed + static_cast<int64_t>(i) * row_bytes + idx_off);
     const bool valid = i < N && meta[static_cast<int64_t>(i) * (K + 2)] >= 0;
+    const int64_t prow = valid && row_map != nullptr ? row_map[i] : i;
+    const int64_t* idx = reinterpret_cast<const int64_t*>(packed + prow * row_bytes + idx_off);
     if (valid)
         for (int k = 0; k < K; ++k) {
             const int le = local_expert(idx[k], rank, epr);
@@ -359,7 +367,7 @@ copy_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int x_bytes, 
             const uint8_t* __restrict__ x_direct, int64_t x_direct_stride,
             const uint8_t* __restrict__ sf_direct, int64_t sf_direct_stride, int num_max_tokens,
             uint8_t* __restrict__ recv_x, uint8_t* __restrict__ recv_sf, float* __restrict__ recv_w,
-            int64_t num_out_rows, int32_t* __restrict__ error_flag) {
+            int64_t num_out_rows, const int32_t* __restrict__ row_map, int32_t* __restrict__ error_flag) {
     constexpr int kChunkVecs = 128;                        // 64 lanes x 2 x 16 B
     const int lane = threadIdx.x & 63;
     // a timed-out window barrier (bit 2): the received rows are not trustworthy, store nothing
@@ -372,7 +380,7 @@ copy_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int x_bytes, 
     const int64_t i = it / nchunks;
     const int c = static_cast<int>(it - i * nchunks);
     if (meta[i * (K + 2)] < 0) return;                     // past the received rows (count_kernel)
-    const uint8_t* row = packed + i * row_bytes;
+    const uint8_t* row = packed + (row_map != nullptr ? static_cast<int64_t>(row_map[i]) : i) * row_bytes;
     const uint8_t* xs = row;
     const uint8_t* sfs = row + sf_off;
     if (x_direct != nullptr) {
@@ -443,7 +451,7 @@ copy_expanded_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int 
                      const int32_t* __restrict__ inv, const int32_t* __restrict__ block_offsets,
                      const int32_t* __restrict__ expert_end, int nb, int epr,
                      uint8_t* __restrict__ recv_x, uint8_t* __restrict__ recv_sf, float* __restrict__ recv_w,
-                     int64_t num_out_rows, int32_t* __restrict__ error_flag) {
+                     int64_t num_out_rows, const int32_t* __restrict__ row_map, int32_t* __restrict__ error_flag) {
     constexpr int kChunkVecs = 128;                        // 64 lanes x 2 x 16 B
     constexpr int kRows = 4;                               // destination rows in flight per wave
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -480,7 +488,7 @@ copy_expanded_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int 
                         const int64_t t = meta[static_cast<int64_t>(i) * (K + 2)] % num_max_tokens;
                         rows[q] = x_direct + t * x_direct_stride;
                     } else {
-                        rows[q] = packed + static_cast<int64_t>(i) * row_bytes;
+                        rows[q] = packed + (row_map != nullptr ? static_cast<int64_t>(row_map[i]) : i) * row_bytes;
                     }
                     const u32x4* xs = reinterpret_cast<const u32x4*>(rows[q]);
                     a[q][0] = v0 < nvec ? xs[v0] : zero;
@@ -514,8 +522,10 @@ copy_expanded_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int 
                     for (int v = lane; v < sf_bytes / 4; v += 64)
                         reinterpret_cast<uint32_t*>(recv_sf + d * sf_bytes)[v] = reinterpret_cast<const uint32_t*>(sfs)[v];
             }
-            if (recv_w != nullptr && lane == 0)
-                recv_w[d] = reinterpret_cast<const float*>(packed + static_cast<int64_t>(src_i[q]) * row_bytes + w_off)[src_k[q]];
+            if (recv_w != nullptr && lane == 0) {
+                const int64_t prow = row_map != nullptr ? static_cast<int64_t>(row_map[src_i[q]]) : src_i[q];
+                recv_w[d] = reinterpret_cast<const float*>(packed + prow * row_bytes + w_off)[src_k[q]];
+            }
         }
     }
 }
@@ -605,18 +615,20 @@ int deepep_dispatch_pack(const void* x, int64_t x_row_stride_bytes, int x_bytes,
 
 int deepep_dispatch_count(const void* packed, int64_t row_bytes, int idx_off, int src_off, int num_recv, int num_topk,
                           int rank, int num_local_experts, const int32_t* recv_rank_psum, int num_ranks,
+                          int pad_rows, int32_t* row_map,
                           int32_t* src_metadata, int64_t* recv_topk_idx, int32_t* block_counts,
                           deepep_stream_t stream) {
     if (num_recv == 0) return DEEPEP_OK;                  // a rank that receives nothing
     if (num_recv < 0 || num_topk < 1 || num_topk > 32 || num_local_experts < 1 || num_local_experts > 1024 ||
         num_ranks < 1 || src_metadata == nullptr || block_counts == nullptr || packed == nullptr ||
-        recv_rank_psum == nullptr)
+        recv_rank_psum == nullptr || pad_rows < 0 || (pad_rows > 0 && row_map == nullptr) ||
+        static_cast<int64_t>(pad_rows) * num_ranks >= (int64_t(1) << 31))
         return deepep_amd_set_error(DEEPEP_ERR_INVALID_ARG, "dispatch_count: invalid arguments");
     const int nblocks = (num_recv + kBlockRows - 1) / kBlockRows;
     hipLaunchKernelGGL(count_kernel, dim3(nblocks), dim3(kBlockRows), num_local_experts * 4,
                        reinterpret_cast<hipStream_t>(stream), static_cast<const uint8_t*>(packed), row_bytes,
                        idx_off, src_off, num_recv, num_topk, rank, num_local_experts, recv_rank_psum, num_ranks,
-                       src_metadata, recv_topk_idx, block_counts);
+                       pad_rows, row_map, src_metadata, recv_topk_idx, block_counts);
     return launch_status("dispatch_count");
 }
 
@@ -633,7 +645,7 @@ int deepep_dispatch_scan(int32_t* block_counts, int num_blocks, int num_local_ex
 
 int deepep_dispatch_slots(const void* packed, int64_t row_bytes, int idx_off, int num_recv, int num_topk,
                           int rank, int num_local_experts, const int32_t* block_offsets, int32_t* src_metadata,
-                          int32_t* inv, deepep_stream_t stream) {
+                          int32_t* inv, const int32_t* row_map, deepep_stream_t stream) {
     if (num_recv == 0) return DEEPEP_OK;
     if (num_recv < 0 || num_topk < 1 || num_topk > 32 || num_local_experts < 1 || num_local_experts > 1024 ||
         packed == nullptr || block_offsets == nullptr || src_metadata == nullptr ||
@@ -642,7 +654,8 @@ int deepep_dispatch_slots(const void* packed, int64_t row_bytes, int idx_off, in
     const int nblocks = (num_recv + kBlockRows - 1) / kBlockRows;
     hipLaunchKernelGGL(slots_kernel, dim3(nblocks), dim3(kBlockRows), num_local_experts * kSlotWaves * 8,
                        reinterpret_cast<hipStream_t>(stream), static_cast<const uint8_t*>(packed), row_bytes,
-                       idx_off, num_recv, num_topk, rank, num_local_experts, block_offsets, src_metadata, inv);
+                       idx_off, num_recv, num_topk, rank, num_local_experts, block_offsets, src_metadata, inv,
+                       row_map);
     return launch_status("dispatch_slots");
 }
 
@@ -652,7 +665,7 @@ int deepep_dispatch_copy(const void* packed, int64_t row_bytes, int x_bytes, int
                          const void* sf_direct, int64_t sf_direct_stride_bytes, int num_max_tokens,
                          void* recv_x, void* recv_sf, float* recv_topk_weights, int64_t num_out_rows,
                          const int32_t* inv, const int32_t* block_offsets, const int32_t* expert_end,
-                         int num_local_experts, int32_t* error_flag, deepep_stream_t stream) {
+                         int num_local_experts, const int32_t* row_map, int32_t* error_flag, deepep_stream_t stream) {
     if (num_recv == 0) return DEEPEP_OK;
     if (num_recv < 0 || num_topk < 1 || num_topk > 32 || x_bytes % 16 || row_bytes % 16 || !a16(packed) ||
         num_out_rows < 0 ||
@@ -676,7 +689,7 @@ int deepep_dispatch_copy(const void* packed, int64_t row_bytes, int x_bytes, int
                                x_direct_stride_bytes, static_cast<const uint8_t*>(sf_direct), sf_direct_stride_bytes,
                                num_max_tokens, inv, block_offsets, expert_end, nb, num_local_experts,
                                static_cast<uint8_t*>(recv_x), static_cast<uint8_t*>(recv_sf), recv_topk_weights,
-                               num_out_rows, error_flag);
+                               num_out_rows, row_map, error_flag);
         };
         if (x_direct != nullptr) launch(copy_expanded_kernel<true>);
         else launch(copy_expanded_kernel<false>);
@@ -691,7 +704,7 @@ int deepep_dispatch_copy(const void* packed, int64_t row_bytes, int x_bytes, int
                        static_cast<const uint8_t*>(x_direct), x_direct_stride_bytes,
                        static_cast<const uint8_t*>(sf_direct), sf_direct_stride_bytes, num_max_tokens,
                        static_cast<uint8_t*>(recv_x), static_cast<uint8_t*>(recv_sf), recv_topk_weights,
-                       num_out_rows, error_flag);
+                       num_out_rows, row_map, error_flag);
     return launch_status("dispatch_copy");
 }
 

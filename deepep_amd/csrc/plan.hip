@@ -80,7 +80,7 @@ plan_expert_kernel(const int32_t* __restrict__ meta, int num_recv, int K, int R,
                    const int32_t* __restrict__ recv_tok, const int32_t* __restrict__ recv_pairs, int nb, int bpc,
                    int flags, int32_t* __restrict__ table_a, int32_t* __restrict__ wtable_a,
                    const uint64_t* __restrict__ bases, int64_t row_bytes, int64_t window_bytes,
-                   uint64_t* __restrict__ out_rows, int32_t* __restrict__ err) {
+                   uint64_t* __restrict__ out_rows, int32_t* __restrict__ err, int padded) {
     __shared__ int s_n[kMaxRanks];
     const int lane = threadIdx.x;
     const int s = blockIdx.x / nb, b = blockIdx.x - s * nb;
@@ -106,11 +106,15 @@ plan_expert_kernel(const int32_t* __restrict__ meta, int num_recv, int K, int R,
     }
     __syncthreads();
     const int seg_row0 = wave_sum(lane < s ? rows_l : 0) + __shfl(rows_s_before, s, 64);
-    const int chunk_base = wave_sum(before_l);
-    const int chunk_units = wave_sum(n_l);                      // units of the whole chunk
-    const int grouped_base = wave_sum(lane < s ? n_l : 0);
+    // padded (a sync-free dispatch's handle: the host knows no counts): every chunk holds R x `padded`
+    // unit positions, source s's units at s * padded + p (or p * R + s interleaved); positions past a
+    // source's count stay the caller's fill and are skipped
+    const int chunk_base = padded > 0 ? (b / bpc) * R * padded : wave_sum(before_l);
+    const int chunk_units = padded > 0 ? R * padded : wave_sum(n_l);     // units of the whole chunk
+    const int grouped_base = padded > 0 ? s * padded : wave_sum(lane < s ? n_l : 0);
     p0 = __shfl(p0, s, 64);
     auto position = [&](int p) -> int {                         // unit p of source s inside the chunk
+        if (padded > 0) return interleave ? p * R + s : grouped_base + p;
         if (!interleave) return grouped_base + p;
         int pos = 0;
         for (int l = 0; l < R; ++l) pos += min(s_n[l], p + (l < s ? 1 : 0));
@@ -187,7 +191,7 @@ __global__ void __launch_bounds__(64)
 plan_source_kernel(const int64_t* __restrict__ topk_idx, int T, int K, int epr, int R, int t_max,
                    const int32_t* __restrict__ dst_slot, const int32_t* __restrict__ send_tok,
                    const int32_t* __restrict__ send_pairs, int nb, int bpc, int flags, int64_t row_floats,
-                   int64_t w_off, int32_t* __restrict__ table_b, int width, int32_t* __restrict__ wtable) {
+                   int64_t w_off, int32_t* __restrict__ table_b, int width, int32_t* __restrict__ wtable, int padded) {
     __shared__ int s_base[kMaxRanks];
     const int lane = threadIdx.x, b = blockIdx.x;
     const int t = b * kBlk + lane;
@@ -207,7 +211,8 @@ plan_source_kernel(const int64_t* __restrict__ topk_idx, int T, int K, int epr, 
             }
         }
         const int incl = wave_incl_scan(lane < R ? n_l : 0, lane);
-        if (lane < R) s_base[lane] = incl - n_l + extra;
+        // padded: expert rank d's rows of the chunk start at d * padded (a worst-case-padded exchange)
+        if (lane < R) s_base[lane] = (padded > 0 ? lane * padded : incl - n_l) + extra;
         __syncthreads();
     }
     int rk[kMaxTopk];
@@ -296,9 +301,12 @@ int deepep_plan_expert(const int32_t* src_metadata, int num_recv, int num_topk, 
                        int num_max_tokens, const int32_t* recv_tok, const int32_t* recv_pairs, int num_blocks,
                        int blocks_per_chunk, int flags, int32_t* table_a, int32_t* wtable_a,
                        const uint64_t* window_bases, int64_t window_row_bytes, int64_t window_bytes,
-                       uint64_t* out_rows, int32_t* error_flag, deepep_stream_t stream) {
+                       uint64_t* out_rows, int32_t* error_flag, int padded_stride, deepep_stream_t stream) {
     const bool single = flags & DEEPEP_PLAN_SINGLE;
-    if (num_recv < 0 || num_topk < 1 || num_topk > kMaxTopk || num_ranks < 1 || num_ranks > kMaxRanks || rank < 0 ||
+    if (num_recv < 0 || padded_stride < 0 ||
+        static_cast<int64_t>(padded_stride) * num_ranks * ((num_blocks + blocks_per_chunk - 1) /
+                                                           (blocks_per_chunk > 0 ? blocks_per_chunk : 1)) >=
+            (int64_t(1) << 31) || num_topk < 1 || num_topk > kMaxTopk || num_ranks < 1 || num_ranks > kMaxRanks || rank < 0 ||
         rank >= num_ranks || num_max_tokens < 1 || num_blocks < 0 || blocks_per_chunk < 1 ||
         (num_blocks > 0 && (recv_tok == nullptr || (single && recv_pairs == nullptr))) ||
         (num_recv > 0 && src_metadata == nullptr) ||
@@ -310,7 +318,7 @@ int deepep_plan_expert(const int32_t* src_metadata, int num_recv, int num_topk, 
     hipLaunchKernelGGL(plan_expert_kernel, dim3(num_ranks * num_blocks), dim3(64), 0,
                        reinterpret_cast<hipStream_t>(stream), src_metadata, num_recv, num_topk, num_ranks, rank,
                        num_max_tokens, recv_tok, recv_pairs, num_blocks, blocks_per_chunk, flags, table_a, wtable_a,
-                       window_bases, window_row_bytes, window_bytes, out_rows, error_flag);
+                       window_bases, window_row_bytes, window_bytes, out_rows, error_flag, padded_stride);
     return launch_status("plan_expert");
 }
 
@@ -318,10 +326,10 @@ int deepep_plan_source(const int64_t* topk_idx, int num_tokens, int num_topk, in
                        int num_max_tokens, const int32_t* dst_slot, const int32_t* send_tok,
                        const int32_t* send_pairs, int num_blocks, int blocks_per_chunk, int flags,
                        int64_t row_floats, int64_t weights_offset, int32_t* table_b, int table_b_width,
-                       int32_t* wtable, deepep_stream_t stream) {
+                       int32_t* wtable, int padded_stride, deepep_stream_t stream) {
     const bool single = flags & DEEPEP_PLAN_SINGLE, window = flags & DEEPEP_PLAN_WINDOW;
     const int need_width = single ? num_topk : (num_ranks < num_topk ? num_ranks : num_topk);
-    if (num_tokens < 0 || num_topk < 1 || num_topk > kMaxTopk || num_ranks < 1 || num_ranks > kMaxRanks ||
+    if (num_tokens < 0 || padded_stride < 0 || (window && padded_stride > 0) || num_topk < 1 || num_topk > kMaxTopk || num_ranks < 1 || num_ranks > kMaxRanks ||
         num_experts % num_ranks != 0 || num_tokens > num_max_tokens || blocks_per_chunk < 1 ||
         num_blocks < (num_tokens + kBlk - 1) / kBlk || table_b_width != need_width ||
         (num_tokens > 0 && (topk_idx == nullptr || table_b == nullptr)) ||
@@ -332,7 +340,8 @@ int deepep_plan_source(const int64_t* topk_idx, int num_tokens, int num_topk, in
     hipLaunchKernelGGL(plan_source_kernel, dim3((num_tokens + kBlk - 1) / kBlk), dim3(64), 0,
                        reinterpret_cast<hipStream_t>(stream), topk_idx, num_tokens, num_topk,
                        num_experts / num_ranks, num_ranks, num_max_tokens, dst_slot, send_tok, send_pairs, num_blocks,
-                       blocks_per_chunk, flags, row_floats, weights_offset, table_b, table_b_width, wtable);
+                       blocks_per_chunk, flags, row_floats, weights_offset, table_b, table_b_width, wtable,
+                       padded_stride);
     return launch_status("plan_source");
 }
 

@@ -139,6 +139,22 @@ sym_wait_kernel(const uint64_t* peer_flags, int rank, int num_ranks, int slot, i
     __threadfence_system();
 }
 
+// The notify put: workgroup d copies src row d (bytes) into destination d's window at dest_offset with
+// system-scope write-through stores (they reach the peer's HBM; the barrier after the put orders them).
+__global__ void __launch_bounds__(256)
+sym_put_kernel(const uint32_t* __restrict__ src, int64_t bytes, const uint64_t* __restrict__ dest_bases,
+               int64_t dest_offset, const int32_t* __restrict__ error_flag) {
+    if (error_flag != nullptr && (__hip_atomic_load(error_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 2))
+        return;
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const int64_t d = blockIdx.x;
+    const u32x4* s = reinterpret_cast<const u32x4*>(src + d * (bytes / 4));
+    uint8_t* dst = reinterpret_cast<uint8_t*>(dest_bases[d]) + dest_offset;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, 0, static_cast<int>(bytes), 0x00020000);
+    for (int64_t v = threadIdx.x; v < bytes / 16; v += blockDim.x)
+        __builtin_amdgcn_raw_buffer_store_b128(s[v], rs, static_cast<int>(v * 16), 0, 17);    // sc0 sc1
+}
+
 // After a barrier or a wait: every XCD invalidates its L2 (system scope) before the stream's next
 // kernel reads what the peers stored into this rank's window (one extra small launch).
 __global__ void __launch_bounds__(64) invalidate_all_xcds_kernel() {
@@ -293,6 +309,19 @@ int deepep_stream_destroy(deepep_stream_t stream) {
     deepep_amd_register_budget(stream, 0);
     const hipError_t e = hipStreamDestroy(reinterpret_cast<hipStream_t>(stream));
     return e == hipSuccess ? DEEPEP_OK : hip_fail(e, "hipStreamDestroy");
+}
+
+int deepep_sym_put(const void* src, int64_t bytes, const uint64_t* dest_bases, int num_ranks, int64_t dest_offset,
+                   const int32_t* error_flag, deepep_stream_t stream) {
+    if (num_ranks < 1 || num_ranks > 64 || bytes < 0 || bytes % 16 || bytes > (int64_t(1) << 30) || dest_offset < 0 ||
+        dest_offset % 16 || (bytes > 0 && (src == nullptr || dest_bases == nullptr)) ||
+        (reinterpret_cast<uintptr_t>(src) & 15))
+        return deepep_amd_set_error(DEEPEP_ERR_INVALID_ARG, "sym_put: bad arguments");
+    if (bytes == 0) return DEEPEP_OK;
+    hipLaunchKernelGGL(sym_put_kernel, dim3(num_ranks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                       static_cast<const uint32_t*>(src), bytes, dest_bases, dest_offset, error_flag);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? DEEPEP_OK : hip_fail(e, "put launch");
 }
 
 int deepep_sym_barrier(const uint64_t* peer_flags, int rank, int num_ranks, int64_t epoch, int64_t timeout_us,

@@ -39,10 +39,10 @@ class BlockCounts:
     notify).  Host lists (known since the dispatch's host sync) size the exchanges; the device tensor
     `dev` [4, R, nb] (send_tok, send_pairs, recv_tok, recv_pairs) feeds the plan kernels."""
     num_blocks: int
-    send_tok: List[List[int]]
-    send_pairs: List[List[int]]
-    recv_tok: List[List[int]]
-    recv_pairs: List[List[int]]
+    send_tok: Optional[List[List[int]]]              # the host lists are None after a dispatch without a
+    send_pairs: Optional[List[List[int]]]            # CPU sync: the combine plan is then worst-case padded
+    recv_tok: Optional[List[List[int]]]
+    recv_pairs: Optional[List[List[int]]]
     dev: torch.Tensor
 
 
@@ -119,8 +119,18 @@ def build_ep_plan(kern, handle: 'EPHandle', *, num_ranks: int, rank: int, single
     expanded = handle.do_expand
     rank_layout = R <= K                             # use_rank_layout (combine_utils.cuh:8-13)
     dev = handle.recv_src_metadata.device
+    # A handle from a dispatch without a CPU sync: the counts live on the device only, so every chunk
+    # is laid out for the worst case -- `padded` unit positions per source rank (a chunk's tokens, times
+    # K for the single reduction), the unused ones skipped by phase A (zero partials over RCCL, padding
+    # rows the scatter ignores over xGMI) -- and the RCCL exchange moves R x padded rows per chunk.
+    padded = 0
+    if cnt.recv_tok is None:
+        padded = bpc * PLAN_BLOCK_TOKENS * (K if single else 1)
     # ---- expert side: phase-A units of every chunk, concatenated
-    units = _chunk_sums(cnt.recv_pairs if single else cnt.recv_tok, bpc, C)       # [c][source rank]
+    if padded:
+        units = [[padded] * R for _ in range(C)]
+    else:
+        units = _chunk_sums(cnt.recv_pairs if single else cnt.recv_tok, bpc, C)   # [c][source rank]
     n_units = [sum(u) for u in units]
     total = sum(n_units)
     flags = ((PLAN_EXPANDED if expanded else 0) | (PLAN_SINGLE if single else 0) |
@@ -132,15 +142,19 @@ def build_ep_plan(kern, handle: 'EPHandle', *, num_ranks: int, rank: int, single
     wtable_a = torch.full((total, K), -1, dtype=torch.int32, device=dev) if not expanded else None
     if window is not None:
         row_bytes = packed_row_layout(hidden, K, True, single)[0]
-        out_rows = torch.zeros((total,), dtype=torch.int64, device=dev)
+        # 1 marks a padding position (skipped silently), 0 a unit the plan kernel rejects (flagged)
+        out_rows = torch.full((total,), 1 if padded else 0, dtype=torch.int64, device=dev)
         bases, win_bytes, err = window.data_bases_dev, window.data_bytes, window.error_flag
     else:
         row_bytes, out_rows, bases, win_bytes, err = 0, None, None, 0, None
     kern.plan_expert(handle.recv_src_metadata, K, R, rank, T_max, cnt.dev[2], cnt.dev[3], nb, bpc, flags,
                      table_a, wtable_a, bases, row_bytes, out_rows, window_bytes=win_bytes, error_flag=err,
-                     stream=stream)
+                     padded_stride=padded, stream=stream)
     # ---- source side: the rows phase B reduces per owned token
-    back = _chunk_sums(cnt.send_pairs if single else cnt.send_tok, bpc, C)       # [c][expert rank]
+    if padded:
+        back = [[padded] * R for _ in range(C)]
+    else:
+        back = _chunk_sums(cnt.send_pairs if single else cnt.send_tok, bpc, C)   # [c][expert rank]
     width_b = K if single else min(R, K)
     table_b = torch.empty((T, width_b), dtype=torch.int32, device=dev)
     wtable_b = None
@@ -155,7 +169,8 @@ def build_ep_plan(kern, handle: 'EPHandle', *, num_ranks: int, rank: int, single
     sflags = (PLAN_SINGLE if single else 0) | (PLAN_WINDOW if window is not None else 0) | \
              (PLAN_RANK_LAYOUT if rank_layout and not single else 0)
     kern.plan_source(handle.topk_idx, handle.num_experts, R, T_max, handle.dst_buffer_slot_idx, cnt.dev[0],
-                     cnt.dev[1], nb, bpc, sflags, row_floats, w_off_f, table_b, wtable_b, stream=stream)
+                     cnt.dev[1], nb, bpc, sflags, row_floats, w_off_f, table_b, wtable_b,
+                     padded_stride=padded if window is None else 0, stream=stream)
     plan = CombinePlan(num_ranks=R, num_tokens=T, num_topk=K, expanded=expanded, chunks=[],
                        window_row_bytes=row_bytes)
     u0 = 0

@@ -194,7 +194,7 @@ class HipKernels:
 
     def plan_expert(self, meta, num_topk, num_ranks, rank, num_max_tokens, recv_tok, recv_pairs, num_blocks,
                     blocks_per_chunk, flags, table_a, wtable_a, window_bases, window_row_bytes, out_rows,
-                    window_bytes: int = 0, error_flag=None, stream=None):
+                    window_bytes: int = 0, error_flag=None, padded_stride: int = 0, stream=None):
         """window_bytes: the data extent of every window (out_rows rows are bounded by it); error_flag:
         an error record (_lib.ERROR_RECORD_INTS ints) or None.  table_a / wtable_a / out_rows should be
         pre-filled with -1 / -1 / 0: a unit the kernel rejects is left as it was."""
@@ -207,11 +207,13 @@ class HipKernels:
         rc = self.lib.deepep_plan_expert(ptr(meta), meta.shape[0], num_topk, num_ranks, rank, num_max_tokens,
                                          ptr(recv_tok), ptr(recv_pairs), num_blocks, blocks_per_chunk, flags,
                                          ptr(table_a), ptr(wtable_a), ptr(window_bases), window_row_bytes,
-                                         int(window_bytes), ptr(out_rows), ptr(error_flag), _stream_handle(stream))
+                                         int(window_bytes), ptr(out_rows), ptr(error_flag), int(padded_stride),
+                                         _stream_handle(stream))
         _lib.check(rc, 'plan_expert')
 
     def plan_source(self, topk_idx, num_experts, num_ranks, num_max_tokens, dst_slot, send_tok, send_pairs,
-                    num_blocks, blocks_per_chunk, flags, row_floats, weights_offset, table_b, wtable, stream=None):
+                    num_blocks, blocks_per_chunk, flags, row_floats, weights_offset, table_b, wtable,
+                    padded_stride: int = 0, stream=None):
         _require(topk_idx.is_cuda and topk_idx.dtype == torch.int64 and topk_idx.is_contiguous(), 'topk_idx int64')
         _require(table_b.dtype == torch.int32 and table_b.is_contiguous(), 'table_b int32')
         _require(wtable is None or (wtable.dtype == torch.int32 and wtable.is_contiguous()), 'wtable int32')
@@ -219,7 +221,7 @@ class HipKernels:
         rc = self.lib.deepep_plan_source(ptr(topk_idx), T, K, num_experts, num_ranks, num_max_tokens, ptr(dst_slot),
                                          ptr(send_tok), ptr(send_pairs), num_blocks, blocks_per_chunk, flags,
                                          row_floats, weights_offset, ptr(table_b), table_b.shape[1], ptr(wtable),
-                                         _stream_handle(stream))
+                                         int(padded_stride), _stream_handle(stream))
         _lib.check(rc, 'plan_source')
 
     def dispatch_pack(self, x_bytes, sf_bytes, topk_idx, topk_weights, src_base, dst_slot, send_offsets,
@@ -246,11 +248,16 @@ class HipKernels:
         _lib.check(rc, 'dispatch_pack')
 
     def dispatch_count(self, packed, layout: RowLayout, num_recv, rank, num_local_experts, rank_psum, meta,
-                       recv_topk_idx, block_counts, stream=None):
+                       recv_topk_idx, block_counts, pad_rows: int = 0, row_map=None, stream=None):
+        """pad_rows > 0: `packed` is a worst-case-sized receive buffer, source s's rows at s * pad_rows;
+        row_map (int32 [num_recv]) receives each received row's packed row (for slots / copy)."""
+        _require(pad_rows == 0 or (row_map is not None and row_map.dtype == torch.int32 and
+                                   row_map.numel() >= num_recv and packed.shape[0] >= pad_rows * rank_psum.shape[0]),
+                 'padded receive rows need a row map and R * pad_rows packed rows')
         rc = self.lib.deepep_dispatch_count(
             ptr(packed), layout.row_bytes, layout.idx_off, layout.src_off, num_recv, layout.num_topk, rank,
-            num_local_experts, ptr(rank_psum), rank_psum.shape[0], ptr(meta), ptr(recv_topk_idx),
-            ptr(block_counts), _stream_handle(stream))
+            num_local_experts, ptr(rank_psum), rank_psum.shape[0], pad_rows, ptr(row_map), ptr(meta),
+            ptr(recv_topk_idx), ptr(block_counts), _stream_handle(stream))
         _lib.check(rc, 'dispatch_count')
 
     def dispatch_scan(self, block_counts, num_local_experts, expert_alignment, expanded, expert_counts,
@@ -261,17 +268,17 @@ class HipKernels:
         _lib.check(rc, 'dispatch_scan')
 
     def dispatch_slots(self, packed, layout: RowLayout, num_recv, rank, num_local_experts, block_offsets, meta,
-                       inv=None, stream=None):
+                       inv=None, row_map=None, stream=None):
         """inv: optional int32 [expanded rows]: inv[slot] = row * K + lane (the expanded copy's map)."""
         _require(inv is None or (inv.dtype == torch.int32 and inv.is_contiguous()), 'inv int32')
         rc = self.lib.deepep_dispatch_slots(ptr(packed), layout.row_bytes, layout.idx_off, num_recv,
                                             layout.num_topk, rank, num_local_experts, ptr(block_offsets),
-                                            ptr(meta), ptr(inv), _stream_handle(stream))
+                                            ptr(meta), ptr(inv), ptr(row_map), _stream_handle(stream))
         _lib.check(rc, 'dispatch_slots')
 
     def dispatch_copy(self, packed, layout: RowLayout, num_recv, meta, expanded, recv_x_bytes, recv_sf_bytes,
                       recv_w, x_direct=None, sf_direct=None, num_max_tokens: int = 0, error_flag=None,
-                      inv=None, block_offsets=None, expert_end=None, stream=None):
+                      inv=None, block_offsets=None, expert_end=None, row_map=None, stream=None):
         """x_direct / sf_direct: [T, bytes] uint8 views of the sender's rows (one rank: the packed rows
         then carry only metadata and row i's x is x_direct[src_metadata[i][0] % num_max_tokens]).
         inv / block_offsets / expert_end (expanded): the blocked destination-major copy (dispatch_slots'
@@ -292,7 +299,7 @@ class HipKernels:
                                            ptr(recv_x_bytes), ptr(recv_sf_bytes), ptr(recv_w),
                                            recv_x_bytes.shape[0], ptr(inv), ptr(block_offsets), ptr(expert_end),
                                            block_offsets.shape[1] if block_offsets is not None else 0,
-                                           ptr(error_flag), _stream_handle(stream))
+                                           ptr(row_map), ptr(error_flag), _stream_handle(stream))
         _lib.check(rc, 'dispatch_copy')
 
     def combine_buffer_size(self, num_max_tokens_per_rank: int, hidden: int, num_topk: int,

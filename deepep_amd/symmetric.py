@@ -8,10 +8,11 @@ Every rank allocates one uncached device window (deepep_sym_alloc), exports it w
 HIP IPC, and opens every peer's window (deepep_sym_import); kernels then store into a
 peer's HBM over xGMI.  Layout of a window:
 
-    [0, HEADER_BYTES)        int64 flags[64 slots][64 ranks]: barrier epochs written by the peers
+    [0, 32 KiB)              int64 flags[64 slots][64 ranks]: barrier epochs written by the peers
                              (slot 0: the full barrier; slots 1..63: split barriers of pipelined phases),
-                             then int64 counters[2][64 slots]: this rank's device-side epoch counts
-    [HEADER_BYTES, ...)      data: the combine receive rows (see ElasticBuffer._combine_xgmi)
+                             then int64 counters[3][64 slots]: this rank's device-side epoch counts
+    [NOTIFY_OFFSET, HEADER_BYTES)  the notify area: slot s holds rank s's dispatch counts for this rank
+    [HEADER_BYTES, ...)      data: the dispatch's received rows / the combine receive rows
 """
 import ctypes
 from typing import Callable, List, Optional
@@ -21,7 +22,8 @@ import torch.distributed as dist
 
 from . import _lib
 
-HEADER_BYTES = 64 * 1024
+HEADER_BYTES = 1 << 20          # DEEPEP_SYM_HEADER_BYTES
+NOTIFY_OFFSET = 64 * 1024       # DEEPEP_SYM_NOTIFY_OFFSET
 
 
 class _DeviceArray:
@@ -127,6 +129,22 @@ class SymmetricBuffer:
                        'a window address or plan entry was rejected (nothing was stored through it)')
                 raise RuntimeError(f'deepep_amd: symmetric buffer {_lib.describe_error_record(rec)}: {why}; '
                                    f'the last results are invalid')
+
+    def put_notify(self, records: torch.Tensor, stream) -> None:
+        """Store records[d] (int32 [num_ranks, n], n * 4 a multiple of 16 bytes) into slot `rank` of rank d's
+        notify area (the dispatch notify's transport); a barrier must follow before it is read."""
+        assert records.dtype == torch.int32 and records.is_contiguous() and records.shape[0] == self.num_ranks
+        n = records.shape[1]
+        assert (n * 4) % 16 == 0 and self.num_ranks * n * 4 <= HEADER_BYTES - NOTIFY_OFFSET, 'notify too large'
+        handle = stream.cuda_stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        _lib.check(self.lib.deepep_sym_put(records.data_ptr(), n * 4, self.bases_dev.data_ptr(), self.num_ranks,
+                                           NOTIFY_OFFSET + self.rank * n * 4, self.error_flag.data_ptr(), handle),
+                   'sym_put')
+
+    def notify_area(self, n: int) -> torch.Tensor:
+        """This rank's notify area as int32 [num_ranks, n]: row s = what rank s put here."""
+        return torch.as_tensor(_DeviceArray(self.base + NOTIFY_OFFSET, self.num_ranks * n * 4),
+                               device=self.device).view(torch.int32).view(self.num_ranks, n)
 
     def check(self) -> None:
         """Raise if a barrier timed out or a window address was rejected (host sync)."""

@@ -223,9 +223,13 @@ int deepep_dispatch_pack(const void* x, int64_t x_row_stride_bytes, int x_bytes,
  * histograms block_counts [ceil(num_recv / DEEPEP_DISPATCH_BLOCK_ROWS)][num_local_experts]. recv_rank_psum is the
  * inclusive prefix sum of rows per source rank (device memory).  Rows from recv_rank_psum[num_ranks-1]
  * up to num_recv (a launch sized for the worst case, dispatch(do_cpu_sync=False)) get src_metadata
- * columns 0-1 = -1 and recv_topk_idx -1; passes 3 and 4 skip them. */
+ * columns 0-1 = -1 and recv_topk_idx -1; passes 3 and 4 skip them.
+ * pad_rows > 0: the packed rows come from a worst-case-sized exchange, source s's rows at s * pad_rows
+ * (not contiguous); row_map (int32 [num_recv]) then receives the packed row of every received row i,
+ * which passes 3 and 4 take as their row_map.  pad_rows 0: packed row i is row i (row_map may be NULL). */
 int deepep_dispatch_count(const void* packed, int64_t row_bytes, int idx_off, int src_off, int num_recv, int num_topk,
                           int rank, int num_local_experts, const int32_t* recv_rank_psum, int num_ranks,
+                          int pad_rows, int32_t* row_map,
                           int32_t* src_metadata, int64_t* recv_topk_idx, int32_t* block_counts,
                           deepep_stream_t stream);
 
@@ -240,7 +244,7 @@ int deepep_dispatch_scan(int32_t* block_counts, int num_blocks, int num_local_ex
  * inv[slot] = row * num_topk + lane for every slot written (alignment padding rows are not written). */
 int deepep_dispatch_slots(const void* packed, int64_t row_bytes, int idx_off, int num_recv, int num_topk,
                           int rank, int num_local_experts, const int32_t* block_offsets, int32_t* src_metadata,
-                          int32_t* inv, deepep_stream_t stream);
+                          int32_t* inv, const int32_t* row_map, deepep_stream_t stream);
 
 /* Pass 4: recv_x / recv_sf rows (row i, or every local slot when expanded) and top-k weights
  * ([num_recv][K] or, expanded, [slot]).  recv_sf / recv_topk_weights may be NULL.  With x_direct
@@ -260,7 +264,7 @@ int deepep_dispatch_copy(const void* packed, int64_t row_bytes, int x_bytes, int
                          const void* sf_direct, int64_t sf_direct_stride_bytes, int num_max_tokens,
                          void* recv_x, void* recv_sf, float* recv_topk_weights, int64_t num_out_rows,
                          const int32_t* inv, const int32_t* block_offsets, const int32_t* expert_end,
-                         int num_local_experts, int32_t* error_flag, deepep_stream_t stream);
+                         int num_local_experts, const int32_t* row_map, int32_t* error_flag, deepep_stream_t stream);
 
 /* ------------------------------------------------------------------ EP > 1 combine plan
  * The EP > 1 combine runs in pipeline chunks of source tokens: chunk c = tokens
@@ -298,12 +302,17 @@ int deepep_route_block_counts(const int64_t* topk_idx, int num_tokens, int num_t
  * a window row whose bytes do not lie inside [0, window_bytes) of its window, or metadata no correct
  * dispatch produces, gives out_rows[u] = 0 (DEEPEP_FAULT_PLAN_ROW), which the scatter skips.  Callers
  * pre-fill table_a / wtable_a with -1 and out_rows with 0, so an unwritten unit is never an address.
- * error_flag: DEEPEP_ERROR_RECORD_INTS device ints or NULL (bit 1 and the record are set on a fault). */
+ * error_flag: DEEPEP_ERROR_RECORD_INTS device ints or NULL (bit 1 and the record are set on a fault).
+ * padded_stride > 0 (a handle whose counts only the device knows: dispatch without a CPU sync): chunk c
+ * holds num_ranks * padded_stride unit positions starting at c * num_ranks * padded_stride; unit p of
+ * source s sits at s * padded_stride + p (or p * num_ranks + s with DEEPEP_PLAN_INTERLEAVE).  The positions
+ * no unit takes keep the caller's fill: -1 slots (a zero partial) and, for out_rows, the value 1, which
+ * the scatter skips silently. */
 int deepep_plan_expert(const int32_t* src_metadata, int num_recv, int num_topk, int num_ranks, int rank,
                        int num_max_tokens, const int32_t* recv_tok, const int32_t* recv_pairs, int num_blocks,
                        int blocks_per_chunk, int flags, int32_t* table_a, int32_t* wtable_a,
                        const uint64_t* window_bases, int64_t window_row_bytes, int64_t window_bytes,
-                       uint64_t* out_rows, int32_t* error_flag, deepep_stream_t stream);
+                       uint64_t* out_rows, int32_t* error_flag, int padded_stride, deepep_stream_t stream);
 
 /* Source side, per owned token t (chunk c = t / B).  Multiple reduction: table_b [T][min(R, K)] = the
  * rows of t's partials in ascending dedup-master-lane order (a rank's master is its highest top-k
@@ -312,12 +321,14 @@ int deepep_plan_expert(const int32_t* src_metadata, int num_recv, int num_topk, 
  * A row is the partial's row in chunk c's receive buffer (grouped by expert rank, ascending token:
  * dst_slot [T][R] from deepep_dispatch_route gives the rank among earlier tokens) or, with
  * DEEPEP_PLAN_WINDOW, the window row slot * num_max_tokens + t.  Single reduction: table_b [T][K] = the
- * row of (t, k): receive-buffer order (expert rank, then (token, lane)) or window row k * T_max + t. */
+ * row of (t, k): receive-buffer order (expert rank, then (token, lane)) or window row k * T_max + t.
+ * padded_stride > 0 (not with DEEPEP_PLAN_WINDOW): the receive buffer of a chunk is worst-case padded,
+ * expert rank d's rows from d * padded_stride (the plan_expert layout above, after the exchange). */
 int deepep_plan_source(const int64_t* topk_idx, int num_tokens, int num_topk, int num_experts, int num_ranks,
                        int num_max_tokens, const int32_t* dst_slot, const int32_t* send_tok,
                        const int32_t* send_pairs, int num_blocks, int blocks_per_chunk, int flags,
                        int64_t row_floats, int64_t weights_offset, int32_t* table_b, int table_b_width,
-                       int32_t* wtable, deepep_stream_t stream);
+                       int32_t* wtable, int padded_stride, deepep_stream_t stream);
 
 /* ------------------------------------------------------------------ symmetric buffer over xGMI
  * Replaces the reference's NCCLSymmetricMemoryContext (csrc/elastic/nccl.cu:62-153, buffer.hpp:181-208)
@@ -332,10 +343,24 @@ int deepep_sym_export(void* ptr, void* handle);             /* handle: DEEPEP_IP
 int deepep_sym_import(const void* handle, void** ptr);      /* a peer's window, mapped into this process */
 int deepep_sym_close(void* ptr);
 
+/* Window header, DEEPEP_SYM_HEADER_BYTES from the window base (zero at allocation): the int64 flag
+ * table [DEEPEP_SYM_FLAG_SLOTS][64], then int64 counters [3][DEEPEP_SYM_FLAG_SLOTS] (publishes, waits,
+ * workgroup arrivals), then from DEEPEP_SYM_NOTIFY_OFFSET the notify area the dispatch's counts are
+ * exchanged through (deepep_sym_put); the data region starts at DEEPEP_SYM_HEADER_BYTES. */
+#define DEEPEP_SYM_NOTIFY_OFFSET 65536
+#define DEEPEP_SYM_HEADER_BYTES 1048576
+
+/* Store src + d * bytes (bytes % 16 == 0) at dest_bases[d] + dest_offset for every d < num_ranks:
+ * system-scope write-through stores into the peers' windows (dest_bases: device uint64 [num_ranks],
+ * e.g. the window bases, so dest_offset addresses the header's notify area).  The dispatch notify's
+ * transport: rank r puts its count record for every destination into slot r of that destination's
+ * area, then a barrier makes them visible (dispatch.cuh:79-258's notify over NVLink).  Nothing is
+ * stored once bit 2 of error_flag (device int or NULL) is set. */
+int deepep_sym_put(const void* src, int64_t bytes, const uint64_t* dest_bases, int num_ranks, int64_t dest_offset,
+                   const int32_t* error_flag, deepep_stream_t stream);
+
 /* Group barrier on the stream: peer_flags (device, uint64 [num_ranks]) holds the address of every
- * rank's window header (int64 flag table [DEEPEP_SYM_FLAG_SLOTS][64], then int64 counters
- * [3][DEEPEP_SYM_FLAG_SLOTS]: publishes, waits, workgroup arrivals; DEEPEP_SYM_HEADER_BYTES in all,
- * zero at allocation).  Every XCD's L2 is first written back (the stores into peer windows before
+ * rank's window header (above).  Every XCD's L2 is first written back (the stores into peer windows before
  * the call may sit in any of them).  Rank r then stores
  * the epoch into entry [r] of slot 0 of every rank's table (system-scope release) and waits until
  * its own entries all reach it (system-scope acquire).  epoch <= 0: the next epoch is counted on
@@ -343,7 +368,6 @@ int deepep_sym_close(void* ptr);
  * for every call of a window, or host epochs (growing by one per call) for every call, not both.
  * After timeout_us (<= 0: 100 s) the wait gives up and sets bit 2 of *error_flag (comm.cuh:30-54
  * traps instead). */
-#define DEEPEP_SYM_HEADER_BYTES 65536
 int deepep_sym_barrier(const uint64_t* peer_flags, int rank, int num_ranks, int64_t epoch, int64_t timeout_us,
                        int32_t* error_flag, deepep_stream_t stream);
 
@@ -368,7 +392,8 @@ int deepep_sym_wait(const uint64_t* peer_flags, int rank, int num_ranks, int slo
  * Windows: window_bases (device uint64 [num_windows]) and window_bytes, the data extent of each.  Every
  * row is checked before it is stored: unless all its bytes (the bf16 row and, with weights, the weight
  * tail) lie inside one window, the unit is skipped, bit 4 of error_flag is set and the fault recorded
- * (DEEPEP_FAULT_SCATTER_ROW); out_rows[u] == 0 (a unit plan_expert rejected) is skipped with bit 1.
+ * (DEEPEP_FAULT_SCATTER_ROW); out_rows[u] == 0 (a unit plan_expert rejected) is skipped with bit 1,
+ * out_rows[u] == 1 (a padding position of a padded plan) silently.
  * error_flag: DEEPEP_ERROR_RECORD_INTS device ints or NULL. */
 int deepep_combine_reduce_scatter(int weighted,
                                   const void* src, int64_t num_src_rows, int64_t src_row_stride,

@@ -68,14 +68,17 @@ class OracleKernels:
 
     def plan_expert(self, meta, num_topk, num_ranks, rank, num_max_tokens, recv_tok, recv_pairs, num_blocks,
                     blocks_per_chunk, flags, table_a, wtable_a, window_bases, window_row_bytes, out_rows,
-                    window_bytes=0, error_flag=None, stream=None):
+                    window_bytes=0, error_flag=None, padded_stride=0, stream=None):
         plan_ref.plan_expert(meta, num_topk, num_ranks, rank, num_max_tokens, recv_tok, recv_pairs, num_blocks,
-                             blocks_per_chunk, flags, table_a, wtable_a, window_bases, window_row_bytes, out_rows)
+                             blocks_per_chunk, flags, table_a, wtable_a, window_bases, window_row_bytes, out_rows,
+                             padded=padded_stride)
 
     def plan_source(self, topk_idx, num_experts, num_ranks, num_max_tokens, dst_slot, send_tok, send_pairs,
-                    num_blocks, blocks_per_chunk, flags, row_floats, weights_offset, table_b, wtable, stream=None):
+                    num_blocks, blocks_per_chunk, flags, row_floats, weights_offset, table_b, wtable,
+                    padded_stride=0, stream=None):
         plan_ref.plan_source(topk_idx, num_experts, num_ranks, num_max_tokens, dst_slot, send_tok, send_pairs,
-                             num_blocks, blocks_per_chunk, flags, row_floats, weights_offset, table_b, wtable)
+                             num_blocks, blocks_per_chunk, flags, row_floats, weights_offset, table_b, wtable,
+                             padded=padded_stride)
 
     # ------------------------------------------------------------------ dispatch primitives (CPU stand-ins)
     def dispatch_route(self, topk_idx, num_experts, num_ranks, dst_slot, send_counts, stream=None):
@@ -107,22 +110,32 @@ class OracleKernels:
         packed[dest, layout.src_off:layout.src_off + 4] = src.view(torch.uint8).view(-1, 4)
 
     @staticmethod
-    def _local(packed, layout, N, rank, epr):
+    def _rows(packed, N, row_map):
+        """The packed rows of received rows 0..N-1 (a padded receive buffer reads through row_map)."""
+        return packed[:N] if row_map is None else packed[row_map[:N].long()]
+
+    @staticmethod
+    def _local(packed, layout, N, rank, epr, row_map=None):
         K = layout.num_topk
+        packed = OracleKernels._rows(packed, N, row_map)
         idx = packed[:N, layout.idx_off:layout.idx_off + 8 * K].contiguous().view(torch.int64).view(N, K)
         inr = (idx >= rank * epr) & (idx < (rank + 1) * epr)
         return torch.where(inr, idx - rank * epr, torch.full_like(idx, -1))
 
     def dispatch_count(self, packed, layout, num_recv, rank, num_local_experts, rank_psum, meta, recv_topk_idx,
-                       block_counts, stream=None):
+                       block_counts, pad_rows=0, row_map=None, stream=None):
         K, epr = layout.num_topk, num_local_experts
         N = min(num_recv, int(rank_psum[-1]))          # rows received; the rest get metadata -1
         meta[N:num_recv, :2] = -1
         if recv_topk_idx is not None:
             recv_topk_idx[N:num_recv] = -1
-        le = self._local(packed, layout, N, rank, epr)
-        src = packed[:N, layout.src_off:layout.src_off + 4].contiguous().view(torch.int32).view(N)
         src_rank = torch.searchsorted(rank_psum.to(torch.int64), torch.arange(N), right=True).clamp(max=rank_psum.numel() - 1)
+        if pad_rows:
+            start = torch.cat([torch.zeros(1, dtype=torch.int64), rank_psum.to(torch.int64)])[src_rank]
+            row_map[:N] = (src_rank * pad_rows + torch.arange(N) - start).to(torch.int32)
+        rm = row_map if pad_rows else None
+        le = self._local(packed, layout, N, rank, epr, rm)
+        src = self._rows(packed, N, rm)[:, layout.src_off:layout.src_off + 4].contiguous().view(torch.int32).view(N)
         master = torch.where(le >= 0, torch.arange(K).view(1, K), torch.full_like(le, -1)).amax(dim=1)
         meta[:N, 0] = src
         meta[:N, 1] = (src_rank * K + master).to(torch.int32)
@@ -146,8 +159,10 @@ class OracleKernels:
         psum_expert.copy_((start + counts if expanded else start + aligned).to(torch.int32))
 
     def dispatch_slots(self, packed, layout, num_recv, rank, num_local_experts, block_offsets, meta, inv=None,
-                       stream=None):
-        le = self._local(packed, layout, num_recv, rank, num_local_experts)
+                       row_map=None, stream=None):
+        n = int((meta[:num_recv, 0] >= 0).sum())         # the received rows come first
+        le = torch.full((num_recv, layout.num_topk), -1, dtype=torch.int64)
+        le[:n] = self._local(packed, layout, n, rank, num_local_experts, row_map)
         meta[:num_recv, 2:] = -1
         rows = DISPATCH_BLOCK_ROWS
         for b in range(block_offsets.shape[0]):
@@ -165,9 +180,10 @@ class OracleKernels:
 
     def dispatch_copy(self, packed, layout, num_recv, meta, expanded, recv_x_bytes, recv_sf_bytes, recv_w,
                       x_direct=None, sf_direct=None, num_max_tokens=0, error_flag=None, inv=None,
-                      block_offsets=None, expert_end=None, stream=None):
+                      block_offsets=None, expert_end=None, row_map=None, stream=None):
         K = layout.num_topk
         N = int((meta[:num_recv, 0] >= 0).sum())         # the received rows come first
+        packed = self._rows(packed, N, row_map)
         if x_direct is not None:
             t = (meta[:N, 0].long() % num_max_tokens)
             xs = x_direct[t]

@@ -45,11 +45,14 @@ def route_block_counts(topk_idx, num_experts, num_ranks, num_blocks):
     return tok.to(torch.int32), pairs.to(torch.int32)
 
 
-def _positions(unit_src, unit_chunk, counts, R, interleave):
+def _positions(unit_src, unit_chunk, counts, R, interleave, padded=0):
     """Unit index of every unit (given in receive order) inside the concatenated chunk tables:
-    chunk base + position inside the chunk (grouped by source rank, or round-robin)."""
+    chunk base + position inside the chunk (grouped by source rank, or round-robin).  padded > 0:
+    every chunk holds R * padded positions, unit p of source s at s * padded + p (p * R + s)."""
     n = unit_src.numel()                                       # counts: [chunks, R]
     base = torch.cumsum(counts.sum(dim=1), 0) - counts.sum(dim=1)
+    if padded:
+        base = torch.arange(counts.shape[0]) * R * padded
     # p = rank of the unit among the units of its (source, chunk) group, in receive order
     key = unit_chunk * R + unit_src
     order = torch.argsort(key, stable=True)
@@ -60,7 +63,9 @@ def _positions(unit_src, unit_chunk, counts, R, interleave):
     out = torch.empty(n, dtype=torch.int64)
     for i in range(n):
         c, s, pi = int(unit_chunk[i]), int(unit_src[i]), int(p[i])
-        if interleave:
+        if padded:
+            pos = pi * R + s if interleave else s * padded + pi
+        elif interleave:
             pos = sum(min(int(counts[c, l]), pi + (1 if l < s else 0)) for l in range(R))
         else:
             pos = int(counts[c, :s].sum()) + pi
@@ -69,7 +74,7 @@ def _positions(unit_src, unit_chunk, counts, R, interleave):
 
 
 def plan_expert(meta, num_topk, num_ranks, rank, num_max_tokens, recv_tok, recv_pairs, num_blocks,
-                blocks_per_chunk, flags, table_a, wtable_a, window_bases, window_row_bytes, out_rows):
+                blocks_per_chunk, flags, table_a, wtable_a, window_bases, window_row_bytes, out_rows, padded=0):
     K, R, T_max, bpc = num_topk, num_ranks, num_max_tokens, blocks_per_chunk
     single, expanded = bool(flags & SINGLE), bool(flags & EXPANDED)
     n_recv = int(recv_tok.sum())
@@ -82,7 +87,7 @@ def plan_expert(meta, num_topk, num_ranks, rank, num_max_tokens, recv_tok, recv_
     counts = torch.stack([cnt[:, c * bpc:(c + 1) * bpc].sum(dim=1) for c in range(C)])    # [C, R]
     if single:
         ii, kk = (m[:, 2:] >= 0).nonzero(as_tuple=True)         # (row, lane) order
-        u = _positions(src[ii], chunk[ii], counts, R, bool(flags & INTERLEAVE))
+        u = _positions(src[ii], chunk[ii], counts, R, bool(flags & INTERLEAVE), padded)
         table_a[u, 0] = m[ii, 2 + kk].to(torch.int32)
         if out_rows is not None:
             bases = window_bases.long().cpu()
@@ -90,7 +95,7 @@ def plan_expert(meta, num_topk, num_ranks, rank, num_max_tokens, recv_tok, recv_
             addr = bases[src[ii].clamp(0, R - 1)] + (kk * T_max + st[ii]) * window_row_bytes
             out_rows[u] = torch.where(ok, addr, torch.zeros_like(addr)).to(out_rows.dtype)
         return
-    u = _positions(src, chunk, counts, R, bool(flags & INTERLEAVE))
+    u = _positions(src, chunk, counts, R, bool(flags & INTERLEAVE), padded)
     rows = torch.arange(n_recv)
     if expanded:
         table_a[u] = m[:, 2:2 + K].to(torch.int32)
@@ -107,7 +112,7 @@ def plan_expert(meta, num_topk, num_ranks, rank, num_max_tokens, recv_tok, recv_
 
 
 def plan_source(topk_idx, num_experts, num_ranks, num_max_tokens, dst_slot, send_tok, send_pairs, num_blocks,
-                blocks_per_chunk, flags, row_floats, weights_offset, table_b, wtable):
+                blocks_per_chunk, flags, row_floats, weights_offset, table_b, wtable, padded=0):
     """Per owned token, from the routing alone (running counters, not dst_slot)."""
     T, K = topk_idx.shape
     R, T_max, bpc = num_ranks, num_max_tokens, blocks_per_chunk
@@ -130,7 +135,7 @@ def plan_source(topk_idx, num_experts, num_ranks, num_max_tokens, dst_slot, send
                 if window:
                     tb[t, k] = k * T_max + t
                 else:
-                    tb[t, k] = int(counts[c, :d].sum()) + int(running[c, d])
+                    tb[t, k] = (d * padded if padded else int(counts[c, :d].sum())) + int(running[c, d])
                     running[c, d] += 1
             continue
         master = {d: k for k, d in enumerate(ranks) if d >= 0}            # highest lane wins
@@ -139,7 +144,7 @@ def plan_source(topk_idx, num_experts, num_ranks, num_max_tokens, dst_slot, send
             if window:
                 row[d] = (d if rank_layout else mk) * T_max + t
             else:
-                row[d] = int(counts[c, :d].sum()) + int(running[c, d])
+                row[d] = (d * padded if padded else int(counts[c, :d].sum())) + int(running[c, d])
                 running[c, d] += 1
         for j, d in enumerate(sorted(master, key=lambda d: master[d])[:width]):
             tb[t, j] = row[d]

@@ -81,13 +81,15 @@ def test_invalid_arguments_are_rejected_without_a_gpu(lib):
     assert lib.deepep_set_launch_config(0, -1, -1, 0) == 0
     # EP > 1 plan builders: rank out of range, too few blocks, wrong table width, single w/o expanded
     assert lib.deepep_plan_expert(16, 4, 8, 8, 8, 64, 16, 16, 1, 1, 1, 16, None, None, 0, 0, None, None,
-                                  None) == -1
+                                  0, None) == -1
     assert b'plan_expert' in lib.deepep_amd_last_error()
     assert lib.deepep_plan_expert(16, 4, 8, 8, 0, 64, 16, 16, 1, 1, 2, 16, None, None, 0, 0, None, None,
-                                  None) == -1
-    # out_rows need window bases and an extent of at least one row
+                                  0, None) == -1
+    # out_rows need window bases and an extent of at least one row; a negative padded stride
     assert lib.deepep_plan_expert(16, 4, 8, 8, 0, 64, 16, 16, 1, 1, 1, 16, None, 32, 256, 128, 48, None,
-                                  None) == -1
+                                  0, None) == -1
+    assert lib.deepep_plan_expert(16, 4, 8, 8, 0, 64, 16, 16, 1, 1, 1, 16, None, None, 0, 0, None, None,
+                                  -1, None) == -1
     # the scatter needs its windows (bases and an extent holding a whole row)
     assert lib.deepep_combine_reduce_scatter(0, 16, 4, 64, None, 0, 1, None, 32, 4, 64, None, 0, None, 0, 0, 0,
                                              None, 1, 4096, None, None) == -1
@@ -95,8 +97,10 @@ def test_invalid_arguments_are_rejected_without_a_gpu(lib):
     assert lib.deepep_combine_reduce_scatter(0, 16, 4, 64, None, 0, 1, None, 32, 4, 64, None, 0, None, 0, 0, 0,
                                              48, 1, 64, None, None) == -1
     # dispatch pack: negative destination rows
-    assert lib.deepep_plan_source(16, 200, 8, 64, 8, 256, 16, 16, 16, 1, 1, 0, 0, 0, 16, 8, None, None) == -1
-    assert lib.deepep_plan_source(16, 64, 8, 64, 8, 256, 16, 16, 16, 1, 1, 0, 0, 0, 16, 7, None, None) == -1
+    assert lib.deepep_plan_source(16, 200, 8, 64, 8, 256, 16, 16, 16, 1, 1, 0, 0, 0, 16, 8, None, 0, None) == -1
+    assert lib.deepep_plan_source(16, 64, 8, 64, 8, 256, 16, 16, 16, 1, 1, 0, 0, 0, 16, 7, None, 0, None) == -1
+    # a padded stride with window rows (the window layout is never padded)
+    assert lib.deepep_plan_source(16, 64, 8, 64, 8, 256, 16, 16, 16, 4, 1, 16, 0, 0, 16, 8, None, 64, None) == -1
     assert lib.deepep_dispatch_pack(16, 64, 64, None, 0, 0, 32, None, 4, 2, 0, 48, 64, 2, 80, None, 128, -1,
                                     64, 64, 96, 112, None, None) == -1
     assert lib.deepep_route_block_counts(16, 200, 8, 64, 8, 1, 16, 16, None) == -1

@@ -207,6 +207,83 @@ def _sync_free_rank(rank, world, T, H, K, E, comm, results):
             comm.bar.abort()
 
 
+def _dispatch_sync_free_rank(rank, world, T, H, K, E, comm, results):
+    """A fresh dispatch(do_cpu_sync=False) and the handle's first combine, both under
+    set_sync_debug_mode('error'): the worst-case-padded RCCL exchange (equal splits, no host sizes)
+    and the padded combine plan."""
+    try:
+        torch.cuda.set_device(0)
+        from deepep_amd import ElasticBuffer
+        rng, idx_all, w_all = _routing(world, T, K, E, seed=313 + world)
+        disp = oracle.simulate_dispatch(idx_all, E, T)
+        x_all = [oracle.f32_to_bf16(rng.standard_normal((T, H)).astype(np.float32)) for _ in range(world)]
+        bias = [oracle.f32_to_bf16(rng.standard_normal((T, H)).astype(np.float32)) for _ in range(world)]
+        x_exp_all, w_exp_all = [], []
+        for d in disp:
+            xe = np.zeros((d['num_expanded'], H), np.uint16)
+            we = np.zeros((d['num_expanded'],), np.float32)
+            for row, (g, k) in enumerate(d['expanded_src']):
+                s, t = divmod(int(g), T)
+                xe[row], we[row] = x_all[s][t], w_all[s][t, k]
+            x_exp_all.append(xe), w_exp_all.append(we)
+        metas = [d['src_metadata'] for d in disp]
+        failures = []
+        for amr in (True, False):
+            expect = oracle.combine_ep(x_exp_all, metas, idx_all, E, T, expanded=True, allow_multiple_reduction=amr,
+                                       topk_weights_per_rank=w_exp_all if amr else None,
+                                       bias_per_rank=[(b, None) for b in bias])[rank]
+            buf = ElasticBuffer(FakeGroup(rank, world, comm), num_max_tokens_per_rank=T, hidden=H, num_topk=K,
+                                allow_multiple_reduction=amr)
+            comm.install(buf, rank)
+            x, b = _bf16(x_all[rank]), _bf16(bias[rank])
+            idx, w = torch.from_numpy(idx_all[rank]).cuda(), torch.from_numpy(w_all[rank]).cuda()
+            torch.cuda.synchronize()
+            comm.bar.wait()
+            if rank == 0:
+                torch.cuda.set_sync_debug_mode('error')
+            comm.bar.wait()
+            try:
+                ex_x, _, ex_w, handle, _ = buf.dispatch(x, topk_idx=idx, topk_weights=w, num_experts=E,
+                                                        do_expand=True, do_cpu_sync=False)
+                if amr:
+                    out, out_w, _ = buf.combine(ex_x, handle, topk_weights=ex_w, bias=b)
+                else:
+                    out, out_w, _ = buf.combine(ex_x, handle, bias=b)
+            finally:
+                comm.bar.wait()
+                if rank == 0:
+                    torch.cuda.set_sync_debug_mode(0)
+            torch.cuda.synchronize()
+            n = int(handle.psum_num_recv_tokens_per_scaleup_rank[-1].item())
+            meta = handle.recv_src_metadata.cpu().numpy()
+            if meta.shape[0] != world * T or not np.array_equal(meta[:n], metas[rank]) or not (meta[n:] == -1).all():
+                failures.append(f'amr={amr}: metadata')
+            if not np.array_equal(_u16(out), expect[0]):
+                failures.append(f'amr={amr}: combined_x')
+            if amr and not np.array_equal(out_w.cpu().numpy(), expect[1]):
+                failures.append(f'amr={amr}: combined_topk_weights')
+            comm.bar.wait()
+        results[rank] = failures
+    except Exception:
+        import traceback
+        results[rank] = [traceback.format_exc()]
+        if comm is not None:
+            comm.bar.abort()
+
+
+@pytest.mark.parametrize('world,T', [(4, 128), (8, 1088)])
+def test_dispatch_without_cpu_sync_ep_gt_1(world, T):
+    """EP > 1 dispatch(do_cpu_sync=False) + first combine over the (simulated) RCCL transport with no
+    host synchronisation (csrc/elastic/buffer.hpp:1065-1070); T = 1088 gives a pipelined (multi-chunk)
+    padded combine.  Bitwise vs the oracle, plain and single reduction."""
+    H, K, E = 256, 8, 64
+    comm = ThreadComm(world)
+    results = run_threads(world, _dispatch_sync_free_rank, (world, T, H, K, E, comm))
+    assert len(results) == world, results
+    bad = {r: f for r, f in results.items() if f}
+    assert not bad, bad
+
+
 @pytest.mark.parametrize('world,T', [(1, 1024), (4, 1024), (8, 1088)])
 def test_first_combine_has_no_host_sync(world, T):
     """Fresh dispatch, then the handle's FIRST combine (plan built on the device, pipelined exchange at

@@ -380,6 +380,134 @@ def test_xgmi_transport_matches_oracle(world, T, H, K, empty_rank, chunks):
         pytest.fail(f'{len(results)}/{world} ranks reported; failures: {tails}', pytrace=False)
 
 
+def _sync_free_worker(rank, world, port, T, H, K, chunks, queue):
+    """dispatch(do_cpu_sync=False) + the handle's first combine over xGMI, with no host sync: the notify
+    goes through the windows, every launch is sized for the worst case and bounded on the device, the
+    combine plan is worst-case padded.  Run under set_sync_debug_mode('error') and, on a second buffer,
+    captured whole into one HIP graph (no eager call before it) and replayed; bitwise vs the oracle."""
+    sys.path.insert(0, ROOT)
+    try:
+        os.environ['MASTER_ADDR'] = '127.0.0.1'
+        os.environ['MASTER_PORT'] = str(port)
+        os.environ['DEEPEP_TRANSPORT'] = 'xgmi'
+        if chunks:
+            os.environ['DEEPEP_COMBINE_CHUNKS'] = str(chunks)
+        import torch.distributed as dist
+        torch.cuda.set_device(0)
+        dist.init_process_group('gloo', rank=rank, world_size=world)
+        import oracle
+        from deepep_amd import ElasticBuffer
+        dev = torch.device('cuda', 0)
+        E = 8 * world
+        rng = np.random.default_rng(700 + world)
+        idx_all = []
+        for r in range(world):
+            idx = np.array([rng.permutation(E)[:K] for _ in range(T)], dtype=np.int64).reshape(T, K)
+            idx[rng.random((T, K)) < 0.15] = -1
+            idx[0] = -1                                   # a token routed nowhere
+            idx_all.append(idx)
+        w_all = [rng.random((T, K)).astype(np.float32) * (i >= 0) for i in idx_all]
+        x_all = [oracle.f32_to_bf16(rng.standard_normal((T, H)).astype(np.float32)) for _ in range(world)]
+        b_all = [oracle.f32_to_bf16(rng.standard_normal((T, H)).astype(np.float32)) for _ in range(world)]
+        disp = oracle.simulate_dispatch(idx_all, E, T)
+        # the combine reduces the dispatched rows themselves (expert outputs = their inputs)
+        x_exp_all, w_exp_all = [], []
+        for d in disp:
+            xe = np.zeros((d['num_expanded'], H), np.uint16)
+            we = np.zeros((d['num_expanded'],), np.float32)
+            for row, (g, k) in enumerate(d['expanded_src']):
+                s, t = divmod(int(g), T)
+                xe[row], we[row] = x_all[s][t], w_all[s][t, k]
+            x_exp_all.append(xe), w_exp_all.append(we)
+        expect = oracle.combine_ep(x_exp_all, [d['src_metadata'] for d in disp], idx_all, E, T, expanded=True,
+                                   topk_weights_per_rank=w_exp_all,
+                                   bias_per_rank=[(b, None) for b in b_all])[rank]
+        x, bias = _bf16(x_all[rank], dev), _bf16(b_all[rank], dev)
+        idx, w = torch.from_numpy(idx_all[rank]).to(dev), torch.from_numpy(w_all[rank]).to(dev)
+        failures = []
+
+        def step(buf):
+            ex_x, _, ex_w, handle, _ = buf.dispatch(x, topk_idx=idx, topk_weights=w, num_experts=E, do_expand=True,
+                                                    do_cpu_sync=False)
+            out, out_w, _ = buf.combine(ex_x, handle, topk_weights=ex_w, bias=bias)
+            return out, out_w, handle
+
+        def check(tag, out, out_w, handle):
+            n = int(handle.psum_num_recv_tokens_per_scaleup_rank[-1].item())
+            meta = handle.recv_src_metadata.cpu().numpy()
+            if handle.recv_src_metadata.shape[0] != world * T or not (meta[n:] == -1).all():
+                failures.append(f'{tag}: metadata is not worst-case shaped')
+            if not np.array_equal(meta[:n], disp[rank]['src_metadata']):
+                failures.append(f'{tag}: recv_src_metadata differs from the oracle dispatch')
+            if not np.array_equal(_u16(out), expect[0]):
+                failures.append(f'{tag}: combined_x differs from the oracle')
+            if not np.array_equal(out_w.cpu().numpy(), expect[1]):
+                failures.append(f'{tag}: combined_topk_weights differ from the oracle')
+
+        buf = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=T, hidden=H, num_topk=K,
+                            explicitly_destroy=True, num_gpu_timeout_secs=30)
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.set_sync_debug_mode('error')
+        try:
+            out, out_w, handle = step(buf)
+        finally:
+            torch.cuda.set_sync_debug_mode(0)
+        torch.cuda.synchronize()
+        check('sync-debug', out, out_w, handle)
+        buf._sym.check()
+        # the whole dispatch + first combine captured (plans and window traffic inside the graph)
+        gbuf = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=T, hidden=H, num_topk=K,
+                             explicitly_destroy=True, num_gpu_timeout_secs=30)
+        torch.cuda.synchronize()
+        dist.barrier()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            g_out, g_w, g_handle = step(gbuf)
+        for it in range(2):
+            g_out.zero_()
+            torch.cuda.synchronize()
+            dist.barrier()
+            graph.replay()
+            torch.cuda.synchronize()
+            check(f'graph replay {it}', g_out, g_w, g_handle)
+        del graph
+        gbuf._sym.check()
+        for b in (buf, gbuf):
+            b.destroy()
+        queue.put((rank, failures))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:
+        queue.put((rank, [traceback.format_exc()]))
+
+
+@pytest.mark.parametrize('world,T,H,K,chunks', [(4, 64, 512, 8, 2), (8, 40, 256, 8, 0)])
+def test_xgmi_dispatch_without_cpu_sync_then_combine(world, T, H, K, chunks):
+    """EP > 1 without any host synchronisation (the reference's do_cpu_sync=False,
+    csrc/elastic/buffer.hpp:1065-1070): processes sharing the GPU over HIP-IPC windows."""
+    ctx = mp.get_context('spawn')
+    queue = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sync_free_worker, args=(r, world, port, T, H, K, chunks, queue))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    results = {}
+    try:
+        for _ in range(world):
+            rank, failures = queue.get(timeout=150)
+            results[rank] = failures
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    if len(results) != world or any(results.values()):
+        tails = {r: [f[-1500:] for f in fl] for r, fl in results.items()}
+        pytest.fail(f'{len(results)}/{world} ranks reported; failures: {tails}', pytrace=False)
+
+
 def test_lost_peer_times_out_instead_of_hanging():
     """Failure detection (comm.cuh:30-54, num_gpu_timeout_secs): rank 0 of a 2-rank window whose
     peer never arrives.  The device barrier and the split-barrier wait give up after the timeout,

@@ -254,3 +254,64 @@ def combine_ep(recv_x_per_rank: Sequence[np.ndarray], src_metadata_per_rank: Seq
                              rank_layout, dedup, b0, b1)
         results.append((out, out_w))
     return results
+
+
+def _split_rows(n: int, parts: int):
+    step = max(1, -(-n // max(1, parts)))
+    return [(lo, min(n, lo + step)) for lo in range(0, n, step)]
+
+
+def combine_ep_one(rank: int, recv_x_per_rank: Sequence[np.ndarray], src_metadata_per_rank: Sequence[np.ndarray],
+                   topk_idx: np.ndarray, num_experts: int, num_max_tokens: int, expanded: bool,
+                   allow_multiple_reduction: bool = True,
+                   topk_weights_per_rank: Optional[Sequence[np.ndarray]] = None,
+                   bias: Tuple[Optional[np.ndarray], Optional[np.ndarray]] = (None, None),
+                   weighted: bool = False, threads: int = 1) -> Tuple[np.ndarray, Optional[np.ndarray]]:
+    """combine_ep for ONE source rank: only the received rows whose source is `rank` are reduced (phase A
+    on every expert rank), only `rank`'s receive buffer is filled and reduced (phase B).  The same
+    arithmetic as combine_ep (same C kernels); phase A and phase B are split over `threads` host threads
+    (the ctypes calls release the GIL), so a full-size rank (8192 tokens x 7168 x top-8) is checked in
+    seconds.  topk_idx: this rank's [T, K] routing."""
+    from concurrent.futures import ThreadPoolExecutor
+    R = len(recv_x_per_rank)
+    K = topk_idx.shape[1]
+    hidden = recv_x_per_rank[0].shape[1]
+    rank_layout = use_rank_layout(allow_multiple_reduction, R, K)
+    assert not (expanded and not allow_multiple_reduction), 'the single reduction is checked by combine_ep'
+    num_slots = min(R, K) if rank_layout else K
+    recv = np.zeros((num_slots, num_max_tokens, hidden), dtype=np.uint16)
+    with_w = topk_weights_per_rank is not None
+    recv_w = np.zeros((num_slots, num_max_tokens, K), dtype=np.float32) if with_w else None
+    with ThreadPoolExecutor(max_workers=max(1, threads)) as pool:
+        for r in range(R):
+            meta = np.asarray(src_metadata_per_rank[r], dtype=np.int32)
+            mine = np.nonzero(meta[:, 1] // K == rank)[0] if meta.shape[0] else np.zeros(0, np.int64)
+            if mine.size == 0:
+                continue
+            m = np.ascontiguousarray(meta[mine])
+            x = np.asarray(recv_x_per_rank[r], dtype=np.uint16)
+            w = topk_weights_per_rank[r] if with_w else None
+            parts = list(pool.map(lambda lh: phase_a(x, m[lh[0]:lh[1]], K, expanded, w, weighted=weighted),
+                                  _split_rows(m.shape[0], threads)))
+            partial = np.concatenate([p[0] for p in parts])
+            tok = m[:, 0] % num_max_tokens
+            slot = np.full(m.shape[0], r) if rank_layout else m[:, 1] % K
+            recv[slot, tok] = partial
+            if with_w:
+                recv_w[slot, tok] = np.concatenate([p[1] for p in parts])
+    idx = np.asarray(topk_idx, dtype=np.int64)
+    T = idx.shape[0]
+    b0, b1 = bias
+    out = np.zeros((T, hidden), dtype=np.uint16)
+    out_w = np.zeros((T, K), dtype=np.float32) if with_w else None
+
+    def part_b(lh):
+        lo, hi = lh
+        o, ow = phase_b(recv[:, lo:hi], recv_w[:, lo:hi] if with_w else None, idx[lo:hi], num_experts, R, rank_layout,
+                        True, None if b0 is None else b0[lo:hi], None if b1 is None else b1[lo:hi])
+        out[lo:hi] = o
+        if with_w:
+            out_w[lo:hi] = ow
+    with ThreadPoolExecutor(max_workers=max(1, threads)) as pool:
+        list(pool.map(part_b, _split_rows(T, threads)))
+    return out, out_w

@@ -151,6 +151,13 @@ class ElasticBuffer(ExchangeMixin):
         _assert(self.transport in ('rccl', 'xgmi'), 'DEEPEP_TRANSPORT must be rccl or xgmi')
         # xGMI combine: CUs for phase A while phase B of earlier chunks runs (0 = the whole chip)
         self.phase_a_cus = int(os.environ.get('DEEPEP_PHASE_A_CUS', 0))
+        # CU footprint of a combine called with num_sms=0: 'chip' (default) takes the whole GPU -- the
+        # combine is HBM-bound on MI355X, so confining it only slows it; 'handle' is the reference's
+        # default: prefer_overlap_with_compute confines the combine to handle.num_sms (its bandwidth
+        # model, elastic.py:1086 -> combine_impl's grid, combine.hpp:135) and leaves the rest of the
+        # CUs to overlapping compute.  DEEPEP_COMBINE_CUS=handle selects it for every buffer.
+        self.combine_cu_mode = os.environ.get('DEEPEP_COMBINE_CUS', 'chip')
+        _assert(self.combine_cu_mode in ('chip', 'handle'), 'DEEPEP_COMBINE_CUS must be chip or handle')
         self._sym = None
         self._sym_gen = None
         self._old_sym_gens = set()
@@ -751,6 +758,8 @@ class ElasticBuffer(ExchangeMixin):
         legacy low_latency_combine, csrc/kernels/legacy/internode_ll.cu:1072-1135).  Requires
         the expanded layout and `topk_weights`.  The weights are still passed through."""
         explicit_sms = num_sms
+        if num_sms == 0 and self.combine_cu_mode == 'handle' and self.prefer_overlap_with_compute:
+            explicit_sms = handle.num_sms          # the reference's SM-confined default (elastic.py:1086)
         num_sms = handle.num_sms if num_sms == 0 else num_sms
         num_qps = self.get_theoretical_num_qps(num_sms) if num_qps == 0 else num_qps
         _assert(num_qps <= self.num_allocated_qps, 'Allocated QPs are not enough')

@@ -947,6 +947,9 @@ int launch_combine(int mode, int weighted, const Params& p_in, deepep_stream_t s
     auto launch_choice = [&](int c) {
         p.xcd_blocks = c == 4 ? 1 : 0;
         p.cap_cus = (c == 0 || c == 4 || c == 6) ? 0 : (budget > 0 ? budget : (c == 5 ? device_cus() : 0));
+        // the persistent item grid exists for 8 rows in flight only (launch_shape): a capped launch always
+        // takes it, so a forced choice 5 never silently runs the full grid
+        if (p.cap_cus > 0 && (c == 0 || c == 4 || c == 5 || c == 6)) sh.group = 8;
         // a persistent grid stages slots per wave (no workgroup barrier between a wave's items), so
         // each wave streams at its own pace
         sh.lds = g_config.stage_lds >= 0 ? g_config.stage_lds != 0 : p.cap_cus == 0;

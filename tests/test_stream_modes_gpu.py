@@ -193,3 +193,70 @@ def test_cu_budget_is_honoured_and_bitwise(num_sms, expect_cus):
     torch.cuda.synchronize()
     assert torch.equal(out, ref) and torch.equal(out_w, ref_w)
     assert torch.equal(out2, ref) and torch.equal(out2_w, ref_w)
+
+
+@pytest.mark.parametrize('world', [1, 4])
+def test_reference_cu_confined_default_is_bitwise(monkeypatch, world):
+    """DEEPEP_COMBINE_CUS=handle: a combine called with num_sms=0 runs on a stream confined to the
+    handle's num_sms (the reference's bandwidth-model default, elastic.py:1086 -> combine_impl's grid,
+    combine.hpp:135), bitwise equal to the whole-chip default.  EP = 1's model value is the whole
+    chip, so the handle's value is lowered to 16 there; EP = 4 keeps the model's value."""
+    from deepep_amd import ElasticBuffer
+    from tests.sim import FakeGroup, ThreadComm
+    import torch.distributed as dist
+    T, H, K, E = 256, 1024, 8, 64
+    monkeypatch.setenv('DEEPEP_COMBINE_CUS', 'bogus')
+    if world == 1:
+        if not dist.is_initialized():
+            os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+            os.environ.setdefault('MASTER_PORT', '29567')
+            dist.init_process_group('gloo', rank=0, world_size=1)
+        with pytest.raises(RuntimeError):
+            ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=T, hidden=H, num_topk=K)
+    monkeypatch.setenv('DEEPEP_COMBINE_CUS', 'handle')
+    comm = ThreadComm(world) if world > 1 else None
+    if world == 1 and not dist.is_initialized():
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        os.environ.setdefault('MASTER_PORT', '29567')
+        dist.init_process_group('gloo', rank=0, world_size=1)
+    results = {}
+
+    def rank_fn(rank):
+        try:
+            torch.cuda.set_device(0)
+            g = torch.Generator(device='cuda').manual_seed(100 + rank)
+            w, idx = torch.topk(torch.rand((T, E), device='cuda', generator=g), K, dim=-1, sorted=False)
+            grp = FakeGroup(rank, world, comm) if world > 1 else dist.group.WORLD
+            bufs = {}
+            for mode in ('chip', 'handle'):
+                bufs[mode] = ElasticBuffer(grp, num_max_tokens_per_rank=T, hidden=H, num_topk=K)
+                bufs[mode].combine_cu_mode = mode          # what DEEPEP_COMBINE_CUS sets at construction
+                if comm is not None:
+                    comm.install(bufs[mode], rank)
+            _, _, ex_w, handle, _ = bufs['chip'].dispatch(torch.zeros((T, H), dtype=torch.bfloat16, device='cuda'),
+                                                         topk_idx=idx.to(torch.int64), topk_weights=w, num_experts=E,
+                                                         do_expand=True)
+            if world == 1:
+                handle.num_sms = 16
+            y = torch.randn((handle.num_expanded_tokens, H), device='cuda', generator=g).to(torch.bfloat16)
+            outs = {m: b.combine(y, handle, topk_weights=ex_w, apply_topk_weights=True) for m, b in bufs.items()}
+            torch.cuda.synchronize()
+            fails = []
+            if not (torch.equal(outs['chip'][0], outs['handle'][0]) and torch.equal(outs['chip'][1], outs['handle'][1])):
+                fails.append('confined combine differs')
+            cus = torch.cuda.get_device_properties(0).multi_processor_count
+            if handle.num_sms < cus and bufs['handle']._cu_budget_stream(handle.num_sms) is None:
+                fails.append('no budget stream for the handle num_sms')
+            results[rank] = fails
+        except Exception:
+            import traceback
+            results[rank] = [traceback.format_exc()]
+            if comm is not None:
+                comm.bar.abort()
+
+    threads = [threading.Thread(target=rank_fn, args=(r,)) for r in range(world)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=160)
+    assert len(results) == world and not any(results.values()), results

@@ -324,12 +324,12 @@ def _bench_single(y, handle, ex_w, weighted, total_bytes, steps, warmup, dev, re
         el = vmax(time.perf_counter() - t0)
         entry = dict(value=round(total_bytes * steps / el / 1e9, 2), ms_per_step=round(el * 1e3 / steps, 4))
         if transport == 'rccl':
-            sb._phase_events = []
+            sb._phase_events, sb._phase_unpipelined = [], True          # one chunk: the exchange separable
             n_ph = max(5, steps // 2)
             for _ in range(n_ph):
                 step()
             torch.cuda.synchronize()
-            ev, sb._phase_events = sb._phase_events, None
+            ev, sb._phase_events, sb._phase_unpipelined = sb._phase_events, None, False
             t_a = vmax(sum(ev[4 * i].elapsed_time(ev[4 * i + 1]) for i in range(n_ph)) / n_ph)
             t_x = vmax(sum(ev[4 * i + 1].elapsed_time(ev[4 * i + 2]) for i in range(n_ph)) / n_ph)
             t_b = vmax(sum(ev[4 * i + 2].elapsed_time(ev[4 * i + 3]) for i in range(n_ph)) / n_ph)
@@ -348,6 +348,14 @@ def _bench_single(y, handle, ex_w, weighted, total_bytes, steps, warmup, dev, re
                    '(weighted: legacy low-latency fma chain), one reduce there; reduce_only = algorithmic bytes '
                    'of all ranks / phase B (max over ranks)')
     return res
+
+
+def _pmc_entry(workload: str) -> dict:
+    try:
+        with open(os.path.join(ROOT, 'profiles', 'pmc_traffic.json')) as f:
+            return json.load(f).get(workload) or {}
+    except (OSError, ValueError):
+        return {}
 
 
 def _pmc_traffic(workload: str, build_id: str):
@@ -577,14 +585,26 @@ def main():
 
     phases = su_line = None
     if world > 1:
-        # Per-phase device time of the EP > 1 combine (phase A | exchange | phase B), same step
-        buf._phase_events = []
         n_ph = max(5, args.steps // 2)
-        for _ in range(n_ph):
-            step()
-        torch.cuda.synchronize()
-        ev = buf._phase_events
-        buf._phase_events = None
+
+        def phase_events(unpipelined: bool):
+            buf._phase_events, buf._phase_unpipelined = [], unpipelined
+            for _ in range(n_ph):
+                step()
+            torch.cuda.synchronize()
+            ev, buf._phase_events, buf._phase_unpipelined = buf._phase_events, None, False
+            return ev
+        # Phase kernels timed INSIDE the pipelined step (`value`'s schedule): per call, the events around
+        # every chunk's phase-A launch (on the phase-A stream), then around every chunk's phase B
+        n_chunks = buf._num_chunks(handle)
+        ev = phase_events(False)
+        per = 4 * n_chunks
+        t_a_pipe = sum(ev[per * i + 2 * c].elapsed_time(ev[per * i + 2 * c + 1])
+                       for i in range(n_ph) for c in range(n_chunks)) / n_ph
+        t_b_pipe = sum(ev[per * i + 2 * n_chunks + 2 * c].elapsed_time(ev[per * i + 2 * n_chunks + 2 * c + 1])
+                       for i in range(n_ph) for c in range(n_chunks)) / n_ph
+        # ... and the same step unpipelined (one chunk), which separates the exchange
+        ev = phase_events(True)
         t_a = sum(ev[4 * i].elapsed_time(ev[4 * i + 1]) for i in range(n_ph)) / n_ph
         t_x = sum(ev[4 * i + 1].elapsed_time(ev[4 * i + 2]) for i in range(n_ph)) / n_ph
         t_b = sum(ev[4 * i + 2].elapsed_time(ev[4 * i + 3]) for i in range(n_ph)) / n_ph
@@ -596,15 +616,27 @@ def main():
         n_recv = sum(handle._recv_counts)
         n_rows = int((handle.recv_src_metadata[:n_recv, 2:] >= 0).sum().item())
         a_bytes = n_rows * H * 2 + n_recv * (H * 2 + K * 4)
-        a_rate = torch.tensor([a_bytes / (t_a * 1e-3) / 1e9], dtype=torch.float64, device=dev)
+        # worst rank of the phase-A rate inside the pipelined step (all chunks' launches) and unpipelined
+        a_rate = torch.tensor([a_bytes / (t_a_pipe * 1e-3) / 1e9, a_bytes / (t_a * 1e-3) / 1e9], dtype=torch.float64,
+                              device=dev)
         dist.all_reduce(a_rate, op=dist.ReduceOp.MIN)
-        a_rate = float(a_rate.item())
+        a_rate, a_rate_unpiped = float(a_rate[0]), float(a_rate[1])
+        build_id = buf.kernels.lib.deepep_amd_build_id().decode()
+        # measured HBM bytes of the same phase-A launch (tools/pmc_ep.py: bench.py's inputs at EP = N, ranks
+        # simulated on one GPU, the same kernels), accepted only from this build
+        traffic, traffic_build, traffic_note = _pmc_traffic(f'phase_a_ep{world}_t{T}_h{H}_k{K}', build_id)
+        pmc_algo = _pmc_entry(f'phase_a_ep{world}_t{T}_h{H}_k{K}').get('algorithmic_bytes_per_launch')
         roofline = dict(bound='hbm', achieved=round(a_rate, 1), peak=HBM_PEAK_GBPS, unit='GB/s',
-                        frac=round(a_rate / HBM_PEAK_GBPS, 4), traffic=None,
+                        frac=round(a_rate / HBM_PEAK_GBPS, 4), traffic=traffic, traffic_build_id=traffic_build,
+                        traffic_note=traffic_note, traffic_algorithmic_bytes_per_launch=pmc_algo, build_id=build_id,
                         kernel='combine_rows_kernel<LOCAL> (phase A)', bytes_per_launch=a_bytes,
-                        kernel_us=round(t_a * 1e3, 2),
-                        note='worst rank; unpipelined phase-A launch timed with HIP events; the end-to-end step '
-                             'is bound by the xGMI exchange (see phases, DESIGN.md section 5)')
+                        kernel_us=round(t_a_pipe * 1e3, 2), pipeline_chunks=n_chunks,
+                        achieved_unpipelined=round(a_rate_unpiped, 1), kernel_us_unpipelined=round(t_a * 1e3, 2),
+                        note='worst rank; phase A = the sum of its per-chunk launches inside the pipelined step, '
+                             'timed with HIP events on the phase-A stream (achieved_unpipelined: the same step '
+                             'with one chunk); traffic: mean PMC bytes of one rank\'s phase-A launch of this '
+                             'workload (traffic_algorithmic_bytes_per_launch its algorithmic bytes); the '
+                             'end-to-end step is bound by the xGMI exchange (see phases, DESIGN.md section 5)')
         vals = torch.tensor([t_a + t_b, t_x, t_a, t_b], dtype=torch.float64, device=dev)
         dist.all_reduce(vals, op=dist.ReduceOp.MAX)
         xb = torch.tensor([float(x_bytes)], dtype=torch.float64, device=dev)
@@ -622,12 +654,16 @@ def main():
                             'pipelined combine step (RCCL transport, the main loop), gbps_per_rank_phase_a_exchange '
                             'the unpipelined phase A + exchange (the analogue of combine_impl, which the reference '
                             'times); min over ranks')
+        pipe = torch.tensor([t_a_pipe, t_b_pipe], dtype=torch.float64, device=dev)
+        dist.all_reduce(pipe, op=dist.ReduceOp.MAX)
         phases = dict(phase_a_ms=round(float(vals[2]), 4), exchange_ms=round(float(vals[1]), 4),
                       phase_b_ms=round(float(vals[3]), 4),
+                      pipelined_phase_a_ms=round(float(pipe[0]), 4), pipelined_phase_b_ms=round(float(pipe[1]), 4),
                       reduce_only_gbps=round(total_bytes / (float(vals[0]) * 1e-3) / 1e9, 1),
                       exchange_gbps_per_rank=round(float(xb.item()) / world / (float(vals[1]) * 1e-3) / 1e9, 1),
                       pipeline_chunks=buf._num_chunks(handle), transport=buf.transport,
-                      note='phases measured unpipelined (1 chunk); `value` runs pipeline_chunks chunks; max over ranks; reduce_only = algorithmic bytes of all ranks / (phase A + phase B); '
+                      note='phase_*_ms / exchange_ms: the step unpipelined (1 chunk); pipelined_phase_*_ms: the sum of the '
+                           'per-chunk launches inside the pipelined step (`value`); max over ranks; reduce_only = algorithmic bytes of all ranks / (phase A + phase B); '
                            'exchange = off-rank partial rows + weights / exchange time, per rank')
 
     xgmi = None

@@ -145,6 +145,7 @@ class ElasticBuffer(ExchangeMixin):
         self._kernels = None
         self.runtime = self           # non-None while alive (the reference keeps its C++ runtime here)
         self._phase_events = None     # optional list: bench instrumentation of the EP > 1 phases
+        self._phase_unpipelined = False   # bench: instrumented calls run one chunk (phases not overlapped)
         # EP > 1 combine transport: 'rccl' (all-to-all of packed partial rows, the default) or 'xgmi'
         # (phase A stores straight into the owners' symmetric windows, deepep_amd/symmetric.py)
         self.transport = os.environ.get('DEEPEP_TRANSPORT', 'rccl')
@@ -685,8 +686,8 @@ class ElasticBuffer(ExchangeMixin):
 
     def _num_chunks(self, handle: EPHandle) -> int:
         """Pipeline depth of the EP > 1 combine: DEEPEP_COMBINE_CHUNKS, else 4 for batches of at
-        least 1024 tokens per rank (1 when phase instrumentation is on or on the CPU)."""
-        if self.num_ranks == 1 or self._phase_events is not None:
+        least 1024 tokens per rank (1 on the CPU, or when the bench asks for unpipelined phases)."""
+        if self.num_ranks == 1 or (self._phase_events is not None and self._phase_unpipelined):
             return 1
         env = os.environ.get('DEEPEP_COMBINE_CHUNKS')
         if env:

@@ -65,6 +65,16 @@ for step in "$@"; do
                     $(find $OUT/pmc_FETCH_SIZE $OUT/pmc_WRITE_SIZE $OUT/pmc_TCC_EA0_RDREQ_sum $OUT/pmc_TCC_EA0_WRREQ_sum -name '*counter_collection.csv')
                 cp profiles/pmc_traffic.json $OUT/pmc_traffic.json ;;
         benchjson) run bench 600 python bench.py && grep '^{' $OUT/bench.log | tail -1 > $OUT/bench.json ;;
+        pmcep)  # phase A of the EP = N combine (bench.py's inputs, ranks simulated on one GPU): PMC passes, folded
+                # into profiles/pmc_traffic.json so an N > 1 bench line of this build carries measured traffic
+                for n in 2 4 8; do
+                    for c in FETCH_SIZE WRITE_SIZE; do
+                        run pmcep${n}_$c 300 timeout -s KILL 240 rocprofv3 --pmc $c -d $OUT/pmcep${n}_$c -o pmc --output-format csv -- python3 tools/pmc_ep.py $n
+                    done
+                    run pmcepfold$n 120 python tools/summarize_prof.py ep profiles/pmc_traffic.json $OUT/pmc_ep${n}_meta.json \
+                        $(find $OUT/pmcep${n}_FETCH_SIZE $OUT/pmcep${n}_WRITE_SIZE -name '*counter_collection.csv')
+                done
+                cp profiles/pmc_traffic.json $OUT/pmc_traffic.json ;;
         pmcphases) for c in FETCH_SIZE WRITE_SIZE; do
                     run pmcph_$c 300 timeout -s KILL 120 rocprofv3 --pmc $c -d $OUT/pmcph_$c -o pmc --output-format csv -- python3 tools/pmc_phases.py
                 done ;;

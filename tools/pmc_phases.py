@@ -52,10 +52,12 @@ def main():
     xb = x.view(torch.uint8).view(T, H * 2)
     recv_x = torch.empty_like(ex_x)
     recv_w = torch.zeros((ex_x.shape[0],), dtype=torch.float32, device='cuda')
+    inv, block_offsets = handle._copy_tables           # the product's blocked destination-major copy
     for _ in range(3):
         flush.zero_()
         kern.dispatch_copy(packed, layout, T, meta, True, recv_x.view(torch.uint8), None, recv_w, x_direct=xb,
-                           num_max_tokens=T)
+                           num_max_tokens=T, inv=inv, block_offsets=block_offsets,
+                           expert_end=handle.psum_num_recv_tokens_per_expert)
     meta_out['copy'] = T * H * 2 + ex_x.shape[0] * H * 2
     # ---- EP = 8, rank 0's phases (tools/kphase.py)
     epr = E // R

@@ -68,7 +68,7 @@ def pmc_phases(out, meta_json, *paths):
     def kind(name):
         # the dispatch copy is `copy_kernel(...)`; torch's dtype conversions (`..._copy_kernel_cuda`) also
         # contain the substring, and counting them as the copy gave round 1's "anomaly"
-        if name.startswith('copy_kernel('):
+        if name.startswith('copy_kernel(') or name.startswith('copy_expanded_kernel<'):
             return 'copy'
         if 'combine_rows_kernel<2' in name:
             return 'fused'
@@ -100,8 +100,41 @@ def pmc_phases(out, meta_json, *paths):
     print(json.dumps(res, indent=1))
 
 
+def pmc_ep(out, meta_json, *paths):
+    """Phase A (combine_rows_kernel<0,...>) HBM bytes of tools/pmc_ep.py's EP = N run (every rank's
+    launches; the kernels are serialised under --pmc), 2 x FETCH_SIZE + WRITE_SIZE (KiB) as in pmc(),
+    against the mean algorithmic bytes per launch bench.py's N > 1 roofline uses; folded into `out`
+    (profiles/pmc_traffic.json) as phase_a_ep{N}_t{T}_h{H}_k{K}, with this build's id."""
+    meta = json.load(open(meta_json))
+    per = defaultdict(list)
+    for p in paths:
+        for r in csv.DictReader(open(p)):
+            name = r.get('Kernel_Name', '').replace('(anonymous namespace)::', '').lstrip()
+            if 'combine_rows_kernel<0' in name:
+                per[r['Counter_Name']].append(float(r['Counter_Value']))
+    avg = {c: sum(v) / len(v) for c, v in per.items()}
+    algo = sum(meta['a_bytes']) / len(meta['a_bytes'])
+    key = f"phase_a_ep{meta['world']}_t{meta['tokens']}_h{meta['hidden']}_k{meta['topk']}"
+    entry = {'counters_avg_per_launch': avg, 'algorithmic_bytes_per_launch': algo, 'build_id': _build_id(),
+             'launches': {c: len(v) for c, v in per.items()}, 'source': 'tools/pmc_ep.py (ranks simulated on one GPU)'}
+    if 'FETCH_SIZE' in avg and 'WRITE_SIZE' in avg:
+        entry['hbm_read_bytes_per_launch'] = 2 * avg['FETCH_SIZE'] * 1024
+        entry['hbm_write_bytes_per_launch'] = avg['WRITE_SIZE'] * 1024
+        entry['hbm_bytes_per_launch'] = entry['hbm_read_bytes_per_launch'] + entry['hbm_write_bytes_per_launch']
+        entry['traffic_over_algorithmic'] = entry['hbm_bytes_per_launch'] / algo
+    try:
+        data = json.load(open(out))
+    except (OSError, ValueError):
+        data = {}
+    data[key] = entry
+    json.dump(data, open(out, 'w'), indent=1, sort_keys=True)
+    print(json.dumps({key: entry}, indent=1))
+
+
 if __name__ == '__main__':
-    if sys.argv[1] == 'phases':
+    if sys.argv[1] == 'ep':
+        pmc_ep(sys.argv[2], sys.argv[3], *sys.argv[4:])
+    elif sys.argv[1] == 'phases':
         pmc_phases(sys.argv[2], sys.argv[3], *sys.argv[4:])
     elif sys.argv[1] == 'stats':
         stats(sys.argv[2], sys.argv[3])

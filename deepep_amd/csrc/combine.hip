@@ -169,6 +169,9 @@ constexpr int kAuxNT = 2, kAuxSC1 = 16;      // (sc0 = 1)
 // (sc0 sc1): they must be visible to another GPU once the kernel has completed, whatever MTYPE the
 // importing process maps the window with.  Same speed as sc1 (tools/probe_ld.hip).
 constexpr int kAuxSys = 17;
+// Write-through streaming (sc1 nt): what the dispatch's blocked expanded copy stores with (dispatch.hip);
+// a launch-config option here (store_policy 3), measured against sc1 in tools/kbisect.py.
+constexpr int kAuxSC1NT = 18;
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void* row, int bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(row), 0, bytes, 0x00020000);
@@ -638,6 +641,11 @@ template <int kMode, bool kWeighted, int kVPT, bool kFull, int kAux>
 void launch_lds(const Params& p, bool lds, int waves, int group, hipStream_t stream) {
     const int nvec = p.hidden / 8;
     const int64_t items = static_cast<int64_t>(p.num_units) * ((nvec + 64 * kVPT - 1) / (64 * kVPT));
+    if constexpr (kAux == kAuxSC1NT) {          // the two default shapes only (fused / epilogue, phase A)
+        if (waves == 8) launch_shape<kMode, kWeighted, kVPT, kFull, kAux, true, 8, 8>(p, items, stream);
+        else launch_shape<kMode, kWeighted, kVPT, kFull, kAux, true, 4, 4>(p, items, stream);
+        return;
+    }
     if constexpr (kAux == kAuxSC1 || kAux == kAuxSys) {
         if (lds) {
             if (waves == 8) {
@@ -666,6 +674,7 @@ void launch_aux(const Params& p, const Shape& sh, hipStream_t stream) {
     if (sh.policy == 0) launch_lds<kMode, kWeighted, kVPT, kFull, 0>(p, sh.lds, sh.waves, sh.group, stream);
     else if (sh.policy == 1) launch_lds<kMode, kWeighted, kVPT, kFull, kAuxNT>(p, sh.lds, sh.waves, sh.group, stream);
     else if (sh.policy == 3) launch_lds<kMode, kWeighted, kVPT, kFull, kAuxSys>(p, sh.lds, sh.waves, sh.group, stream);
+    else if (sh.policy == 4) launch_lds<kMode, kWeighted, kVPT, kFull, kAuxSC1NT>(p, sh.lds, sh.waves, sh.group, stream);
     else launch_lds<kMode, kWeighted, kVPT, kFull, kAuxSC1>(p, sh.lds, sh.waves, sh.group, stream);
 }
 
@@ -891,7 +900,9 @@ int launch_combine(int mode, int weighted, const Params& p_in, deepep_stream_t s
     sh.vpt = g_config.vec_per_lane > 0 ? g_config.vec_per_lane : (nvec >= 128 ? 2 : 1);
     if (sh.vpt != 1 && sh.vpt != 2) sh.vpt = 2;
     sh.lds = g_config.stage_lds >= 0 ? g_config.stage_lds != 0 : true;
-    sh.policy = p.out_rows != nullptr ? 3 : (g_config.store_policy >= 0 ? g_config.store_policy : 2);
+    // store policies: 0 plain, 1 nt, 2 sc1 (default), 3 system scope (peer windows), 4 sc1 nt
+    sh.policy = p.out_rows != nullptr ? 3 : (g_config.store_policy == 3 ? 4 :
+                                              (g_config.store_policy >= 0 ? g_config.store_policy : 2));
     // units_per_block 4 / 8 forces the workgroup shape; 0 = automatic
     sh.waves = p.units_per_block == 4 ? 4 : (p.units_per_block == 8 ? 8 : (mode == DEEPEP_MODE_LOCAL ? 4 : 8));
     // rows in flight per lane: 8 for the fused / epilogue reduces (8 rows per token at EP = 1), 4 for
@@ -1013,7 +1024,7 @@ int deepep_last_kernel_choice(void) { return g_last_choice; }
 
 int deepep_set_launch_config(int vec_per_lane, int stage_lds, int store_policy, int rows_in_flight) {
     if (vec_per_lane < 0 || vec_per_lane > 2 || stage_lds < -1 || stage_lds > 1 || store_policy < -1 ||
-        store_policy > 2 || (rows_in_flight != 0 && rows_in_flight != 2 && rows_in_flight != 4 && rows_in_flight != 8))
+        store_policy > 3 || (rows_in_flight != 0 && rows_in_flight != 2 && rows_in_flight != 4 && rows_in_flight != 8))
         return set_error(DEEPEP_ERR_INVALID_ARG, "invalid launch configuration");
     g_config.vec_per_lane = vec_per_lane;
     g_config.stage_lds = stage_lds;

@@ -148,7 +148,8 @@ int deepep_build_local_plan(const int32_t* src_metadata, int num_recv_tokens, in
  * Tuning / diagnostics (process-global; 0 or -1 = automatic, the default):
  *   vec_per_lane   16-byte vectors each lane loads per source row and item (1 or 2)
  *   stage_lds      1: stage the slot table / weights per workgroup in LDS; 0: per wave in registers
- *   store_policy   output store cache policy: 0 plain, 1 nt, 2 sc1 (write-through)
+ *   store_policy   output store cache policy: 0 plain, 1 nt, 2 sc1 (write-through), 3 sc1 nt (the two
+ *                  default shapes only: 8 x 8 rows in flight / 4 x 4)
  *   rows_in_flight source rows each lane loads before accumulating them (2, 4 or 8; LDS staging with
  *                  sc1 or system-scope stores only).  Automatic: 8 for the fused / epilogue reduces,
  *                  4 for phase A (DEEPEP_MODE_LOCAL) and for every launch on a CU-budget stream.

@@ -75,6 +75,9 @@ def main():
         '4-wave workgroups': lambda: kern.combine_reduce(MODE_FUSED, y, out, T, table=table, row_weights=ex_w,
                                                          wtable=table, wsrc=ex_w, out_weights=out_w,
                                                          units_per_block=4, stream=s),
+        'stores sc1 nt': with_config(fused(True, True), cfg=(0, -1, 3, 0)),
+        'stores nt': with_config(fused(True, True), cfg=(0, -1, 1, 0)),
+        'stores plain': with_config(fused(True, True), cfg=(0, -1, 0, 0)),
         'persistent grid (choice 5)': with_config(fused(True, True), choice=5),
         'streaming kernel (choice 1)': with_config(fused(True, True), choice=1),
     }

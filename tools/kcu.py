@@ -51,8 +51,17 @@ def main():
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) * 1e3 / n
 
-    for n in (0, 224, 192, 160, 128, 96, 64, 32, 24, 16, 8):
-        row = dict(num_sms=n)
+    # the reference's bandwidth-model CU counts (get_theoretical_num_sms, elastic.py:728-834) that a
+    # DEEPEP_COMBINE_CUS=handle combine is confined to at EP = 2, 4, 8 (this shape's routing)
+    model = {}
+    saved = (buf.num_ranks, buf.num_nvlink_ranks)
+    for r in (2, 4, 8):
+        buf.num_ranks = buf.num_nvlink_ranks = r
+        model[buf.get_theoretical_num_sms(E, K)] = f'model_ep{r}'
+    buf.num_ranks, buf.num_nvlink_ranks = saved
+    print(json.dumps(dict(model_num_sms={v: k for k, v in model.items()})), flush=True)
+    for n in [0, 224, 192, 160, 128, 96, 64, 32, 24, 16, 8] + sorted(model, reverse=True):
+        row = dict(num_sms=n, tag=model.get(n, ''))
         s0 = torch.cuda.current_stream()
         row['api_us'] = round(timed(lambda: buf.combine(y, handle, topk_weights=ex_w, apply_topk_weights=True,
                                                         num_sms=n), s0), 1)

@@ -83,12 +83,12 @@ def main():
     kern.lib.deepep_set_kernel_choice(-1)
     # output store policy of phase A (40 % of its bytes are the partial rows): plain / nt / sc1
     for rnd in range(2):
-        for pol in (0, 1, 2):
+        for pol in (0, 1, 2, 3):
             assert kern.lib.deepep_set_launch_config(0, -1, pol, 0) == 0
             us = timeit(lambda: kern.combine_reduce(MODE_LOCAL, y, packed[:, :H], n_recv, table=table_a, row_weights=w,
                                                     wtable=table_a, wsrc=w, out_weights=pw, weights_pad=32, stream=s), s)
-            print(json.dumps(dict(phase='A_store', policy=('plain', 'nt', 'sc1')[pol], round=rnd, us=round(us, 1),
-                                  gbps=round(bytes_a / us / 1e3, 1))), flush=True)
+            print(json.dumps(dict(phase='A_store', policy=('plain', 'nt', 'sc1', 'sc1 nt')[pol], round=rnd,
+                                  us=round(us, 1), gbps=round(bytes_a / us / 1e3, 1))), flush=True)
     kern.lib.deepep_set_launch_config(0, -1, -1, 0)
     # same bytes, rows in a random order (no expert grouping): the scatter's cost
     perm = torch.randperm(n_exp, device='cuda', generator=g).to(torch.int32)

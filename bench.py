@@ -49,6 +49,53 @@ def _init_dist(n_gpus: int):
     return dist.get_rank(), dist.get_world_size()
 
 
+_XGMI = {'enabled': os.environ.get('DEEPEP_BENCH_XGMI', '1') != '0', 'preflight': None}
+
+
+def _xgmi_preflight() -> dict:
+    """Start xgmi_preflight.py as a child (before this process touches the GPU): a small xGMI
+    dispatch + combine checked bit for bit against the default transport, in a gloo world of the
+    children on MASTER_PORT + 1.  A GPU fault there ends the child, not the bench."""
+    import subprocess
+    import tempfile
+    # the children's own store: torchrun's agent store (TORCHELASTIC_USE_AGENT_STORE) serves the parents
+    env = {k: v for k, v in os.environ.items() if not k.startswith('TORCHELASTIC_')}
+    env['MASTER_PORT'] = str(int(os.environ.get('MASTER_PORT', '29500')) + 1)
+    env['MASTER_ADDR'] = os.environ.get('MASTER_ADDR', '127.0.0.1')
+    limit = 150.0
+    t0 = time.perf_counter()
+    with tempfile.TemporaryFile('w+') as out, tempfile.TemporaryFile('w+') as err:
+        p = subprocess.Popen([sys.executable, os.path.join(ROOT, 'xgmi_preflight.py')], env=env, cwd=ROOT,
+                             stdout=out, stderr=err, text=True)
+        rc = None
+        while rc is None and time.perf_counter() - t0 < limit:
+            try:
+                rc = p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                print(f'[bench] xgmi preflight running ({time.perf_counter() - t0:.0f} s)', file=sys.stderr, flush=True)
+        if rc is None:
+            p.kill()
+            p.wait()
+            return dict(ok=False, error=f'preflight timed out ({limit:.0f} s)', seconds=round(time.perf_counter() - t0, 1))
+        out.seek(0)
+        err.seek(0)
+        stdout, stderr = out.read(), err.read()
+    lines = [ln for ln in stdout.splitlines() if ln.startswith('{')]
+    try:
+        res = json.loads(lines[-1]) if lines else {}
+    except ValueError:
+        res = {}
+    res['exit_status'] = rc
+    res['ok'] = bool(res.get('ok')) and rc == 0
+    if not res['ok'] and not res.get('error'):
+        res['error'] = (stderr.strip().splitlines() or ['no output'])[-1][:300]
+    return res
+
+
+def _xgmi_enabled() -> bool:
+    return _XGMI['enabled']
+
+
 def _cpu_threads() -> int:
     """Host threads for the CPU baseline: the GPU box's CPU share per GPU (16; os.cpu_count() there
     reports the whole machine's CPUs, many times as many -- both are in the line)."""
@@ -285,7 +332,7 @@ def _bench_single(y, handle, ex_w, weighted, total_bytes, steps, warmup, dev, re
         return float(t.item())
 
     res, outs = {}, {}
-    transports = ['rccl'] + (['xgmi'] if os.environ.get('DEEPEP_BENCH_XGMI', '1') != '0' else [])
+    transports = ['rccl'] + (['xgmi'] if _xgmi_enabled() else [])
     for transport in transports:
         sb, err = None, None
         try:
@@ -397,7 +444,16 @@ def main():
                     help='skip the per-launch flushed timing (keeps a rocprof kernel average to back-to-back launches)')
     args = ap.parse_args()
 
+    multi = 'RANK' in os.environ and int(os.environ.get('WORLD_SIZE', '1')) > 1
+    if multi and _XGMI['enabled']:
+        _XGMI['preflight'] = _xgmi_preflight()
     rank, world = _init_dist(args.gpus)
+    if _XGMI['preflight'] is not None:
+        # the xGMI legs run only when every rank's preflight passed
+        ok = torch.tensor([1 if _XGMI['preflight']['ok'] else 0], dtype=torch.int32,
+                          device=torch.device('cuda', torch.cuda.current_device()))
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        _XGMI['enabled'] = bool(ok.item())
     from deepep_amd import ElasticBuffer
     from deepep_amd.kernels import MODE_EPILOGUE, MODE_FUSED
     T, H, K, E = args.tokens, args.hidden, args.topk, args.experts
@@ -667,7 +723,9 @@ def main():
                            'exchange = off-rank partial rows + weights / exchange time, per rank')
 
     xgmi = None
-    if world > 1 and os.environ.get('DEEPEP_BENCH_XGMI', '1') != '0':
+    if world > 1 and not _xgmi_enabled() and _XGMI['preflight'] is not None:
+        xgmi = dict(skipped='xgmi_preflight failed on at least one rank (see xgmi_preflight)')
+    if world > 1 and _xgmi_enabled():
         xgmi = _bench_xgmi(buf, y, handle, ex_w, weighted, total_bytes, args.steps, args.warmup, dev)
     single = None
     if world > 1 and os.environ.get('DEEPEP_BENCH_SINGLE', '1') != '0':
@@ -708,7 +766,7 @@ def main():
                     transport=buf.transport if world > 1 else 'local',
                     note='ElasticBuffer.dispatch(do_expand=True) wall time incl. host count syncs; cached = '
                          'dispatch(handle=...) (no sync); bytes = x read once + expanded rows written')
-    if world > 1 and os.environ.get('DEEPEP_BENCH_XGMI', '1') != '0':
+    if world > 1 and _xgmi_enabled():
         dispatch['xgmi'] = _bench_xgmi_dispatch(buf, x_disp, topk_idx, topk_w, E, disp_bytes, time_dispatch, dev)
     del x_disp
 
@@ -784,7 +842,7 @@ def main():
                        'parallelism': f'ep{world}', 'transport': transport},
             'roofline': roofline, 'cpu_baseline': cpu_baseline, 'cpu_torch': cpu_torch, 'loopback': loopback,
             'phases': phases, 'su_bandwidth': su_line, 'rccl': rccl, 'xgmi': xgmi, 'single_reduction': single,
-            'dispatch': dispatch,
+            'dispatch': dispatch, 'xgmi_preflight': _XGMI['preflight'],
         }
         print(json.dumps(line), flush=True)
     dist.barrier()

@@ -38,7 +38,7 @@ def binary_build_id(path: str) -> Optional[str]:
         data = f.read()
     i = data.find(b'DEEPEP_BUILD_ID=')
     return data[i + 16:i + 32].decode(errors='replace') if i >= 0 else None
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 MODE_LOCAL, MODE_EPILOGUE, MODE_FUSED = 0, 1, 2
 
@@ -96,10 +96,12 @@ SIGNATURES = {
     'deepep_last_kernel_choice': (_I, []),
     'deepep_combine_buffer_size': (_I64, [_I, _I, _I, _I, _I]),
     'deepep_dispatch_route': (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P]),
+    'deepep_dispatch_notify': (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _I64, _P]),
+    'deepep_dispatch_notify_workspace': (_I64, [_I, _I, _I]),
     'deepep_dispatch_expert_counts': (_I, [_P, _I, _I, _I, _P, _P]),
     'deepep_dispatch_pack': (_I, [_P, _I64, _I, _P, _I64, _I, _P, _P, _I, _I, _I, _P, _P, _I,
                                   _P, _P, _I64, _I64, _I, _I, _I, _I, _P, _P]),
-    'deepep_dispatch_count': (_I, [_P, _I64, _I, _I, _I, _I, _I, _I, _P, _I, _I, _P, _P, _P, _P, _P]),
+    'deepep_dispatch_count': (_I, [_P, _I64, _I, _I, _I, _I, _I, _I, _P, _I, _I, _P, _I, _P, _P, _P, _P, _P]),
     'deepep_dispatch_scan': (_I, [_P, _I, _I, _I, _I, _P, _P, _P]),
     'deepep_dispatch_slots': (_I, [_P, _I64, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P]),
     'deepep_dispatch_copy': (_I, [_P, _I64, _I, _I, _I, _I, _I, _I, _P, _I, _P, _I64, _P, _I64, _I,

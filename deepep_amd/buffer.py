@@ -172,6 +172,27 @@ class ElasticBuffer(ExchangeMixin):
                 int(os.environ.get('DEEPEP_EAGER_WINDOW', 1)) and not hasattr(group, 'comm'):
             self._window(self._window_bytes(hidden, num_topk, num_max_tokens_per_rank), slots=1, rows_per_slot=1)
 
+    class _HostCopy:
+        """An int32 device vector on its way to pinned host memory (D2H on `stream`, not waited for)."""
+
+        def __init__(self, src: torch.Tensor, pinned: torch.Tensor, stream):
+            self.buf = pinned[:src.numel()]
+            self.buf.copy_(src, non_blocking=True)
+            self.event = torch.cuda.Event()
+            self.event.record(stream)
+
+        def wait(self) -> List[int]:
+            self.event.synchronize()
+            return self.buf.tolist()
+
+    def _host_copy(self, src: torch.Tensor, stream) -> '_HostCopy':
+        """Start the D2H of `src` (int32) into this buffer's pinned staging vector; .wait() returns the
+        values.  One copy in flight per buffer: a dispatch waits for its own before it returns."""
+        n = src.numel()
+        if getattr(self, '_pinned', None) is None or self._pinned.numel() < n:
+            self._pinned = torch.empty((max(n, 4096),), dtype=torch.int32, pin_memory=True)
+        return ElasticBuffer._HostCopy(src, self._pinned, stream)
+
     def _group_barrier(self) -> None:
         """torch.cuda.synchronize(); group barrier; synchronize (elastic.py:365-367)."""
         if self.use_cuda:
@@ -397,9 +418,10 @@ class ElasticBuffer(ExchangeMixin):
 
         A fresh handle costs one host sync (the notify counts, as the reference's do_cpu_sync=True).
         With do_cpu_sync=False the outputs are padded to the worst case as the reference's
-        (buffer.hpp:1065-1070); on one rank that call then issues kernels only (launches sized for all
-        tokens, bounded on the device by the received count; graph-capturable), while EP > 1 still syncs
-        once (the all-to-all needs host split sizes).  A cached handle (`handle=...`) needs no sync.
+        (buffer.hpp:1065-1070) and the call issues kernels only, at every EP size (launches sized for
+        the worst case, bounded on the device by the received count; RCCL: a worst-case-padded
+        all-to-all, xGMI: the notify through the windows; graph-capturable).  A cached handle
+        (`handle=...`) needs no sync.
         The notify also carries per-64-token-block counts, so the handle's combines never sync."""
         num_topk = (handle.topk_idx if topk_idx is None else topk_idx).shape[1]
         num_sms = self.get_theoretical_num_sms(num_experts or handle.num_experts, num_topk) if num_sms == 0 else num_sms
@@ -478,24 +500,18 @@ class ElasticBuffer(ExchangeMixin):
                     sym.barrier(stream)                           # peers finished reading their windows
                 use_xgmi = use_xgmi and peer_offsets is not None      # a handle made by the RCCL path
             else:
-                # --- send side: destination slots (deterministic ranks), one packed row per (token, dest)
-                dst_slot = torch.empty((T, R), dtype=torch.int32, device=dev)
-                send_counts = torch.empty((R,), dtype=torch.int32, device=dev)
-                kern.dispatch_route(idx64, num_experts, R, dst_slot, send_counts, stream=stream)
-                expert_hist = torch.empty((num_experts,), dtype=torch.int32, device=dev)
-                kern.dispatch_expert_counts(idx64, num_experts, expert_hist, stream=stream)
-                # per 64-token block and destination: tokens and (token, lane) pairs -- the sizes of
-                # every pipeline chunk of the EP > 1 combine (handle.BlockCounts), so the combine plan
-                # never needs a host sync of its own
+                # --- send side: destination slots (deterministic ranks), one packed row per (token, dest),
+                # and the notify (dispatch.cuh:79-258): every destination d gets [tokens | tokens per local
+                # expert | per-64-token-block tokens | per-block (token, lane) pairs] from this rank -- the
+                # block counts size every pipeline chunk of the EP > 1 combine (handle.BlockCounts), so its
+                # plan never needs a host sync of its own.  One exchange sizes every receive-side
+                # allocation (and, unless sync-free, ONE host sync brings the counts to the host).
                 nb = chunk_geometry(num_max_tokens_per_rank, 1)[0] if R > 1 else 0
-                blk = torch.empty((2, R, nb), dtype=torch.int32, device=dev)
-                if R > 1:
-                    kern.route_block_counts(idx64, num_experts, R, nb, blk[0], blk[1], stream=stream)
-                # notify (dispatch.cuh:79-258): every destination gets [tokens | tokens per local expert |
-                # block counts] from this rank; one exchange sizes every receive-side allocation and every
-                # combine exchange (and, unless sync-free, ONE host sync brings them to the host).
-                notify = torch.cat([send_counts.view(R, 1), expert_hist.view(R, epr), blk[0], blk[1]], dim=1)
-                w_n = notify.shape[1]
+                w_n = 1 + epr + 2 * nb
+                dst_slot = torch.empty((T, R), dtype=torch.int32, device=dev)
+                send_offsets = torch.empty((R,), dtype=torch.int32, device=dev)
+                notify = torch.empty((R, w_n), dtype=torch.int32, device=dev)
+                kern.dispatch_notify(idx64, num_experts, R, nb, dst_slot, notify, send_offsets, stream=stream)
                 if R == 1:
                     recv_notify = notify
                 elif use_xgmi:
@@ -505,7 +521,7 @@ class ElasticBuffer(ExchangeMixin):
                     # reference's notify over NVLink, with no host collective (graph-capturable).
                     rec_w = align(R + w_n, 4)
                     rec = torch.zeros((R, rec_w), dtype=torch.int32, device=dev)
-                    rec[:, :R] = send_counts.view(1, R)
+                    rec[:, :R] = notify[:, 0].view(1, R)
                     rec[:, R:R + w_n] = notify
                     sym.barrier(stream)                           # peers finished reading their windows
                     sym.put_notify(rec, stream)
@@ -518,31 +534,40 @@ class ElasticBuffer(ExchangeMixin):
                 else:
                     recv_notify = torch.empty_like(notify)
                     self._a2a(recv_notify, notify)
+                host_notify = None
                 if sync_free:
                     # no CPU sync: the sizes stay on the device; launches are sized for the worst case (one
                     # rank: T rows both ways, which a cached dispatch over this handle reuses)
                     send_counts_l = recv_counts_l = [T] if R == 1 else None
-                    expert_counts_l = own_blk = recv_blk = None
+                    expert_counts_l = own_tok = own_pairs = recv_blk = None
+                elif R == 1 and self.use_cuda:
+                    # one rank: the counts only size the outputs, so they travel to pinned host memory
+                    # while the receive-side kernels (sized for all T tokens, as sync-free) run; the host
+                    # waits for them just before it allocates the outputs
+                    host_notify = self._host_copy(notify.view(-1), stream)
+                    send_counts_l = recv_counts_l = [T]
                 else:
-                    host = [int(v) for v in torch.cat([send_counts, blk.view(-1),
-                                                       recv_notify.reshape(-1)]).tolist()]   # host sync
-                    send_counts_l = host[:R]
-                    own_blk = host[R:R + 2 * R * nb]
+                    flat = notify.view(-1) if R == 1 else torch.cat([notify.view(-1), recv_notify.reshape(-1)])
+                    host = [int(v) for v in flat.tolist()]                # host sync
+                    own, rec_host = host[:R * w_n], (host if R == 1 else host[R * w_n:])
+                    send_counts_l = own[0::w_n]
+                    own_tok = [own[d * w_n + 1 + epr:d * w_n + 1 + epr + nb] for d in range(R)]
+                    own_pairs = [own[d * w_n + 1 + epr + nb:(d + 1) * w_n] for d in range(R)]
                     _, recv_counts_l, expert_counts_l, _, recv_blk = notify_layout(
-                        host[R + 2 * R * nb:], R, r, epr, all_gathered=False, num_blocks=nb)
+                        rec_host, R, r, epr, all_gathered=False, num_blocks=nb)
                 counts = None
                 if R > 1:
+                    own_b = notify[:, 1 + epr:].reshape(R, 2, nb).transpose(0, 1)
                     rb = recv_notify[:, 1 + epr:].reshape(R, 2, nb).transpose(0, 1)
-                    dev_counts = torch.cat([blk, rb]).contiguous()
+                    dev_counts = torch.cat([own_b, rb]).contiguous()
                     if sync_free:
                         counts = BlockCounts(nb, None, None, None, None, dev_counts)
                     else:
-                        counts = BlockCounts(nb, [own_blk[d * nb:(d + 1) * nb] for d in range(R)],
-                                             [own_blk[(R + d) * nb:(R + d + 1) * nb] for d in range(R)],
-                                             [b[:nb] for b in recv_blk], [b[nb:] for b in recv_blk], dev_counts)
-                recv_counts_t = recv_notify[:, 0].contiguous()
-                send_offsets = (torch.cumsum(send_counts, 0) - send_counts).to(torch.int32)
-            # received rows: known on the host, or the worst case (R * T_max) without a CPU sync
+                        counts = BlockCounts(nb, own_tok, own_pairs, [b[:nb] for b in recv_blk],
+                                             [b[nb:] for b in recv_blk], dev_counts)
+                recv_counts_t = recv_notify[:, 0]                 # rows per source (a strided view)
+            # received rows: known on the host, or the worst case (R * T_max) without a CPU sync (one
+            # rank, counts still on their way to the host: all T tokens)
             N = num_max_tokens_per_rank * R if sync_free else sum(recv_counts_l)
             pad_rows = num_max_tokens_per_rank if padded else 0
             row_map = None
@@ -581,6 +606,7 @@ class ElasticBuffer(ExchangeMixin):
                 psum_expert = cached.psum_num_recv_tokens_per_expert
                 meta = cached.recv_src_metadata[:N]
                 inv, block_offsets = getattr(cached, '_copy_tables', (None, None))
+                copy_meta, copy_rows = getattr(cached, '_copy_meta', None) or (meta, N)
                 row_map = getattr(cached, '_row_map', None)
                 out_idx = None if do_expand else cached._recv_topk_idx.clone()
                 aligned_l = cached.num_recv_tokens_per_expert_list
@@ -589,19 +615,21 @@ class ElasticBuffer(ExchangeMixin):
                     cumulative_local_expert_recv_stats += expert_counts.to(cumulative_local_expert_recv_stats.dtype)
                 self._before_epilogue(previous_event_before_epilogue)
             else:
-                psum_rank = torch.cumsum(recv_counts_t, 0).to(torch.int32)
+                psum_rank = torch.empty((R,), dtype=torch.int32, device=dev)
                 meta = torch.empty((N, K + 2), dtype=torch.int32, device=dev)
                 out_idx = None if do_expand else torch.empty((N, K), dtype=torch.int64, device=dev)
                 nblocks = (N + DISPATCH_BLOCK_ROWS - 1) // DISPATCH_BLOCK_ROWS
                 block_counts = torch.empty((nblocks, epr), dtype=torch.int32, device=dev)
-                kern.dispatch_count(recv_packed, layout, N, r, epr, psum_rank, meta, out_idx, block_counts,
-                                    pad_rows=pad_rows, row_map=row_map, stream=stream)
+                kern.dispatch_count(recv_packed, layout, N, r, epr, None, meta, out_idx, block_counts,
+                                    pad_rows=pad_rows, row_map=row_map, rank_counts=recv_counts_t,
+                                    psum_out=psum_rank, stream=stream)
                 expert_counts = torch.empty((epr,), dtype=torch.int32, device=dev)
                 psum_expert = torch.empty((epr,), dtype=torch.int32, device=dev)
                 kern.dispatch_scan(block_counts, epr, expert_alignment, do_expand, expert_counts, psum_expert,
                                    stream=stream)
                 # known since the notify; [] without a CPU sync (as the reference's handle)
-                aligned_l = [] if sync_free else [align(c, expert_alignment) for c in expert_counts_l]
+                aligned_l = [] if sync_free or host_notify is not None else \
+                    [align(c, expert_alignment) for c in expert_counts_l]
                 if cumulative_local_expert_recv_stats is not None:
                     cumulative_local_expert_recv_stats += expert_counts.to(cumulative_local_expert_recv_stats.dtype)
                 self._before_epilogue(previous_event_before_epilogue)
@@ -615,6 +643,18 @@ class ElasticBuffer(ExchangeMixin):
                                         stream=stream)
                 else:
                     meta[:, 2:] = -1
+                copy_meta, copy_rows = meta, N
+                if host_notify is not None:
+                    # one rank, host-synced: the counts have reached the host meanwhile; the launches above
+                    # covered all T tokens (rows past the received ones hold metadata -1), the handle and the
+                    # non-expanded outputs take the received rows
+                    host = host_notify.wait()
+                    send_counts_l = recv_counts_l = [host[0]]
+                    expert_counts_l = host[1:1 + epr]
+                    aligned_l = [align(c, expert_alignment) for c in expert_counts_l]
+                    N = host[0]
+                    meta = meta[:N]
+                    out_idx = out_idx[:N] if out_idx is not None else None
             num_unaligned = expert_counts
             if do_expand and cached is not None:
                 num_expanded = cached.num_expanded_tokens
@@ -639,9 +679,14 @@ class ElasticBuffer(ExchangeMixin):
             out_sf = alloc((n_rows, sf.shape[1]), dtype=sf.dtype, device=dev) if sf is not None else None
             out_w = None
             if topk_weights is not None:
-                out_w = (torch.zeros((n_rows,), dtype=torch.float32, device=dev) if do_expand else
-                         alloc((N, K), dtype=torch.float32, device=dev))
-            kern.dispatch_copy(recv_packed, layout, N, meta, do_expand,
+                # expanded: the copy writes the weight of every expanded row; rows it never writes (expert
+                # alignment padding, the worst-case tail of a sync-free call) hold 0
+                exact = expert_alignment == 1 and (bool(cached.num_recv_tokens_per_expert_list)
+                                                   if cached is not None else not sync_free)
+                out_w = ((torch.empty if exact else torch.zeros)((n_rows,), dtype=torch.float32, device=dev)
+                         if do_expand else alloc((N, K), dtype=torch.float32, device=dev))
+            kern.dispatch_copy(recv_packed, layout, copy_rows if do_expand else N, copy_meta if do_expand else meta,
+                               do_expand,
                                out_x.view(torch.uint8), out_sf.view(torch.uint8) if out_sf is not None else None,
                                out_w, x_direct=x_bytes if direct else None,
                                sf_direct=sf_bytes if direct else None, num_max_tokens=num_max_tokens_per_rank,
@@ -669,6 +714,7 @@ class ElasticBuffer(ExchangeMixin):
             handle._recv_topk_idx = recv_idx64
             handle._counts = counts
             handle._copy_tables = (inv, block_offsets)      # reused by cached dispatches
+            handle._copy_meta = (copy_meta, copy_rows) if copy_rows != N else None
             handle._row_map = row_map
         out_x = (out_x, out_sf) if out_sf is not None else out_x
         return out_x, out_idx, out_w, handle, EventOverlap(event)

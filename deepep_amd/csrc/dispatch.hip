@@ -127,6 +127,134 @@ expert_hist_kernel(const int64_t* __restrict__ topk_idx, int64_t n, int E, int32
         if (s_hist[e] != 0) atomicAdd(&counts[e], s_hist[e]);
 }
 
+// ---------------------------------------------------------------- notify: the send side in two launches
+// Everything the send side of a fresh dispatch derives from topk_idx: dst_slot (as route_count +
+// route_assign), and the record every destination d gets -- notify[d] = [tokens to d | tokens per expert
+// of d (expert_hist's slice) | per-64-token-block tokens to d | per-block (token, lane) pairs to d
+// (block_counts_kernel)] -- plus the exclusive prefix of the per-rank counts (the packed rows' send
+// offsets).  Two launches over 256-token workgroups replace five launches and three torch ops between
+// them (a fresh dispatch is launch-bound: each launch costs ~10 us of host time):
+//   count:  per workgroup, tokens per destination and an expert histogram (LDS) into the workspace;
+//           the per-64-token-block counts (one wave = one block) straight into notify;
+//   assign: per workgroup, the destination slots of its tokens (base = the earlier workgroups' counts,
+//           ballot ranks inside), and a grid-strided share of the totals: per-destination tokens,
+//           expert counts summed over the workgroups' histograms, send offsets, zeroed tail blocks.
+// No atomics on global memory and no zeroed inputs; deterministic.
+constexpr int kNotifyTok = 256;                      // tokens per workgroup (4 waves)
+
+__global__ void __launch_bounds__(kNotifyTok)
+notify_count_kernel(const int64_t* __restrict__ topk_idx, int T, int K, int E, int R, int nb,
+                    int32_t* __restrict__ notify, int32_t* __restrict__ ws_cnt, int32_t* __restrict__ ws_hist) {
+    extern __shared__ int32_t s_hist[];              // [E]
+    __shared__ int32_t s_cnt[4][64];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int epr = E / R;
+    const int64_t W = 1 + epr + 2 * static_cast<int64_t>(nb);
+    for (int e = tid; e < E; e += kNotifyTok) s_hist[e] = 0;
+    __syncthreads();
+    const int t = blockIdx.x * kNotifyTok + tid;
+    uint64_t mask = 0;
+    int rk[32];
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+        rk[k] = -1;
+        if (k < K && t < T) {
+            const int64_t e = topk_idx[static_cast<int64_t>(t) * K + k];
+            if (e >= 0 && e < E) {
+                rk[k] = static_cast<int>(e) / epr;
+                mask |= 1ull << rk[k];
+                atomicAdd(&s_hist[static_cast<int>(e)], 1);
+            }
+        }
+    }
+    const int b = blockIdx.x * (kNotifyTok / 64) + wave;     // this wave's 64-token block
+    for (int r = 0; r < R; ++r) {
+        const uint64_t bal = __ballot((mask >> r) & 1ull);
+        if (lane == 0) s_cnt[wave][r] = __popcll(bal);
+        if (nb > 0) {
+            int c = 0;
+#pragma unroll
+            for (int k = 0; k < 32; ++k) c += rk[k] == r;
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+            if (lane == 0 && b < nb) {
+                notify[r * W + 1 + epr + b] = __popcll(bal);
+                notify[r * W + 1 + epr + nb + b] = c;
+            }
+        }
+    }
+    __syncthreads();
+    if (tid < R)
+        ws_cnt[static_cast<int64_t>(blockIdx.x) * R + tid] = s_cnt[0][tid] + s_cnt[1][tid] + s_cnt[2][tid] + s_cnt[3][tid];
+    for (int e = tid; e < E; e += kNotifyTok) ws_hist[static_cast<int64_t>(blockIdx.x) * E + e] = s_hist[e];
+}
+
+__global__ void __launch_bounds__(kNotifyTok)
+notify_assign_kernel(const int64_t* __restrict__ topk_idx, int T, int K, int E, int R, int nb, int nblk,
+                     const int32_t* __restrict__ ws_cnt, const int32_t* __restrict__ ws_hist,
+                     int32_t* __restrict__ dst_slot, int32_t* __restrict__ notify, int32_t* __restrict__ send_offsets) {
+    __shared__ int32_t s_base[64];
+    __shared__ int32_t s_cnt[4][64];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int blk = blockIdx.x, grid = gridDim.x;
+    const int epr = E / R;
+    const int64_t W = 1 + epr + 2 * static_cast<int64_t>(nb);
+    if (tid < R) {
+        int base = 0;
+        for (int j = 0; j < blk && j < nblk; ++j) base += ws_cnt[static_cast<int64_t>(j) * R + tid];
+        s_base[tid] = base;
+    }
+    const int t = blk * kNotifyTok + tid;
+    uint64_t mask = 0;
+    if (t < T)
+        for (int k = 0; k < K; ++k) {
+            const int64_t e = topk_idx[static_cast<int64_t>(t) * K + k];
+            if (e >= 0 && e < E) mask |= 1ull << (static_cast<int>(e) / epr);
+        }
+    for (int r = 0; r < R; ++r) {
+        const int c = __popcll(__ballot((mask >> r) & 1ull));
+        if (lane == 0) s_cnt[wave][r] = c;
+    }
+    __syncthreads();
+    if (blk < nblk && t < T) {
+        const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+        for (int r = 0; r < R; ++r) {
+            const bool hit = (mask >> r) & 1ull;
+            const uint64_t bal = __ballot(hit);
+            int slot = -1;
+            if (hit) {
+                slot = s_base[r] + __popcll(bal & lt);
+                for (int w = 0; w < wave; ++w) slot += s_cnt[w][r];
+            }
+            dst_slot[static_cast<int64_t>(t) * R + r] = slot;
+        }
+    }
+    // the totals, grid-strided: expert counts (sum of the workgroups' histograms), per-destination
+    // tokens and send offsets (workgroup 0), tail blocks no count workgroup covered (zeros)
+    for (int e = blk * kNotifyTok + tid; e < E; e += grid * kNotifyTok) {
+        int c = 0;
+        for (int j = 0; j < nblk; ++j) c += ws_hist[static_cast<int64_t>(j) * E + e];
+        const int r = e / epr;
+        notify[r * W + 1 + (e - r * epr)] = c;
+    }
+    if (blk == 0 && tid < R) {
+        int total = 0, before = 0;
+        for (int j = 0; j < nblk; ++j) total += ws_cnt[static_cast<int64_t>(j) * R + tid];
+        for (int q = 0; q < tid; ++q)
+            for (int j = 0; j < nblk; ++j) before += ws_cnt[static_cast<int64_t>(j) * R + q];
+        notify[tid * W] = total;
+        send_offsets[tid] = before;
+    }
+    const int covered = nblk * (kNotifyTok / 64);
+    for (int i = blk * kNotifyTok + tid; i < R * nb; i += grid * kNotifyTok) {
+        const int r = i / nb, bb = i - r * nb;
+        if (bb >= covered) {
+            notify[r * W + 1 + epr + bb] = 0;
+            notify[r * W + 1 + epr + nb + bb] = 0;
+        }
+    }
+}
+
 // ---------------------------------------------------------------- pack: one wave per token
 // packed row layout (bytes): [x | sf @sf_off | topk_idx (int64) @idx_off | weights @w_off | src @src_off]
 // Row of (token t, destination r): base_r + (send_offsets[r] + dst_slot[t][r]) * row_bytes, base_r =
@@ -224,12 +352,21 @@ __device__ __forceinline__ int local_expert(int64_t e, int rank, int epr) {
 // the received ones get metadata -1 (and recv_topk_idx -1): the later kernels skip them.
 __global__ void __launch_bounds__(kBlockRows)
 count_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int idx_off, int src_off, int N, int K,
-             int rank, int epr, const int32_t* __restrict__ rank_psum, int R, int pad_rows,
-             int32_t* __restrict__ row_map,
+             int rank, int epr, const int32_t* __restrict__ recv_counts, int counts_stride, int32_t* __restrict__ psum_out,
+             int R, int pad_rows, int32_t* __restrict__ row_map,
              int32_t* __restrict__ meta, int64_t* __restrict__ recv_topk_idx, int32_t* __restrict__ block_counts) {
     extern __shared__ int32_t s_hist[];                 // [epr]
+    __shared__ int32_t rank_psum[64];                   // inclusive prefix of rows per source rank
     for (int e = threadIdx.x; e < epr; e += kBlockRows) s_hist[e] = 0;
+    if (threadIdx.x < R)
+        rank_psum[threadIdx.x] = recv_counts[static_cast<int64_t>(threadIdx.x) * (counts_stride > 0 ? counts_stride : 1)];
     __syncthreads();
+    if (counts_stride > 0) {                            // counts -> inclusive prefix (R <= 64)
+        if (threadIdx.x == 0)
+            for (int s = 1; s < R; ++s) rank_psum[s] += rank_psum[s - 1];
+        __syncthreads();
+        if (psum_out != nullptr && blockIdx.x == 0 && threadIdx.x < R) psum_out[threadIdx.x] = rank_psum[threadIdx.x];
+    }
     const int i = blockIdx.x * kBlockRows + threadIdx.x;
     const int received = min(N, rank_psum[R - 1]);
     if (i >= received && i < N) {
@@ -263,8 +400,9 @@ count_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int idx_off,
         meta[mrow + 1] = src_rank * K + master;
     }
     __syncthreads();
-    for (int e = threadIdx.x; e < epr; e += kBlockRows)
-        block_counts[static_cast<int64_t>(blockIdx.x) * epr + e] = s_hist[e];
+    if (blockIdx.x * kBlockRows < N)                    // (N == 0: the one workgroup formed psum_out only)
+        for (int e = threadIdx.x; e < epr; e += kBlockRows)
+            block_counts[static_cast<int64_t>(blockIdx.x) * epr + e] = s_hist[e];
 }
 
 // One thread per local expert: offsets of every workgroup inside the expert's group, expert starts
@@ -566,6 +704,34 @@ int deepep_dispatch_route(const int64_t* topk_idx, int num_tokens, int num_topk,
     return launch_status("dispatch_route");
 }
 
+int64_t deepep_dispatch_notify_workspace(int num_tokens, int num_experts, int num_ranks) {
+    const int64_t nblk = (static_cast<int64_t>(std::max(num_tokens, 0)) + kNotifyTok - 1) / kNotifyTok;
+    return nblk * (num_ranks + num_experts) * 4;
+}
+
+int deepep_dispatch_notify(const int64_t* topk_idx, int num_tokens, int num_topk, int num_experts, int num_ranks,
+                           int num_blocks, int32_t* dst_slot, int32_t* notify, int32_t* send_offsets,
+                           void* workspace, int64_t workspace_bytes, deepep_stream_t stream) {
+    if (num_tokens < 0 || num_topk < 1 || num_topk > 32 || num_ranks < 1 || num_ranks > 64 ||
+        num_experts < num_ranks || num_experts % num_ranks != 0 || num_experts > 32768 ||
+        num_blocks < 0 || (num_ranks > 1 && num_blocks < (num_tokens + 63) / 64) ||
+        notify == nullptr || send_offsets == nullptr || (num_tokens > 0 && (dst_slot == nullptr || topk_idx == nullptr)) ||
+        workspace_bytes < deepep_dispatch_notify_workspace(num_tokens, num_experts, num_ranks) ||
+        (num_tokens > 0 && workspace == nullptr))
+        return deepep_amd_set_error(DEEPEP_ERR_INVALID_ARG, "dispatch_notify: invalid arguments");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const int nblk = (num_tokens + kNotifyTok - 1) / kNotifyTok;
+    int32_t* ws_cnt = static_cast<int32_t*>(workspace);
+    int32_t* ws_hist = ws_cnt + static_cast<int64_t>(nblk) * num_ranks;
+    if (nblk > 0)
+        hipLaunchKernelGGL(notify_count_kernel, dim3(nblk), dim3(kNotifyTok), static_cast<size_t>(num_experts) * 4, s,
+                           topk_idx, num_tokens, num_topk, num_experts, num_ranks, num_blocks, notify, ws_cnt, ws_hist);
+    hipLaunchKernelGGL(notify_assign_kernel, dim3(std::max(nblk, 1)), dim3(kNotifyTok), 0, s, topk_idx, num_tokens,
+                       num_topk, num_experts, num_ranks, num_blocks, nblk, ws_cnt, ws_hist, dst_slot, notify,
+                       send_offsets);
+    return launch_status("dispatch_notify");
+}
+
 int deepep_dispatch_expert_counts(const int64_t* topk_idx, int num_tokens, int num_topk, int num_experts,
                                   int32_t* counts, deepep_stream_t stream) {
     if (num_tokens < 0 || num_topk < 1 || num_topk > 32 || num_experts < 1 || num_experts > 32768 ||
@@ -615,20 +781,23 @@ int deepep_dispatch_pack(const void* x, int64_t x_row_stride_bytes, int x_bytes,
 
 int deepep_dispatch_count(const void* packed, int64_t row_bytes, int idx_off, int src_off, int num_recv, int num_topk,
                           int rank, int num_local_experts, const int32_t* recv_rank_psum, int num_ranks,
-                          int pad_rows, int32_t* row_map,
+                          int recv_counts_stride, int32_t* psum_out, int pad_rows, int32_t* row_map,
                           int32_t* src_metadata, int64_t* recv_topk_idx, int32_t* block_counts,
                           deepep_stream_t stream) {
-    if (num_recv == 0) return DEEPEP_OK;                  // a rank that receives nothing
+    // a rank that receives nothing: no rows, but one workgroup still forms psum_out
+    if (num_recv == 0 && (psum_out == nullptr || recv_counts_stride == 0)) return DEEPEP_OK;
     if (num_recv < 0 || num_topk < 1 || num_topk > 32 || num_local_experts < 1 || num_local_experts > 1024 ||
-        num_ranks < 1 || src_metadata == nullptr || block_counts == nullptr || packed == nullptr ||
-        recv_rank_psum == nullptr || pad_rows < 0 || (pad_rows > 0 && row_map == nullptr) ||
+        num_ranks < 1 || num_ranks > 64 || recv_counts_stride < 0 ||
+        (num_recv > 0 && (src_metadata == nullptr || block_counts == nullptr || packed == nullptr)) ||
+        recv_rank_psum == nullptr || pad_rows < 0 || (num_recv > 0 && pad_rows > 0 && row_map == nullptr) ||
         static_cast<int64_t>(pad_rows) * num_ranks >= (int64_t(1) << 31))
         return deepep_amd_set_error(DEEPEP_ERR_INVALID_ARG, "dispatch_count: invalid arguments");
-    const int nblocks = (num_recv + kBlockRows - 1) / kBlockRows;
+    const int nblocks = std::max(1, (num_recv + kBlockRows - 1) / kBlockRows);
     hipLaunchKernelGGL(count_kernel, dim3(nblocks), dim3(kBlockRows), num_local_experts * 4,
                        reinterpret_cast<hipStream_t>(stream), static_cast<const uint8_t*>(packed), row_bytes,
-                       idx_off, src_off, num_recv, num_topk, rank, num_local_experts, recv_rank_psum, num_ranks,
-                       pad_rows, row_map, src_metadata, recv_topk_idx, block_counts);
+                       idx_off, src_off, num_recv, num_topk, rank, num_local_experts, recv_rank_psum,
+                       recv_counts_stride, psum_out, num_ranks, pad_rows, row_map, src_metadata, recv_topk_idx,
+                       block_counts);
     return launch_status("dispatch_count");
 }
 

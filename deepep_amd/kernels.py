@@ -170,6 +170,26 @@ class HipKernels:
                                             ptr(send_counts), ptr(block_counts), _stream_handle(stream))
         _lib.check(rc, 'dispatch_route')
 
+    def dispatch_notify(self, topk_idx, num_experts, num_ranks, num_blocks, dst_slot, notify, send_offsets,
+                        stream=None):
+        """The send side in two launches: dst_slot [T, R], notify int32 [R, 1 + E/R + 2 * num_blocks] (per
+        destination: tokens | tokens per expert | per-block tokens | per-block pairs), send_offsets [R]."""
+        _require(topk_idx.is_cuda and topk_idx.dtype == torch.int64 and topk_idx.is_contiguous(), 'topk_idx int64')
+        T, K = topk_idx.shape
+        W = 1 + num_experts // num_ranks + 2 * num_blocks
+        _require(notify.dtype == torch.int32 and notify.is_contiguous() and tuple(notify.shape) == (num_ranks, W),
+                 'notify must be contiguous int32 [num_ranks, 1 + experts_per_rank + 2 * num_blocks]')
+        _require(dst_slot.dtype == torch.int32 and dst_slot.is_contiguous() and dst_slot.numel() == T * num_ranks,
+                 'dst_slot must be contiguous int32 [num_tokens, num_ranks]')
+        _require(send_offsets.dtype == torch.int32 and send_offsets.is_contiguous() and
+                 send_offsets.numel() == num_ranks, 'send_offsets must be contiguous int32 [num_ranks]')
+        ws_bytes = int(self.lib.deepep_dispatch_notify_workspace(T, num_experts, num_ranks))
+        ws = torch.empty((max(ws_bytes, 16),), dtype=torch.uint8, device=topk_idx.device)
+        rc = self.lib.deepep_dispatch_notify(ptr(topk_idx), T, K, num_experts, num_ranks, num_blocks, ptr(dst_slot),
+                                             ptr(notify), ptr(send_offsets), ptr(ws), ws.numel(),
+                                             _stream_handle(stream))
+        _lib.check(rc, 'dispatch_notify')
+
     def dispatch_expert_counts(self, topk_idx, num_experts, counts, stream=None):
         """counts[e] = (t, k) entries routed to expert e (int32 [num_experts])."""
         _require(topk_idx.is_cuda and topk_idx.dtype == torch.int64 and topk_idx.is_contiguous(), 'topk_idx int64')
@@ -248,15 +268,26 @@ class HipKernels:
         _lib.check(rc, 'dispatch_pack')
 
     def dispatch_count(self, packed, layout: RowLayout, num_recv, rank, num_local_experts, rank_psum, meta,
-                       recv_topk_idx, block_counts, pad_rows: int = 0, row_map=None, stream=None):
-        """pad_rows > 0: `packed` is a worst-case-sized receive buffer, source s's rows at s * pad_rows;
+                       recv_topk_idx, block_counts, pad_rows: int = 0, row_map=None, rank_counts=None,
+                       psum_out=None, stream=None):
+        """rank_psum: inclusive prefix of rows per source rank (int32 [R]); or, with rank_psum None,
+        rank_counts: rows per source rank (an int32 [R] view of any stride, e.g. the notify records'
+        first column), whose prefix the kernel forms and writes to psum_out (int32 [R]).
+        pad_rows > 0: `packed` is a worst-case-sized receive buffer, source s's rows at s * pad_rows;
         row_map (int32 [num_recv]) receives each received row's packed row (for slots / copy)."""
+        src = rank_psum if rank_psum is not None else rank_counts
+        _require(src is not None and src.dim() == 1 and src.dtype == torch.int32 and src.stride(0) >= 1,
+                 'dispatch_count needs rank_psum or rank_counts (int32 [num_ranks])')
+        R = src.shape[0]
+        stride = 0 if rank_psum is not None else src.stride(0)
+        _require(psum_out is None or (psum_out.dtype == torch.int32 and psum_out.is_contiguous() and
+                                      psum_out.numel() == R), 'psum_out must be contiguous int32 [num_ranks]')
         _require(pad_rows == 0 or (row_map is not None and row_map.dtype == torch.int32 and
-                                   row_map.numel() >= num_recv and packed.shape[0] >= pad_rows * rank_psum.shape[0]),
+                                   row_map.numel() >= num_recv and packed.shape[0] >= pad_rows * R),
                  'padded receive rows need a row map and R * pad_rows packed rows')
         rc = self.lib.deepep_dispatch_count(
             ptr(packed), layout.row_bytes, layout.idx_off, layout.src_off, num_recv, layout.num_topk, rank,
-            num_local_experts, ptr(rank_psum), rank_psum.shape[0], pad_rows, ptr(row_map), ptr(meta),
+            num_local_experts, ptr(src), R, stride, ptr(psum_out), pad_rows, ptr(row_map), ptr(meta),
             ptr(recv_topk_idx), ptr(block_counts), _stream_handle(stream))
         _lib.check(rc, 'dispatch_count')
 

@@ -26,7 +26,7 @@
  *       materialised once per handle
  *   deepep_combine_buffer_size
  *       ElasticBuffer::get_combine_buffer_size (csrc/elastic/buffer.hpp:616-650)
- *   deepep_dispatch_route / _expert_counts / _pack   (the handle producer, send side)
+ *   deepep_dispatch_notify (or _route / _expert_counts) / _pack   (the handle producer, send side)
  *       dispatch_impl's notify, slot assignment and token push
  *       (deep_ep/include/deep_ep/impls/dispatch.cuh:79-258, 336-392)
  *   deepep_dispatch_count / _scan / _slots / _copy   (receive side)
@@ -48,7 +48,7 @@ extern "C" {
 
 typedef struct ihipStream_t* deepep_stream_t;   /* == hipStream_t */
 
-#define DEEPEP_AMD_ABI_VERSION 11
+#define DEEPEP_AMD_ABI_VERSION 12
 
 #define DEEPEP_OK               0
 #define DEEPEP_ERR_INVALID_ARG  (-1)
@@ -199,6 +199,19 @@ int deepep_dispatch_route(const int64_t* topk_idx, int num_tokens, int num_topk,
 int deepep_dispatch_expert_counts(const int64_t* topk_idx, int num_tokens, int num_topk, int num_experts,
                                   int32_t* counts, deepep_stream_t stream);
 
+/* The send side of a fresh dispatch in two launches: dst_slot as deepep_dispatch_route; notify int32
+ * [num_ranks][W], W = 1 + experts_per_rank + 2 * num_blocks, row d = [tokens routed to d |
+ * deepep_dispatch_expert_counts' slice of d's experts | per-64-token-block tokens routed to d
+ * (deepep_route_block_counts' tok) | per-block (token, lane) pairs routed to d (its pairs)] -- the record
+ * dispatch_impl's notify sends to d (dispatch.cuh:79-258); send_offsets int32 [num_ranks] = the exclusive
+ * prefix of the per-rank token counts.  num_blocks may be 0 (no block counts, one rank) or >=
+ * ceil(num_tokens / 64); blocks past the tokens hold 0.  No output needs zeroing.  workspace: device
+ * scratch of at least deepep_dispatch_notify_workspace(...) bytes. */
+int64_t deepep_dispatch_notify_workspace(int num_tokens, int num_experts, int num_ranks);
+int deepep_dispatch_notify(const int64_t* topk_idx, int num_tokens, int num_topk, int num_experts, int num_ranks,
+                           int num_blocks, int32_t* dst_slot, int32_t* notify, int32_t* send_offsets,
+                           void* workspace, int64_t workspace_bytes, deepep_stream_t stream);
+
 /* Write packed row send_offsets[r] + dst_slot[t][r] for every (token t, destination r), in `packed`
  * (dest_bases NULL: one local buffer for an all-to-all) or in rank r's buffer at dest_bases[r] (device
  * uint64 [num_ranks]: the peers' symmetric windows, system-scope stores -- the xGMI push of
@@ -221,8 +234,11 @@ int deepep_dispatch_pack(const void* x, int64_t x_row_stride_bytes, int x_bytes,
 
 /* Receive side, pass 1: src_metadata columns 0-1 ({src_global_idx, src_rank * K + master lane}),
  * recv_topk_idx (local expert or -1, int64 [num_recv][K], may be NULL) and per-block expert
- * histograms block_counts [ceil(num_recv / DEEPEP_DISPATCH_BLOCK_ROWS)][num_local_experts]. recv_rank_psum is the
- * inclusive prefix sum of rows per source rank (device memory).  Rows from recv_rank_psum[num_ranks-1]
+ * histograms block_counts [ceil(num_recv / DEEPEP_DISPATCH_BLOCK_ROWS)][num_local_experts]. recv_counts_stride
+ * 0: recv_rank_psum is the inclusive prefix sum of rows per source rank (device memory);
+ * recv_counts_stride > 0: recv_rank_psum[s * recv_counts_stride] is the row count of source rank s (the
+ * notify records' first column) and the prefix sum is formed here, and written to psum_out (int32
+ * [num_ranks], may be NULL).  num_ranks <= 64.  Rows from the last prefix sum
  * up to num_recv (a launch sized for the worst case, dispatch(do_cpu_sync=False)) get src_metadata
  * columns 0-1 = -1 and recv_topk_idx -1; passes 3 and 4 skip them.
  * pad_rows > 0: the packed rows come from a worst-case-sized exchange, source s's rows at s * pad_rows
@@ -230,7 +246,7 @@ int deepep_dispatch_pack(const void* x, int64_t x_row_stride_bytes, int x_bytes,
  * which passes 3 and 4 take as their row_map.  pad_rows 0: packed row i is row i (row_map may be NULL). */
 int deepep_dispatch_count(const void* packed, int64_t row_bytes, int idx_off, int src_off, int num_recv, int num_topk,
                           int rank, int num_local_experts, const int32_t* recv_rank_psum, int num_ranks,
-                          int pad_rows, int32_t* row_map,
+                          int recv_counts_stride, int32_t* psum_out, int pad_rows, int32_t* row_map,
                           int32_t* src_metadata, int64_t* recv_topk_idx, int32_t* block_counts,
                           deepep_stream_t stream);
 

@@ -90,6 +90,23 @@ class OracleKernels:
                                    torch.full(is_to.shape, -1, dtype=torch.int64)).to(torch.int32))
         send_counts.copy_(is_to.sum(dim=0).to(torch.int32))
 
+    def dispatch_notify(self, topk_idx, num_experts, num_ranks, num_blocks, dst_slot, notify, send_offsets,
+                        stream=None):
+        R, epr = num_ranks, num_experts // num_ranks
+        send_counts = torch.empty((R,), dtype=torch.int32)
+        self.dispatch_route(topk_idx, num_experts, R, dst_slot, send_counts)
+        hist = torch.empty((num_experts,), dtype=torch.int32)
+        self.dispatch_expert_counts(topk_idx, num_experts, hist)
+        notify[:, 0] = send_counts
+        notify[:, 1:1 + epr] = hist.view(R, epr)
+        if num_blocks:
+            tok = torch.empty((R, num_blocks), dtype=torch.int32)
+            pairs = torch.empty((R, num_blocks), dtype=torch.int32)
+            self.route_block_counts(topk_idx, num_experts, R, num_blocks, tok, pairs)
+            notify[:, 1 + epr:1 + epr + num_blocks] = tok
+            notify[:, 1 + epr + num_blocks:] = pairs
+        send_offsets.copy_((torch.cumsum(send_counts, 0) - send_counts).to(torch.int32))
+
     def dispatch_expert_counts(self, topk_idx, num_experts, counts, stream=None):
         valid = topk_idx[topk_idx >= 0].view(-1)
         counts.copy_(torch.bincount(valid, minlength=num_experts)[:num_experts].to(torch.int32))
@@ -123,8 +140,14 @@ class OracleKernels:
         return torch.where(inr, idx - rank * epr, torch.full_like(idx, -1))
 
     def dispatch_count(self, packed, layout, num_recv, rank, num_local_experts, rank_psum, meta, recv_topk_idx,
-                       block_counts, pad_rows=0, row_map=None, stream=None):
+                       block_counts, pad_rows=0, row_map=None, rank_counts=None, psum_out=None, stream=None):
         K, epr = layout.num_topk, num_local_experts
+        if rank_psum is None:
+            rank_psum = torch.cumsum(rank_counts, 0).to(torch.int32)
+            if psum_out is not None:
+                psum_out.copy_(rank_psum)
+        if num_recv == 0:
+            return
         N = min(num_recv, int(rank_psum[-1]))          # rows received; the rest get metadata -1
         meta[N:num_recv, :2] = -1
         if recv_topk_idx is not None:

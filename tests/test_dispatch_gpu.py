@@ -201,3 +201,74 @@ def test_dispatch_modes_on_gpu(alignment, do_cpu_sync, do_handle_copy, fp8):
     buf = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=T, hidden=H, num_topk=K)
     fails = dispatch_mode_checks(buf, x, idx, w, E, T, alignment, do_cpu_sync, do_handle_copy)
     assert not fails, fails
+
+
+@pytest.mark.parametrize('R,K,E,T,T_max,masked', [
+    (1, 8, 256, 8192, 8192, 0.0),          # config 2's send side
+    (1, 2, 8, 1, 128, 0.5),
+    (1, 16, 64, 3000, 4096, 0.1),
+    (8, 8, 256, 8192, 8192, 0.05),         # config 3's
+    (8, 8, 256, 5000, 16384, 0.0),         # blocks past the batch hold zeros
+    (2, 3, 6, 1025, 1100, 0.3),
+    (64, 4, 128, 700, 700, 0.1),
+    (4, 8, 32, 0, 256, 0.0),               # an empty batch
+    (3, 6, 24, 32768, 32768, 0.2),
+    (8, 32, 256, 4000, 4096, 0.1),         # top-32
+])
+def test_dispatch_notify_matches_multi_launch_send_side(hip, R, K, E, T, T_max, masked):
+    """deepep_dispatch_notify (two launches) == route + expert counts + block counts + prefix, bitwise,
+    and the count kernel's counts mode (prefix formed in the kernel, psum_out) == its prefix-sum mode."""
+    from deepep_amd.handle import chunk_geometry
+    gen = torch.Generator().manual_seed(T + R * 7 + K)
+    idx, _ = _routing(T, E, K, R, masked, False, gen) if T else (torch.zeros((0, K), dtype=torch.int64), None)
+    idx = idx.cuda().contiguous()
+    nb = chunk_geometry(T_max, 1)[0] if R > 1 else 0
+    epr = E // R
+    W = 1 + epr + 2 * nb
+    dst = torch.full((T, R), -5, dtype=torch.int32, device='cuda')
+    notify = torch.full((R, W), -5, dtype=torch.int32, device='cuda')
+    offs = torch.full((R,), -5, dtype=torch.int32, device='cuda')
+    hip.dispatch_notify(idx, E, R, nb, dst, notify, offs)
+    dst_ref = torch.empty((T, R), dtype=torch.int32, device='cuda')
+    cnt = torch.empty((R,), dtype=torch.int32, device='cuda')
+    hist = torch.empty((E,), dtype=torch.int32, device='cuda')
+    if T:
+        hip.dispatch_route(idx, E, R, dst_ref, cnt)
+    else:
+        cnt.zero_()
+    hip.dispatch_expert_counts(idx, E, hist)
+    ref = [cnt.view(R, 1), hist.view(R, epr)]
+    if nb:
+        tok = torch.empty((R, nb), dtype=torch.int32, device='cuda')
+        pairs = torch.empty((R, nb), dtype=torch.int32, device='cuda')
+        hip.route_block_counts(idx, E, R, nb, tok, pairs)
+        ref += [tok, pairs]
+    torch.cuda.synchronize()
+    assert torch.equal(dst, dst_ref), 'dst_slot'
+    assert torch.equal(notify, torch.cat(ref, dim=1)), 'notify record'
+    assert torch.equal(offs, (torch.cumsum(cnt, 0) - cnt).to(torch.int32)), 'send offsets'
+    # count kernel fed with the notify column (strided counts) == fed with the host-formed prefix
+    from deepep_amd._lib import DISPATCH_BLOCK_ROWS
+    from deepep_amd.kernels import RowLayout
+    layout = RowLayout.make(0, 0, K)
+    n = int(cnt.sum())
+    packed = torch.zeros((max(n, 1), layout.row_bytes), dtype=torch.uint8, device='cuda')
+    if n:
+        hip.dispatch_pack(torch.empty((T, 16), dtype=torch.uint8, device='cuda')[:, :0], None, idx, None, 0, dst, offs, packed,
+                          layout)
+    outs = []
+    for mode in ('psum', 'counts'):
+        meta = torch.full((n, K + 2), -3, dtype=torch.int32, device='cuda')
+        bc = torch.full(((n + DISPATCH_BLOCK_ROWS - 1) // DISPATCH_BLOCK_ROWS, epr), -3, dtype=torch.int32,
+                        device='cuda')
+        psum_out = torch.full((R,), -3, dtype=torch.int32, device='cuda')
+        if mode == 'psum':
+            hip.dispatch_count(packed, layout, n, 0, epr, torch.cumsum(cnt, 0).to(torch.int32), meta, None, bc)
+            psum_out = torch.cumsum(cnt, 0).to(torch.int32)
+        else:
+            hip.dispatch_count(packed, layout, n, 0, epr, None, meta, None, bc, rank_counts=notify[:, 0],
+                               psum_out=psum_out)
+        torch.cuda.synchronize()
+        outs.append((meta, bc, psum_out))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b), 'count kernel: counts mode differs from psum mode'

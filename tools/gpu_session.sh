@@ -45,6 +45,9 @@ for step in "$@"; do
         kphase) run kphase 300 python tools/kphase.py ;;
         profphase) run profphase 300 rocprofv3 --kernel-trace --stats -d $OUT/profphase -o prof --output-format csv -- python3 tools/kphase_prof.py ;;
         kcu)    run kcu 300 python tools/kcu.py ;;
+        kdisp)  run kdisp 300 python tools/kdispatch.py ;;
+        kdispprof) export KDISPATCH_CPROFILE=1; run kdispprof 300 python tools/kdispatch.py; unset KDISPATCH_CPROFILE ;;
+        profdisp) run profdisp 300 rocprofv3 --kernel-trace -d $OUT/profdisp -o prof --output-format csv -- python3 tools/kdispatch.py ;;
         kcu2)   run kcu2 300 python tools/kcu2.py ;;
         kphasecu) run kphasecu 300 python tools/kphase_cu.py ;;
         cumask) run cumask 120 python tools/probe_cumask.py ;;

@@ -285,6 +285,11 @@ class ElasticBuffer(ExchangeMixin):
         the value is kept in the handle for API compatibility (and is what `num_sms` means
         to callers that pass it through)."""
         assert num_scaleout_topk == 0
+        key = (num_experts, num_topk, rdma_gbs, nvlink_gbs, sm_read_gbs, sm_write_gbs, self.prefer_overlap_with_compute,
+               os.environ.get('EP_XGMI_GBS'))
+        memo = self.__dict__.setdefault('_num_sms_memo', {})       # every dispatch asks (host time)
+        if key in memo:
+            return memo[key]
         nvlink_gbs = nvlink_gbs or float(os.environ.get('EP_XGMI_GBS', 7 * 64))
         num_device_sms = torch.cuda.get_device_properties(self.device).multi_processor_count if self.use_cuda else 256
 
@@ -300,7 +305,8 @@ class ElasticBuffer(ExchangeMixin):
             num_sms = max(nvlink_gbs / traffic * sm_read / sm_read_gbs, nvlink_gbs / traffic * sm_write / sm_write_gbs)
         num_sms = align(max(4, math.ceil(num_sms * 1.25)), 2)
         num_sms = num_sms if self.prefer_overlap_with_compute else max(num_sms, 64)
-        return min(num_sms, num_device_sms)
+        memo[key] = min(num_sms, num_device_sms)
+        return memo[key]
 
     def get_theoretical_num_qps(self, num_sms: int) -> int:
         num_qps = min(num_sms, 8 + 1)
@@ -457,11 +463,22 @@ class ElasticBuffer(ExchangeMixin):
         K = num_topk
         epr = num_experts // R
         self._note_capture()
-        compute_stream = self._prologue(previous_event, allocate_on_comm_stream)
+        # a call that neither overlaps nor waits on events runs on the caller's stream (as the combine:
+        # the same ordering without the two cross-stream hops)
+        sync_mode = self._sync_mode(previous_event, previous_event_before_epilogue, async_with_compute_stream,
+                                    allocate_on_comm_stream)
+        compute_stream = None if sync_mode else self._prologue(previous_event, allocate_on_comm_stream)
         kern = self.kernels
-        with self._stream_ctx():
+        with (self._null_ctx() if sync_mode else self._stream_ctx()):
             dev = x.device
             stream = torch.cuda.current_stream() if self.use_cuda else None
+            if sync_mode and self.use_cuda and R > 1 and self.transport == 'xgmi' and not self._capturing:
+                # the window is shared by every call: order this call after the earlier calls' work on
+                # the comm / phase-B / CU-budget streams that still reads it
+                for other in [self.comm_stream, getattr(self, '_stream_b', None)] + \
+                        [v[1] for k, v in _BUDGET_STREAMS.items() if k[0] == self.device.index]:
+                    if other is not None and other != stream:
+                        stream.wait_stream(other)
             idx64 = topk_idx if topk_idx.dtype == torch.int64 else topk_idx.to(torch.int64)
             idx64 = idx64.contiguous()
             w = topk_weights.contiguous() if topk_weights is not None else None
@@ -700,8 +717,9 @@ class ElasticBuffer(ExchangeMixin):
             # received ones are -1 (dispatch_count), non-expanded outputs there are zeros / -1
             num_recv = N
             cloned_idx = topk_idx.clone() if do_handle_copy else topk_idx
-        event = self._epilogue([x, sf, topk_idx, topk_weights, out_x, out_sf, out_idx, out_w, meta],
-                               compute_stream, allocate_on_comm_stream, async_with_compute_stream)
+        event = None if sync_mode else self._epilogue([x, sf, topk_idx, topk_weights, out_x, out_sf, out_idx, out_w,
+                                                       meta], compute_stream, allocate_on_comm_stream,
+                                                      async_with_compute_stream)
         is_cached = handle is not None
         if not is_cached:
             handle = EPHandle(do_expand, num_experts, expert_alignment, num_max_tokens_per_rank, num_sms,

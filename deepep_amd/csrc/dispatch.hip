@@ -229,21 +229,38 @@ notify_assign_kernel(const int64_t* __restrict__ topk_idx, int T, int K, int E, 
             dst_slot[static_cast<int64_t>(t) * R + r] = slot;
         }
     }
-    // the totals, grid-strided: expert counts (sum of the workgroups' histograms), per-destination
-    // tokens and send offsets (workgroup 0), tail blocks no count workgroup covered (zeros)
-    for (int e = blk * kNotifyTok + tid; e < E; e += grid * kNotifyTok) {
+    // the totals, grid-strided: expert counts (sum of the workgroups' histograms, 16 loads in flight
+    // per thread), per-destination tokens and send offsets (workgroup 0), tail blocks no count
+    // workgroup covered (zeros)
+    constexpr int kBatch = 16;
+    auto column_sum = [&](const int32_t* __restrict__ base, int64_t stride) {
         int c = 0;
-        for (int j = 0; j < nblk; ++j) c += ws_hist[static_cast<int64_t>(j) * E + e];
+        for (int j0 = 0; j0 < nblk; j0 += kBatch) {
+            int v[kBatch];
+#pragma unroll
+            for (int j = 0; j < kBatch; ++j) v[j] = j0 + j < nblk ? base[static_cast<int64_t>(j0 + j) * stride] : 0;
+#pragma unroll
+            for (int j = 0; j < kBatch; ++j) c += v[j];
+        }
+        return c;
+    };
+    for (int e = blk * kNotifyTok + tid; e < E; e += grid * kNotifyTok) {
         const int r = e / epr;
-        notify[r * W + 1 + (e - r * epr)] = c;
+        notify[r * W + 1 + (e - r * epr)] = column_sum(ws_hist + e, E);
     }
-    if (blk == 0 && tid < R) {
-        int total = 0, before = 0;
-        for (int j = 0; j < nblk; ++j) total += ws_cnt[static_cast<int64_t>(j) * R + tid];
-        for (int q = 0; q < tid; ++q)
-            for (int j = 0; j < nblk; ++j) before += ws_cnt[static_cast<int64_t>(j) * R + q];
-        notify[tid * W] = total;
-        send_offsets[tid] = before;
+    if (blk == 0) {
+        __syncthreads();                                 // s_base is free again
+        if (tid < R) {
+            const int total = column_sum(ws_cnt + tid, R);
+            s_base[tid] = total;
+            notify[tid * W] = total;
+        }
+        __syncthreads();
+        if (tid < R) {
+            int before = 0;
+            for (int q = 0; q < tid; ++q) before += s_base[q];
+            send_offsets[tid] = before;
+        }
     }
     const int covered = nblk * (kNotifyTok / 64);
     for (int i = blk * kNotifyTok + tid; i < R * nb; i += grid * kNotifyTok) {

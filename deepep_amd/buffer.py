@@ -498,6 +498,7 @@ class ElasticBuffer(ExchangeMixin):
             use_xgmi = R > 1 and self.transport == 'xgmi' and self.use_cuda
             padded = sync_free and R > 1 and not use_xgmi        # worst-case-padded RCCL exchange
             peer_offsets = None
+            host_notify = None                # one rank, host-synced: the counts' D2H, read after the copy launch
             counts = cached._counts if cached is not None else None
             x_bytes = x.contiguous().view(torch.uint8).view(T, H * x.element_size())
             sf_bytes = sf.contiguous().view(torch.uint8).view(T, sf.shape[1] * sf.element_size()) if sf is not None else None
@@ -551,7 +552,6 @@ class ElasticBuffer(ExchangeMixin):
                 else:
                     recv_notify = torch.empty_like(notify)
                     self._a2a(recv_notify, notify)
-                host_notify = None
                 if sync_free:
                     # no CPU sync: the sizes stay on the device; launches are sized for the worst case (one
                     # rank: T rows both ways, which a cached dispatch over this handle reuses)
@@ -637,50 +637,37 @@ class ElasticBuffer(ExchangeMixin):
                 out_idx = None if do_expand else torch.empty((N, K), dtype=torch.int64, device=dev)
                 nblocks = (N + DISPATCH_BLOCK_ROWS - 1) // DISPATCH_BLOCK_ROWS
                 block_counts = torch.empty((nblocks, epr), dtype=torch.int32, device=dev)
-                kern.dispatch_count(recv_packed, layout, N, r, epr, None, meta, out_idx, block_counts,
-                                    pad_rows=pad_rows, row_map=row_map, rank_counts=recv_counts_t,
-                                    psum_out=psum_rank, stream=stream)
                 expert_counts = torch.empty((epr,), dtype=torch.int32, device=dev)
                 psum_expert = torch.empty((epr,), dtype=torch.int32, device=dev)
-                kern.dispatch_scan(block_counts, epr, expert_alignment, do_expand, expert_counts, psum_expert,
-                                   stream=stream)
+                # worst-case expanded rows (the count is known after the notify): the inverse map of the
+                # slots for the blocked destination-major copy
+                inv = torch.empty((N * min(K, epr) + (expert_alignment - 1) * epr,), dtype=torch.int32,
+                                  device=dev) if do_expand else None
+                block_offsets = block_counts if do_expand else None
+                # count -> scan -> slots (expanded; else metadata slot columns -1), back to back
+                kern.dispatch_receive(recv_packed, layout, N, r, epr, recv_counts_t, psum_rank, meta, out_idx,
+                                      block_counts, expert_alignment, do_expand, expert_counts, psum_expert, inv=inv,
+                                      pad_rows=pad_rows, row_map=row_map, stream=stream)
                 # known since the notify; [] without a CPU sync (as the reference's handle)
                 aligned_l = [] if sync_free or host_notify is not None else \
                     [align(c, expert_alignment) for c in expert_counts_l]
                 if cumulative_local_expert_recv_stats is not None:
                     cumulative_local_expert_recv_stats += expert_counts.to(cumulative_local_expert_recv_stats.dtype)
                 self._before_epilogue(previous_event_before_epilogue)
-                if do_expand:
-                    # worst-case expanded rows (the count below is known after the notify): the inverse
-                    # map of the slots for the blocked destination-major copy
-                    inv = torch.empty((N * min(K, epr) + (expert_alignment - 1) * epr,), dtype=torch.int32,
-                                      device=dev)
-                    block_offsets = block_counts
-                    kern.dispatch_slots(recv_packed, layout, N, r, epr, block_counts, meta, inv=inv, row_map=row_map,
-                                        stream=stream)
-                else:
-                    meta[:, 2:] = -1
                 copy_meta, copy_rows = meta, N
-                if host_notify is not None:
-                    # one rank, host-synced: the counts have reached the host meanwhile; the launches above
-                    # covered all T tokens (rows past the received ones hold metadata -1), the handle and the
-                    # non-expanded outputs take the received rows
-                    host = host_notify.wait()
-                    send_counts_l = recv_counts_l = [host[0]]
-                    expert_counts_l = host[1:1 + epr]
-                    aligned_l = [align(c, expert_alignment) for c in expert_counts_l]
-                    N = host[0]
-                    meta = meta[:N]
-                    out_idx = out_idx[:N] if out_idx is not None else None
             num_unaligned = expert_counts
+            # one rank, host-synced (host_notify): every launch, the copy included, is sized as without a
+            # CPU sync (all T tokens) while the counts travel to the host; the outputs are then the exact
+            # leading rows of those allocations
+            deferred = host_notify is not None
+            worst_tokens = num_max_tokens_per_rank * R if sync_free else T
             if do_expand and cached is not None:
                 num_expanded = cached.num_expanded_tokens
                 alloc = torch.zeros if do_zero_padding else torch.empty
                 n_rows = num_expanded
-            elif do_expand and sync_free:
+            elif do_expand and (sync_free or deferred):
                 # worst case of buffer.hpp:1067-1069: every token in min(K, local experts) experts
-                num_expanded = align(num_max_tokens_per_rank * R * min(K, epr) + (expert_alignment - 1) * epr,
-                                     expert_alignment)
+                num_expanded = align(worst_tokens * min(K, epr) + (expert_alignment - 1) * epr, expert_alignment)
                 alloc = torch.zeros if do_zero_padding else torch.empty
                 n_rows = num_expanded
             elif do_expand:
@@ -710,6 +697,21 @@ class ElasticBuffer(ExchangeMixin):
                                error_flag=sym.error_flag if use_xgmi else None,
                                inv=inv if do_expand else None, block_offsets=block_offsets if do_expand else None,
                                expert_end=psum_expert if do_expand else None, row_map=row_map, stream=stream)
+            if deferred:
+                # the counts reached the host while the kernels ran: the handle and the outputs take the
+                # received rows / the exact expanded rows (leading views of the allocations above)
+                host = host_notify.wait()
+                send_counts_l = recv_counts_l = [host[0]]
+                expert_counts_l = host[1:1 + epr]
+                aligned_l = [align(c, expert_alignment) for c in expert_counts_l]
+                N = host[0]
+                n_rows = sum(aligned_l) if do_expand else N
+                num_expanded = n_rows if do_expand else N
+                meta = meta[:N]
+                out_idx = out_idx[:N] if out_idx is not None else None
+                out_x = out_x[:n_rows]
+                out_sf = out_sf[:n_rows] if out_sf is not None else None
+                out_w = out_w[:n_rows] if out_w is not None else None
             recv_idx64 = out_idx
             if out_idx is not None and topk_idx.dtype != torch.int64:
                 out_idx = out_idx.to(topk_idx.dtype)

@@ -371,7 +371,8 @@ __global__ void __launch_bounds__(kBlockRows)
 count_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int idx_off, int src_off, int N, int K,
              int rank, int epr, const int32_t* __restrict__ recv_counts, int counts_stride, int32_t* __restrict__ psum_out,
              int R, int pad_rows, int32_t* __restrict__ row_map,
-             int32_t* __restrict__ meta, int64_t* __restrict__ recv_topk_idx, int32_t* __restrict__ block_counts) {
+             int32_t* __restrict__ meta, int64_t* __restrict__ recv_topk_idx, int32_t* __restrict__ block_counts,
+             int fill_slots) {
     extern __shared__ int32_t s_hist[];                 // [epr]
     __shared__ int32_t rank_psum[64];                   // inclusive prefix of rows per source rank
     for (int e = threadIdx.x; e < epr; e += kBlockRows) s_hist[e] = 0;
@@ -416,6 +417,8 @@ count_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int idx_off,
         meta[mrow] = *reinterpret_cast<const int32_t*>(row + src_off);
         meta[mrow + 1] = src_rank * K + master;
     }
+    if (fill_slots && i < N)                            // non-expanded: no expanded slots
+        for (int k = 0; k < K; ++k) meta[static_cast<int64_t>(i) * (K + 2) + 2 + k] = -1;
     __syncthreads();
     if (blockIdx.x * kBlockRows < N)                    // (N == 0: the one workgroup formed psum_out only)
         for (int e = threadIdx.x; e < epr; e += kBlockRows)
@@ -814,8 +817,37 @@ int deepep_dispatch_count(const void* packed, int64_t row_bytes, int idx_off, in
                        reinterpret_cast<hipStream_t>(stream), static_cast<const uint8_t*>(packed), row_bytes,
                        idx_off, src_off, num_recv, num_topk, rank, num_local_experts, recv_rank_psum,
                        recv_counts_stride, psum_out, num_ranks, pad_rows, row_map, src_metadata, recv_topk_idx,
-                       block_counts);
+                       block_counts, 0);
     return launch_status("dispatch_count");
+}
+
+int deepep_dispatch_receive(const void* packed, int64_t row_bytes, int idx_off, int src_off, int num_recv,
+                            int num_topk, int rank, int num_local_experts, const int32_t* recv_counts,
+                            int num_ranks, int recv_counts_stride, int32_t* psum_out, int pad_rows, int32_t* row_map,
+                            int32_t* src_metadata, int64_t* recv_topk_idx, int32_t* block_counts,
+                            int expert_alignment, int expanded, int32_t* expert_counts, int32_t* psum_expert,
+                            int32_t* inv, deepep_stream_t stream) {
+    if (num_recv < 0 || num_topk < 1 || num_topk > 32 || num_local_experts < 1 || num_local_experts > 1024 ||
+        num_ranks < 1 || num_ranks > 64 || recv_counts_stride < 1 || recv_counts == nullptr || psum_out == nullptr ||
+        (num_recv > 0 && (src_metadata == nullptr || block_counts == nullptr || packed == nullptr)) ||
+        pad_rows < 0 || (num_recv > 0 && pad_rows > 0 && row_map == nullptr) ||
+        static_cast<int64_t>(pad_rows) * num_ranks >= (int64_t(1) << 31) || expert_alignment < 1 ||
+        expert_counts == nullptr || psum_expert == nullptr ||
+        static_cast<int64_t>(num_recv) * num_topk >= (int64_t(1) << 31))
+        return deepep_amd_set_error(DEEPEP_ERR_INVALID_ARG, "dispatch_receive: invalid arguments");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const int nblocks = (num_recv + kBlockRows - 1) / kBlockRows;
+    hipLaunchKernelGGL(count_kernel, dim3(std::max(nblocks, 1)), dim3(kBlockRows), num_local_experts * 4, s,
+                       static_cast<const uint8_t*>(packed), row_bytes, idx_off, src_off, num_recv, num_topk, rank,
+                       num_local_experts, recv_counts, recv_counts_stride, psum_out, num_ranks, pad_rows, row_map,
+                       src_metadata, recv_topk_idx, block_counts, expanded ? 0 : 1);
+    hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, s, block_counts, nblocks, num_local_experts,
+                       expert_alignment, expanded, expert_counts, psum_expert);
+    if (expanded && nblocks > 0)
+        hipLaunchKernelGGL(slots_kernel, dim3(nblocks), dim3(kBlockRows), num_local_experts * kSlotWaves * 8, s,
+                           static_cast<const uint8_t*>(packed), row_bytes, idx_off, num_recv, num_topk, rank,
+                           num_local_experts, block_counts, src_metadata, inv, row_map);
+    return launch_status("dispatch_receive");
 }
 
 int deepep_dispatch_scan(int32_t* block_counts, int num_blocks, int num_local_experts, int expert_alignment,

@@ -291,6 +291,27 @@ class HipKernels:
             ptr(recv_topk_idx), ptr(block_counts), _stream_handle(stream))
         _lib.check(rc, 'dispatch_count')
 
+    def dispatch_receive(self, packed, layout: RowLayout, num_recv, rank, num_local_experts, rank_counts, psum_out,
+                         meta, recv_topk_idx, block_counts, expert_alignment, expanded, expert_counts, psum_expert,
+                         inv=None, pad_rows: int = 0, row_map=None, stream=None):
+        """count (counts mode) -> scan -> slots (expanded) in one call: the receive side's launches back to
+        back.  Non-expanded: meta columns 2.. become -1."""
+        _require(rank_counts.dim() == 1 and rank_counts.dtype == torch.int32 and rank_counts.stride(0) >= 1,
+                 'rank_counts must be an int32 [num_ranks] view')
+        R = rank_counts.shape[0]
+        _require(psum_out.dtype == torch.int32 and psum_out.is_contiguous() and psum_out.numel() == R,
+                 'psum_out must be contiguous int32 [num_ranks]')
+        _require(pad_rows == 0 or (row_map is not None and row_map.dtype == torch.int32 and
+                                   row_map.numel() >= num_recv and packed.shape[0] >= pad_rows * R),
+                 'padded receive rows need a row map and R * pad_rows packed rows')
+        _require(inv is None or (inv.dtype == torch.int32 and inv.is_contiguous()), 'inv int32')
+        rc = self.lib.deepep_dispatch_receive(
+            ptr(packed), layout.row_bytes, layout.idx_off, layout.src_off, num_recv, layout.num_topk, rank,
+            num_local_experts, ptr(rank_counts), R, rank_counts.stride(0), ptr(psum_out), pad_rows, ptr(row_map),
+            ptr(meta), ptr(recv_topk_idx), ptr(block_counts), expert_alignment, int(expanded), ptr(expert_counts),
+            ptr(psum_expert), ptr(inv), _stream_handle(stream))
+        _lib.check(rc, 'dispatch_receive')
+
     def dispatch_scan(self, block_counts, num_local_experts, expert_alignment, expanded, expert_counts,
                       psum_expert, stream=None):
         rc = self.lib.deepep_dispatch_scan(ptr(block_counts), block_counts.shape[0], num_local_experts,

@@ -250,6 +250,16 @@ int deepep_dispatch_count(const void* packed, int64_t row_bytes, int idx_off, in
                           int32_t* src_metadata, int64_t* recv_topk_idx, int32_t* block_counts,
                           deepep_stream_t stream);
 
+/* Passes 1-3 in one call (the launches back to back, no host work between them): deepep_dispatch_count in
+ * counts mode (recv_counts_stride >= 1, psum_out required), deepep_dispatch_scan, and -- expanded -- the
+ * slots pass (inv optional); non-expanded, src_metadata columns 2.. are set to -1. */
+int deepep_dispatch_receive(const void* packed, int64_t row_bytes, int idx_off, int src_off, int num_recv,
+                            int num_topk, int rank, int num_local_experts, const int32_t* recv_counts,
+                            int num_ranks, int recv_counts_stride, int32_t* psum_out, int pad_rows, int32_t* row_map,
+                            int32_t* src_metadata, int64_t* recv_topk_idx, int32_t* block_counts,
+                            int expert_alignment, int expanded, int32_t* expert_counts, int32_t* psum_expert,
+                            int32_t* inv, deepep_stream_t stream);
+
 /* Pass 2: block_counts becomes each block's first slot inside its expert group (expert
  * groups start at aligned offsets); expert_counts = rows per expert; psum_expert as the reference
  * handle's psum_num_recv_tokens_per_expert (expanded: aligned start + count; else inclusive aligned). */

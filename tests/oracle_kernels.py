@@ -171,6 +171,18 @@ class OracleKernels:
             chunk = chunk[chunk >= 0]
             block_counts[b] += torch.bincount(chunk, minlength=epr).to(torch.int32)
 
+    def dispatch_receive(self, packed, layout, num_recv, rank, num_local_experts, rank_counts, psum_out, meta,
+                         recv_topk_idx, block_counts, expert_alignment, expanded, expert_counts, psum_expert,
+                         inv=None, pad_rows=0, row_map=None, stream=None):
+        self.dispatch_count(packed, layout, num_recv, rank, num_local_experts, None, meta, recv_topk_idx, block_counts,
+                            pad_rows=pad_rows, row_map=row_map, rank_counts=rank_counts, psum_out=psum_out)
+        self.dispatch_scan(block_counts, num_local_experts, expert_alignment, expanded, expert_counts, psum_expert)
+        if expanded:
+            self.dispatch_slots(packed, layout, num_recv, rank, num_local_experts, block_counts, meta, inv=inv,
+                                row_map=row_map)
+        else:
+            meta[:num_recv, 2:] = -1
+
     def dispatch_scan(self, block_counts, num_local_experts, expert_alignment, expanded, expert_counts, psum_expert,
                       stream=None):
         counts = block_counts.sum(dim=0).to(torch.int64)

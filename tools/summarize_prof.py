@@ -68,6 +68,7 @@ def pmc_phases(out, meta_json, *paths):
     def kind(name):
         # the dispatch copy is `copy_kernel(...)`; torch's dtype conversions (`..._copy_kernel_cuda`) also
         # contain the substring, and counting them as the copy gave round 1's "anomaly"
+        name = name[5:] if name.startswith('void ') else name
         if name.startswith('copy_kernel(') or name.startswith('copy_expanded_kernel<'):
             return 'copy'
         if 'combine_rows_kernel<2' in name:

@@ -199,11 +199,20 @@ notify_assign_kernel(const int64_t* __restrict__ topk_idx, int T, int K, int E, 
     const int blk = blockIdx.x, grid = gridDim.x;
     const int epr = E / R;
     const int64_t W = 1 + epr + 2 * static_cast<int64_t>(nb);
-    if (tid < R) {
-        int base = 0;
-        for (int j = 0; j < blk && j < nblk; ++j) base += ws_cnt[static_cast<int64_t>(j) * R + tid];
-        s_base[tid] = base;
-    }
+    constexpr int kBatch = 16;                           // loads in flight per thread
+    // sum of base[j * stride] over j < n
+    auto column_sum = [&](const int32_t* __restrict__ base, int64_t stride, int n) {
+        int c = 0;
+        for (int j0 = 0; j0 < n; j0 += kBatch) {
+            int v[kBatch];
+#pragma unroll
+            for (int j = 0; j < kBatch; ++j) v[j] = j0 + j < n ? base[static_cast<int64_t>(j0 + j) * stride] : 0;
+#pragma unroll
+            for (int j = 0; j < kBatch; ++j) c += v[j];
+        }
+        return c;
+    };
+    if (tid < R) s_base[tid] = column_sum(ws_cnt + tid, R, min(blk, nblk));
     const int t = blk * kNotifyTok + tid;
     uint64_t mask = 0;
     if (t < T)
@@ -229,29 +238,16 @@ notify_assign_kernel(const int64_t* __restrict__ topk_idx, int T, int K, int E, 
             dst_slot[static_cast<int64_t>(t) * R + r] = slot;
         }
     }
-    // the totals, grid-strided: expert counts (sum of the workgroups' histograms, 16 loads in flight
-    // per thread), per-destination tokens and send offsets (workgroup 0), tail blocks no count
-    // workgroup covered (zeros)
-    constexpr int kBatch = 16;
-    auto column_sum = [&](const int32_t* __restrict__ base, int64_t stride) {
-        int c = 0;
-        for (int j0 = 0; j0 < nblk; j0 += kBatch) {
-            int v[kBatch];
-#pragma unroll
-            for (int j = 0; j < kBatch; ++j) v[j] = j0 + j < nblk ? base[static_cast<int64_t>(j0 + j) * stride] : 0;
-#pragma unroll
-            for (int j = 0; j < kBatch; ++j) c += v[j];
-        }
-        return c;
-    };
+    // the totals, grid-strided: expert counts (sum of the workgroups' histograms), per-destination
+    // tokens and send offsets (workgroup 0), tail blocks no count workgroup covered (zeros)
     for (int e = blk * kNotifyTok + tid; e < E; e += grid * kNotifyTok) {
         const int r = e / epr;
-        notify[r * W + 1 + (e - r * epr)] = column_sum(ws_hist + e, E);
+        notify[r * W + 1 + (e - r * epr)] = column_sum(ws_hist + e, E, nblk);
     }
     if (blk == 0) {
         __syncthreads();                                 // s_base is free again
         if (tid < R) {
-            const int total = column_sum(ws_cnt + tid, R);
+            const int total = column_sum(ws_cnt + tid, R, nblk);
             s_base[tid] = total;
             notify[tid * W] = total;
         }
@@ -425,50 +421,68 @@ count_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int idx_off,
             block_counts[static_cast<int64_t>(blockIdx.x) * epr + e] = s_hist[e];
 }
 
-// One thread per local expert: offsets of every workgroup inside the expert's group, expert starts
-// aligned to expert_alignment, and the handle's prefix sums (elastic.py:36-45 semantics).  The
-// per-block counts are read 16 at a time so the loads of a thread are in flight together.
+// Thread (expert e, block group g) of 1024 threads: G = 1024 / epr groups of consecutive blocks, so a
+// warp-row of threads reads one block's counts for consecutive experts (coalesced) and every thread walks
+// ceil(nblocks / G) blocks with 16 loads in flight.  Pass 1: each group's partial count; then the experts'
+// totals, a workgroup scan of the aligned totals (expert group starts aligned to expert_alignment) and the
+// handle's prefix sums (elastic.py:36-45 semantics); pass 2: each block's first slot inside its expert
+// group = the group start + the earlier groups' partials + a running sum over the thread's blocks.
+// (Round 2 had one thread per expert walk every block: 32 busy threads and ~340 blocks at EP = 8.)
 __global__ void __launch_bounds__(1024)
 scan_kernel(int32_t* __restrict__ block_counts, int nblocks, int epr, int align, int expanded,
             int32_t* __restrict__ expert_counts, int32_t* __restrict__ psum_expert) {
     constexpr int kBatch = 16;
+    __shared__ int32_t s_part[1024];                     // [g][e]
     __shared__ int32_t s_aligned[1024];
-    const int e = threadIdx.x;
-    int total = 0;
-    if (e < epr) {
-        for (int b0 = 0; b0 < nblocks; b0 += kBatch) {
+    const int tid = threadIdx.x;
+    const int G = 1024 / epr;
+    const int e = tid % epr, g = tid / epr;
+    const bool active = g < G;
+    const int per = (nblocks + G - 1) / G;
+    const int b_lo = min(nblocks, g * per), b_hi = min(nblocks, b_lo + per);
+    int part = 0;
+    if (active)
+        for (int b0 = b_lo; b0 < b_hi; b0 += kBatch) {
             int c[kBatch];
 #pragma unroll
             for (int j = 0; j < kBatch; ++j)
-                c[j] = b0 + j < nblocks ? block_counts[static_cast<int64_t>(b0 + j) * epr + e] : 0;
+                c[j] = b0 + j < b_hi ? block_counts[static_cast<int64_t>(b0 + j) * epr + e] : 0;
 #pragma unroll
-            for (int j = 0; j < kBatch; ++j) total += c[j];
+            for (int j = 0; j < kBatch; ++j) part += c[j];
         }
-        expert_counts[e] = total;
-    }
-    s_aligned[e] = e < epr ? (total + align - 1) / align * align : 0;
+    if (active) s_part[tid] = part;
+    __syncthreads();
+    int total = 0;
+    if (tid < epr)
+        for (int q = 0; q < G; ++q) total += s_part[q * epr + tid];
+    const int aligned = tid < epr ? (total + align - 1) / align * align : 0;
+    s_aligned[tid] = aligned;
     __syncthreads();
     for (int off = 1; off < 1024; off <<= 1) {          // inclusive scan of the aligned group sizes
-        const int v = e >= off ? s_aligned[e - off] : 0;
+        const int v = tid >= off ? s_aligned[tid - off] : 0;
         __syncthreads();
-        s_aligned[e] += v;
+        s_aligned[tid] += v;
         __syncthreads();
     }
-    const int aligned = e < epr ? (total + align - 1) / align * align : 0;
-    const int start = s_aligned[e] - aligned;
-    if (e < epr) {
-        psum_expert[e] = expanded ? start + total : start + aligned;
-        int run = start;
-        for (int b0 = 0; b0 < nblocks; b0 += kBatch) {
-            int c[kBatch];
+    if (tid < epr) {
+        const int start = s_aligned[tid] - aligned;
+        expert_counts[tid] = total;
+        psum_expert[tid] = expanded ? start + total : start + aligned;
+        s_aligned[tid] = start;                           // read below by every group of expert tid
+    }
+    __syncthreads();
+    if (!active) return;
+    int run = s_aligned[e];
+    for (int q = 0; q < g; ++q) run += s_part[q * epr + e];
+    for (int b0 = b_lo; b0 < b_hi; b0 += kBatch) {
+        int c[kBatch];
 #pragma unroll
-            for (int j = 0; j < kBatch; ++j)
-                c[j] = b0 + j < nblocks ? block_counts[static_cast<int64_t>(b0 + j) * epr + e] : 0;
+        for (int j = 0; j < kBatch; ++j)
+            c[j] = b0 + j < b_hi ? block_counts[static_cast<int64_t>(b0 + j) * epr + e] : 0;
 #pragma unroll
-            for (int j = 0; j < kBatch; ++j) {
-                if (b0 + j < nblocks) block_counts[static_cast<int64_t>(b0 + j) * epr + e] = run;
-                run += c[j];
-            }
+        for (int j = 0; j < kBatch; ++j) {
+            if (b0 + j < b_hi) block_counts[static_cast<int64_t>(b0 + j) * epr + e] = run;
+            run += c[j];
         }
     }
 }

@@ -46,6 +46,7 @@ for step in "$@"; do
         profphase) run profphase 300 rocprofv3 --kernel-trace --stats -d $OUT/profphase -o prof --output-format csv -- python3 tools/kphase_prof.py ;;
         kcu)    run kcu 300 python tools/kcu.py ;;
         kdisp)  run kdisp 300 python tools/kdispatch.py ;;
+        koverlap) run koverlap 300 python tools/koverlap.py ;;
         kdispprof) export KDISPATCH_CPROFILE=1; run kdispprof 300 python tools/kdispatch.py; unset KDISPATCH_CPROFILE ;;
         profdisp) run profdisp 300 rocprofv3 --kernel-trace -d $OUT/profdisp -o prof --output-format csv -- python3 tools/kdispatch.py ;;
         kcu2)   run kcu2 300 python tools/kcu2.py ;;

@@ -189,9 +189,13 @@ class ElasticBuffer(ExchangeMixin):
         """Start the D2H of `src` (int32) into this buffer's pinned staging vector; .wait() returns the
         values.  One copy in flight per buffer: a dispatch waits for its own before it returns."""
         n = src.numel()
+        prev = getattr(self, '_host_copy_last', None)
+        if prev is not None:
+            prev.event.synchronize()      # a copy a failed call left in flight must not land on this one's
         if getattr(self, '_pinned', None) is None or self._pinned.numel() < n:
             self._pinned = torch.empty((max(n, 4096),), dtype=torch.int32, pin_memory=True)
-        return ElasticBuffer._HostCopy(src, self._pinned, stream)
+        self._host_copy_last = ElasticBuffer._HostCopy(src, self._pinned, stream)
+        return self._host_copy_last
 
     def _group_barrier(self) -> None:
         """torch.cuda.synchronize(); group barrier; synchronize (elastic.py:365-367)."""

@@ -33,6 +33,7 @@ for step in "$@"; do
         pcopy)  [ -f tools/libprobe_copy.so ] || hipcc --offload-arch=gfx950 -O3 -fPIC -shared -o tools/libprobe_copy.so tools/probe_copy.hip
                 run pcopy 600 python tools/probe_copy.py ;;
         kbisect) run kbisect 600 python tools/kbisect.py ;;
+        klayout) run klayout 300 python tools/klayout.py ;;
         kwaves) run kwaves 600 python tools/kbench_waves.py ;;
         kvar)   run kvar 300 python tools/kvar.py ;;
         kflush) run kflush 300 python tools/kflush.py ;;

@@ -442,6 +442,8 @@ def main():
     ap.add_argument('--no-loopback', action='store_true')
     ap.add_argument('--no-flushed', action='store_true',
                     help='skip the per-launch flushed timing (keeps a rocprof kernel average to back-to-back launches)')
+    ap.add_argument('--no-layout-ref', action='store_true',
+                    help='skip the token-major layout reference (keeps a rocprof kernel average to the product input)')
     args = ap.parse_args()
 
     multi = 'RANK' in os.environ and int(os.environ.get('WORLD_SIZE', '1')) > 1
@@ -595,6 +597,37 @@ def main():
         torch.cuda.synchronize()
         copy_gbps = 2 * y.numel() * 2 * 5 / (c0.elapsed_time(c1) * 1e-3) / 1e9
         del dst
+        # same-run layout reference (tools/klayout.py): the same kernel over the same rows with each token's
+        # K rows adjacent ([T, K] placement) instead of grouped by expert -- what the kernel reaches when
+        # the rows a workgroup reads at once are one contiguous run; output checked bit for bit
+        token_major = None
+        tab = plan.local_table.long()
+        if not args.no_layout_ref and bool((tab >= 0).all().item()):
+            pos = torch.arange(T * K, device=dev).view(T, K)
+            yt = torch.empty_like(y)
+            wt = torch.empty_like(ex_w)
+            yt[pos.reshape(-1)] = y[tab.reshape(-1)]
+            wt[pos.reshape(-1)] = ex_w[tab.reshape(-1)]
+            tab_t = pos.to(torch.int32)
+            ref_o, ref_w = out.clone(), out_w.clone()
+
+            def launch_t():
+                kern.combine_reduce(MODE_FUSED, yt, out, T, table=tab_t, row_weights=wt if weighted else None,
+                                    wtable=tab_t, wsrc=wt, out_weights=out_w, stream=stream)
+            for _ in range(5):
+                launch_t()
+            c0.record(stream)
+            for _ in range(args.steps):
+                launch_t()
+            c1.record(stream)
+            torch.cuda.synchronize()
+            t_us = c0.elapsed_time(c1) * 1e3 / args.steps
+            token_major = dict(kernel_us=round(t_us, 2), frac=round(bytes_rank / (t_us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4),
+                               bitwise_equal=bool(torch.equal(out, ref_o) and torch.equal(out_w, ref_w)),
+                               note='diagnostic only: the same kernel and bytes over the same rows placed token-major '
+                                    '(a token\'s K rows adjacent); the product input is expert-grouped')
+            del yt, wt, tab_t, ref_o, ref_w
+        del tab
         # The reduce phase of the EP > 1 single-reduction combine (allow_multiple_reduction=False): after
         # the exchange a rank's receive window holds its tokens' K unreduced rows at k * T_max + t (rows
         # of 2H + 16 bytes, weight in the tail); one weighted EPILOGUE launch reduces them.  Same
@@ -637,7 +670,8 @@ def main():
                         kernel_us_read_flushed_median=(None if kern_us_read_flushed is None
                                                        else round(kern_us_read_flushed, 2)),
                         bytes_per_launch=bytes_rank, in_region_us_per_step=round(comm_ms * 1e3, 2),
-                        same_run_d2d_copy_gbps=round(copy_gbps, 1), single_reduction_phase_b=single_b)
+                        same_run_d2d_copy_gbps=round(copy_gbps, 1), same_run_token_major_rows=token_major,
+                        single_reduction_phase_b=single_b)
 
     phases = su_line = None
     if world > 1:

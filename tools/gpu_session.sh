@@ -25,7 +25,7 @@ for step in "$@"; do
         benchc4) run bench_c4 600 python bench.py --fp8-dispatch --no-cpu-baseline --no-loopback ;;
         benchc5) run bench_c5 600 python bench.py --tokens 16384 --skew 4 --no-cpu-baseline --no-loopback ;;
         benchplain) run bench_plain 600 python bench.py --plain --no-cpu-baseline --no-loopback ;;
-        prof)   run rocprof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o prof --output-format csv -- python3 bench.py --no-cpu-baseline --no-loopback --no-flushed --steps 20 --warmup 5 ;;
+        prof)   run rocprof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o prof --output-format csv -- python3 bench.py --no-cpu-baseline --no-loopback --no-flushed --no-layout-ref --steps 20 --warmup 5 ;;
         kbench) run kbench 600 python tools/kbench.py ;;
         kalign) run kalign 600 python tools/kbench_align.py ;;
         kab)    run kab 600 python tools/kbench_ab.py ;;

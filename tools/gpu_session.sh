@@ -34,6 +34,7 @@ for step in "$@"; do
                 run pcopy 600 python tools/probe_copy.py ;;
         kbisect) run kbisect 600 python tools/kbisect.py ;;
         klayout) run klayout 300 python tools/klayout.py ;;
+        klayoutruns) export KLAYOUT_RUNS=1; run klayoutruns 400 python tools/klayout.py; unset KLAYOUT_RUNS ;;
         kwaves) run kwaves 600 python tools/kbench_waves.py ;;
         kvar)   run kvar 300 python tools/kvar.py ;;
         kflush) run kflush 300 python tools/kflush.py ;;

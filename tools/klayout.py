@@ -5,7 +5,11 @@ The same 65,536 rows and the same per-token sums, with the rows placed four ways
              the tokens reduced at one moment read ~all 256 expert regions at once (the product case);
   slot    -- [K, T]: row k * T + t (the single-reduction receive window's layout: 8 regions);
   token   -- [T, K]: row t * K + k (a token's 8 rows adjacent: one region);
-  random  -- a random permutation of the rows.
+  random  -- a random permutation of the rows;
+  pairs / quads -- a token's rows in runs of 2 / 4 adjacent rows, the runs at random places
+             (KLAYOUT_RUNS=1; how long a contiguous run has to be before the rate moves);
+  token_shuffled -- a token's rows adjacent, tokens in random order; slot_skewed -- [K, T] with each slot's
+             region shifted by 37 rows (KLAYOUT_RUNS=1).
 Each with the product's weighted reduction + weight pass-through and as a plain sum without it (the
 weights are gathered through the slot, so they follow the rows).  Every output is checked bitwise
 against the product's.  Interleaved over rounds, one JSON line per (round, variant) + medians.
@@ -44,13 +48,24 @@ def main():
     tt = torch.arange(T, device='cuda').view(T, 1)
     layouts = {'expert': table, 'slot': (kk * T + tt).expand(T, K), 'token': (tt * K + kk).expand(T, K),
                'random': torch.randperm(n, device='cuda')[(tt * K + kk).expand(T, K)]}
+    if os.environ.get('KLAYOUT_RUNS') == '1':
+        for name, g in (('pairs', 2), ('quads', 4)):
+            # runs of g adjacent rows: run j of token t at a random run slot, row k % g inside it
+            run = torch.randperm(n // g, device='cuda').view(T, K // g)
+            layouts[name] = run[:, kk.view(-1) // g] * g + kk % g
+        # a token's 8 rows adjacent but the tokens in random order (contiguity without one global sweep)
+        layouts['token_shuffled'] = (torch.randperm(T, device='cuda').view(T, 1) * K + kk).expand(T, K)
+        # [K, T] with each slot's region shifted by a non-power-of-two number of rows (8 sweeps, no aliasing)
+        pad = 37
+        layouts['slot_skewed'] = (kk * (T + pad) + tt).expand(T, K)
     data = {}
     for name, pos in layouts.items():
         if name == 'expert':
             data[name] = (y, ex_w, table.to(torch.int32).contiguous())
             continue
-        yl = torch.empty_like(y)
-        wl = torch.empty_like(ex_w)
+        rows = int(pos.max().item()) + 1
+        yl = torch.empty((rows, H), dtype=y.dtype, device='cuda')
+        wl = torch.empty((rows,), dtype=ex_w.dtype, device='cuda')
         yl[pos.reshape(-1)] = y[table.reshape(-1)]
         wl[pos.reshape(-1)] = ex_w[table.reshape(-1)]
         data[name] = (yl, wl, pos.to(torch.int32).contiguous())

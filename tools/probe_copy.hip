@@ -341,6 +341,9 @@ extern "C" int probe_copy(int variant, const void* x, const int32_t* dst, const 
         case 8: hipLaunchKernelGGL((gather_copy<8, 16>), grid((int64_t)(N + 7) / 8 * nch), dim3(256), 0, s, xx, inv, N, xb, o); break;
         case 40: hipLaunchKernelGGL((gather_copy<4, 0>), grid((int64_t)(N + 3) / 4 * nch), dim3(256), 0, s, xx, inv, N, xb, o); break;
         case 42: hipLaunchKernelGGL((gather_copy<4, 2>), grid((int64_t)(N + 3) / 4 * nch), dim3(256), 0, s, xx, inv, N, xb, o); break;
+        case 48: hipLaunchKernelGGL((gather_copy<4, 18>), grid((int64_t)(N + 3) / 4 * nch), dim3(256), 0, s, xx, inv, N, xb, o); break;
+        case 88: hipLaunchKernelGGL((gather_copy<8, 18>), grid((int64_t)(N + 7) / 8 * nch), dim3(256), 0, s, xx, inv, N, xb, o); break;
+        case 28: hipLaunchKernelGGL((gather_copy<2, 18>), grid((int64_t)(N + 1) / 2 * nch), dim3(256), 0, s, xx, inv, N, xb, o); break;
         case 100: launch_t<4, 2, 16>(xx, dst, T, K, xb, o, s); break;
         case 101: launch_t<8, 2, 16>(xx, dst, T, K, xb, o, s); break;
         case 102: launch_t<4, 4, 16>(xx, dst, T, K, xb, o, s); break;

@@ -46,14 +46,14 @@ def main():
     valid = idx >= 0
     count_e = torch.bincount(idx[valid], minlength=E)[:E]
     start_e = torch.cumsum(count_e, 0) - count_e
-    for tok_blk in (256, 128):
+    for tok_blk in [int(v) for v in os.environ.get('PCOPY_BLOCKS', '256,128').split(',') if v]:
         nbk = (T + tok_blk - 1) // tok_blk
         blk_of = (torch.arange(T, device='cuda') // tok_blk).view(T, 1).expand(T, K)
         cnt = torch.zeros((nbk, E), dtype=torch.int64, device='cuda')
         cnt.index_put_((blk_of[valid], idx[valid]), torch.ones_like(idx[valid]), accumulate=True)
         off = (start_e.view(1, E) + torch.cumsum(cnt, 0) - cnt).to(torch.int32).contiguous()
         cnt32 = cnt.to(torch.int32).contiguous()
-        for v in (3, 5, 6, 7, 8, 9, 10, 0, 3):
+        for v in [int(v) for v in os.environ.get('PCOPY_BLOCKED', '3,5,6,7,8,9,10,0,3').split(',')]:
             out.zero_()
             fn = lambda: lib.probe_blocked_copy(v, x.data_ptr(), inv.data_ptr(), off.data_ptr(), cnt32.data_ptr(),
                                                 nbk, E, xb, out.data_ptr(), s.cuda_stream)
@@ -63,7 +63,7 @@ def main():
             us = timeit(fn, s, iters=20)
             print(json.dumps(dict(variant=f'blocked tok{tok_blk} v{v}', us=round(us, 1), gbps=round(nbytes / us / 1e3, 1),
                                   equal=ok)), flush=True)
-    for v in (0, 300, 104, 0, 200, 201):
+    for v in [int(v) for v in os.environ.get('PCOPY_VARIANTS', '0,300,104,0,200,201').split(',') if v]:
         out.zero_()
         fn = lambda: lib.probe_copy(v, x.data_ptr(), dst.data_ptr(), inv.data_ptr(), T, K, N, xb, out.data_ptr(),
                                     s.cuda_stream)

@@ -29,7 +29,7 @@ from .exchange import ExchangeMixin
 from .handle import BlockCounts, CombinePlan, EPHandle, build_ep_plan, chunk_geometry
 from ._lib import DISPATCH_BLOCK_ROWS
 from .kernels import MODE_EPILOGUE, MODE_FUSED, MODE_LOCAL, RowLayout
-from .utils import align, ceil_div, value_or
+from .utils import align, ceil_div, check_torch_deterministic, value_or
 
 topk_idx_t = torch.int32 if int(os.environ.get('EP_NUM_TOPK_IDX_BITS', 64)) == 32 else torch.int64
 
@@ -433,6 +433,7 @@ class ElasticBuffer(ExchangeMixin):
         all-to-all, xGMI: the notify through the windows; graph-capturable).  A cached handle
         (`handle=...`) needs no sync.
         The notify also carries per-64-token-block counts, so the handle's combines never sync."""
+        check_torch_deterministic()
         num_topk = (handle.topk_idx if topk_idx is None else topk_idx).shape[1]
         num_sms = self.get_theoretical_num_sms(num_experts or handle.num_experts, num_topk) if num_sms == 0 else num_sms
         num_qps = self.get_theoretical_num_qps(num_sms) if num_qps == 0 else num_qps
@@ -828,6 +829,7 @@ class ElasticBuffer(ExchangeMixin):
         expanded row by its top-k weight inside the reduction (the gating-weighted sum of the
         legacy low_latency_combine, csrc/kernels/legacy/internode_ll.cu:1072-1135).  Requires
         the expanded layout and `topk_weights`.  The weights are still passed through."""
+        check_torch_deterministic()
         explicit_sms = num_sms
         if num_sms == 0 and self.combine_cu_mode == 'handle' and self.prefer_overlap_with_compute:
             explicit_sms = handle.num_sms          # the reference's SM-confined default (elastic.py:1086)

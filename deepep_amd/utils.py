@@ -11,3 +11,11 @@ def align(x: int, y: int) -> int:
 
 def value_or(value, default):
     return default if value is None else value
+
+
+def check_torch_deterministic() -> None:
+    """deep_ep/utils/envs.py:183-189: deterministic algorithms together with fill_uninitialized_memory make
+    torch.empty launch a fill kernel that may overlap the communication streams; the reference refuses the
+    combination in dispatch and combine (elastic.py:924, :1083), and so does this build."""
+    import torch
+    assert not (torch.are_deterministic_algorithms_enabled() and torch.utils.deterministic.fill_uninitialized_memory)

@@ -35,6 +35,7 @@ for step in "$@"; do
         kbisect) run kbisect 600 python tools/kbisect.py ;;
         pcopydst) export PCOPY_BLOCKS=128 PCOPY_BLOCKED=9,9 PCOPY_VARIANTS=1,4,8,40,42,48,88,28,200,201,48; run pcopydst 600 python tools/probe_copy.py; unset PCOPY_BLOCKS PCOPY_BLOCKED PCOPY_VARIANTS ;;
         klayout) run klayout 300 python tools/klayout.py ;;
+        kwin)   run kwin 300 python tools/kwin.py ;;
         klayoutruns) export KLAYOUT_RUNS=1; run klayoutruns 400 python tools/klayout.py; unset KLAYOUT_RUNS ;;
         kwaves) run kwaves 600 python tools/kbench_waves.py ;;
         kvar)   run kvar 300 python tools/kvar.py ;;

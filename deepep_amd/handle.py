@@ -115,7 +115,8 @@ def build_ep_plan(kern, handle: 'EPHandle', *, num_ranks: int, rank: int, single
     T, K = handle.topk_idx.shape
     cnt = handle._counts
     nb, bpc, C = chunk_geometry(T_max, num_chunks)
-    assert cnt.num_blocks == nb, 'handle block counts do not match num_max_tokens_per_rank'
+    if cnt.num_blocks != nb:
+        raise RuntimeError('deepep_amd: handle block counts do not match num_max_tokens_per_rank')
     expanded = handle.do_expand
     rank_layout = R <= K                             # use_rank_layout (combine_utils.cuh:8-13)
     dev = handle.recv_src_metadata.device

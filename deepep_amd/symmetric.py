@@ -56,7 +56,8 @@ class SymmetricBuffer:
             bases = [int(b) for b in exchange(self.base)]
         else:
             bases = self._ipc_exchange(group)
-        assert len(bases) == num_ranks and bases[rank] == self.base
+        if len(bases) != num_ranks or bases[rank] != self.base:
+            raise RuntimeError('deepep_amd: window exchange returned inconsistent bases')
         self.bases = bases
         self.bases_dev = torch.tensor(bases, dtype=torch.int64, device=device)     # flags live at offset 0
         self.data_bases_dev = self.bases_dev + HEADER_BYTES
@@ -133,9 +134,13 @@ class SymmetricBuffer:
     def put_notify(self, records: torch.Tensor, stream) -> None:
         """Store records[d] (int32 [num_ranks, n], n * 4 a multiple of 16 bytes) into slot `rank` of rank d's
         notify area (the dispatch notify's transport); a barrier must follow before it is read."""
-        assert records.dtype == torch.int32 and records.is_contiguous() and records.shape[0] == self.num_ranks
+        # explicit checks (not asserts, which python -O strips): the put's extent must stay inside the notify area
+        if not (records.dtype == torch.int32 and records.is_contiguous() and records.shape[0] == self.num_ranks):
+            raise RuntimeError('deepep_amd: notify records must be contiguous int32 [num_ranks, n]')
         n = records.shape[1]
-        assert (n * 4) % 16 == 0 and self.num_ranks * n * 4 <= HEADER_BYTES - NOTIFY_OFFSET, 'notify too large'
+        if (n * 4) % 16 != 0 or self.num_ranks * n * 4 > HEADER_BYTES - NOTIFY_OFFSET:
+            raise RuntimeError(f'deepep_amd: notify record of {n} ints x {self.num_ranks} ranks does not fit the '
+                               f'{HEADER_BYTES - NOTIFY_OFFSET}-byte notify area in 16-byte units')
         handle = stream.cuda_stream if stream is not None else torch.cuda.current_stream().cuda_stream
         _lib.check(self.lib.deepep_sym_put(records.data_ptr(), n * 4, self.bases_dev.data_ptr(), self.num_ranks,
                                            NOTIFY_OFFSET + self.rank * n * 4, self.error_flag.data_ptr(), handle),

@@ -26,6 +26,9 @@ for step in "$@"; do
         benchc5) run bench_c5 600 python bench.py --tokens 16384 --skew 4 --no-cpu-baseline --no-loopback ;;
         benchplain) run bench_plain 600 python bench.py --plain --no-cpu-baseline --no-loopback ;;
         prof)   run rocprof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o prof --output-format csv -- python3 bench.py --no-cpu-baseline --no-loopback --no-flushed --no-layout-ref --steps 20 --warmup 5 ;;
+        profdefault) # the driver's exact command under rocprofv3; per-loop averages from the kernel trace
+                run rocprofdef 900 rocprofv3 --kernel-trace --stats -d $OUT/profdef -o prof --output-format csv -- python3 bench.py
+                python tools/summarize_prof.py timed $OUT/profdef/prof_kernel_trace.csv "combine_rows_kernel<2," $OUT/profdef_timed.md "combine steps + kernel-alone loop (value; roofline.kernel_us),token-major layout reference (roofline.same_run_token_major_rows)" ;;
         kbench) run kbench 600 python tools/kbench.py ;;
         kalign) run kalign 600 python tools/kbench_align.py ;;
         kab)    run kab 600 python tools/kbench_ab.py ;;

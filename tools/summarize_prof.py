@@ -1,6 +1,7 @@
 """Summaries of rocprofv3 output for profiles/ (kernel stats and PMC traffic).
 
   python tools/summarize_prof.py stats  <kernel_stats.csv> <out.md>
+  python tools/summarize_prof.py timed  <kernel_trace.csv> <kernel-name substring> <out.md> [labels,...]
   python tools/summarize_prof.py pmc    <out.json> <workload> <bytes_per_launch> <counter_csv>...
 The PMC summary applies the gfx950 corrections of MI355X_MICROARCH.md (HBM section):
 FETCH_SIZE (KiB) counts half the bytes of a wide coalesced read stream -> x2; WRITE_SIZE (KiB)
@@ -20,6 +21,36 @@ def stats(path, out):
         short = name.split('(')[0][:90]
         lines.append(f"| `{short}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.2f} | {float(r['MinNs']) / 1e3:.2f} | "
                      f"{float(r['MaxNs']) / 1e3:.2f} | {float(r['Percentage']):.1f} |")
+    open(out, 'w').write('\n'.join(lines) + '\n')
+    print('\n'.join(lines))
+
+
+def timed(path, needle, out, labels=''):
+    """Per-loop averages of one kernel from a --kernel-trace run of the default `python bench.py`: the
+    maximal runs of >= 50 back-to-back dispatches of the kernel (in dispatch order), each averaged
+    without its first 5 launches (warmup).  bench.py's loops of the fused kernel come in a fixed order
+    (the timed combine steps of `value`, the kernel-alone loop of `roofline.kernel_us`, the token-major
+    layout reference), so run i is loop i; the whole-process --stats average mixes them with the
+    flushed single launches."""
+    rows = [r for r in csv.DictReader(open(path))]
+    rows.sort(key=lambda r: int(r['Dispatch_Id']))
+    runs, cur = [], []
+    for r in rows:
+        if needle in r['Kernel_Name']:
+            cur.append((int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3)
+        else:
+            if len(cur) >= 50:
+                runs.append(cur)
+            cur = []
+    if len(cur) >= 50:
+        runs.append(cur)
+    names = [v for v in labels.split(',') if v] if labels else []
+    lines = [f'Kernel `{needle}`: loops of >= 50 back-to-back launches (first 5 of each dropped)', '',
+             '| loop | launches | avg us | min us | max us |', '|---|---|---|---|---|']
+    for i, run in enumerate(runs):
+        body = run[5:] if len(run) > 10 else run
+        name = names[i] if i < len(names) else f'loop {i + 1}'
+        lines.append(f'| {name} | {len(body)} | {sum(body) / len(body):.2f} | {min(body):.2f} | {max(body):.2f} |')
     open(out, 'w').write('\n'.join(lines) + '\n')
     print('\n'.join(lines))
 
@@ -139,5 +170,7 @@ if __name__ == '__main__':
         pmc_phases(sys.argv[2], sys.argv[3], *sys.argv[4:])
     elif sys.argv[1] == 'stats':
         stats(sys.argv[2], sys.argv[3])
+    elif sys.argv[1] == 'timed':
+        timed(sys.argv[2], sys.argv[3], sys.argv[4], *(sys.argv[5:6]))
     else:
         pmc(sys.argv[2], sys.argv[3], sys.argv[4], *sys.argv[5:])

@@ -5,15 +5,18 @@ One step = one ElasticBuffer.combine over one synthetic batch already resident i
 8192 tokens/rank x hidden 7168 x top-8 over 256 experts (BASELINE configs 2 and 3),
 expanded layout, gating-weighted (apply_topk_weights=True), weights passed through.
 At N = 1 the combine is one fused HIP launch; at N > 1 it is phase A -> exchange over xGMI ->
-phase B, with two transports timed on the same batch (RCCL all-to-all, pipelined; direct stores
-into the peers' symmetric windows): `value` is the faster one whose output matched the other bit
-for bit, named in config.transport, with both numbers in the line.
+phase B: `value` is the default RCCL all-to-all transport (pipelined), and the other legs timed on
+the same batch (phase A on a CU budget; direct stores into the peers' symmetric windows; the single
+reduction) stay beside it in the line, checked bit for bit.
 
 Algorithmic bytes per token: K*H*2 (rows read) + H*2 (row written)
 + K*4 (slot index) + K*4 (fp32 weight), with K = the token's valid top-k slots.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-(N > 1 is launched by torch.distributed.run, one process per GPU.)
+N > 1: `python bench.py --gpus N` starts its own N rank processes (one per GPU, as the reference's
+harness spawns its ranks, tests/elastic/test_ep.py:568,609) and relays rank 0's line; under
+torch.distributed.run (RANK set) it runs as one of the launched ranks.  Either way every rank checks
+that the world it joined has N ranks (and, over RCCL, that N GPUs are visible) and fails otherwise.
 """
 import argparse
 import json
@@ -30,23 +33,142 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBPS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 
 
-def _init_dist(n_gpus: int):
+def _fail(msg: str, code: int = 3):
+    print(f'[bench] {msg}', file=sys.stderr, flush=True)
+    sys.exit(code)
+
+
+def _free_port_pair() -> int:
+    """A port P with P and P + 1 free on 127.0.0.1 (P: the ranks' rendezvous, P + 1: the xGMI preflight
+    children's own gloo world)."""
+    import socket
+    for _ in range(64):
+        with socket.socket() as a:
+            a.bind(('127.0.0.1', 0))
+            port = a.getsockname()[1]
+            if port >= 65535:
+                continue
+            try:
+                with socket.socket() as b:
+                    b.bind(('127.0.0.1', port + 1))
+            except OSError:
+                continue
+            return port
+    raise RuntimeError('no free port pair on 127.0.0.1')
+
+
+def _launch_ranks(n: int) -> int:
+    """`python bench.py --gpus N` without a launcher: start N rank processes of this script (RANK,
+    LOCAL_RANK, WORLD_SIZE, MASTER_ADDR/PORT set, rendezvous on 127.0.0.1), relay rank 0's JSON line to
+    stdout (everything else to stderr), and return non-zero when any rank fails.  This process never
+    touches the GPU and never execs: the ranks are ordinary children.  When one rank fails the others
+    get 30 s to finish before they are killed (a peer stuck in a collective would otherwise hang)."""
+    import signal
+    import subprocess
+    import threading
+    port = _free_port_pair()
+    base = {k: v for k, v in os.environ.items() if not k.startswith('TORCHELASTIC_')}
+    base.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                DEEPEP_BENCH_LAUNCHER='bench.py')
+    cmd = [sys.executable, '-u', os.path.abspath(__file__), *sys.argv[1:]]
+    procs, lines = [], []
+    print(f'[bench] launching {n} ranks (rendezvous 127.0.0.1:{port})', file=sys.stderr, flush=True)
+    for r in range(n):
+        env = dict(base, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen(cmd, env=env, cwd=ROOT, text=True,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr))
+
+    def relay():                       # rank 0's stdout: JSON lines kept, the rest to stderr
+        for ln in procs[0].stdout:
+            if ln.startswith('{'):
+                lines.append(ln.rstrip('\n'))
+            else:
+                sys.stderr.write(ln)
+                sys.stderr.flush()
+    reader = threading.Thread(target=relay, daemon=True)
+    reader.start()
+
+    def kill_all(*_):
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    old_term = signal.signal(signal.SIGTERM, lambda *a: (kill_all(), sys.exit(143)))
+    failed_at = None
+    try:
+        while any(p.poll() is None for p in procs):
+            time.sleep(0.5)
+            bad = [p for p in procs if p.poll() not in (None, 0)]
+            if bad and failed_at is None:
+                failed_at = time.perf_counter()
+                print(f'[bench] rank {procs.index(bad[0])} exited with {bad[0].returncode}; waiting 30 s for the '
+                      f'others', file=sys.stderr, flush=True)
+            if failed_at is not None and time.perf_counter() - failed_at > 30:
+                kill_all()
+    finally:
+        kill_all()
+        signal.signal(signal.SIGTERM, old_term)
+    reader.join(timeout=10)
+    rcs = [p.wait() for p in procs]
+    for ln in lines:
+        print(ln, flush=True)
+    if any(rcs):
+        print(f'[bench] rank exit codes {rcs}', file=sys.stderr, flush=True)
+        return next(rc for rc in rcs if rc) if all(rc >= 0 for rc in rcs if rc) else 1
+    if not lines:
+        print('[bench] rank 0 printed no result line', file=sys.stderr, flush=True)
+        return 1
+    return 0
+
+
+def _init_dist(n_gpus: int, use_gpu: bool = True):
+    """Join the ranks' process group and check it: the world must have exactly --gpus ranks, and over
+    RCCL every rank needs its own GPU.  A mismatch exits non-zero (never a silent one-rank line)."""
+    backend = os.environ.get('DEEPEP_BENCH_BACKEND', 'nccl')
     if 'RANK' in os.environ and int(os.environ.get('WORLD_SIZE', '1')) > 1:
         local_rank = int(os.environ.get('LOCAL_RANK', 0))
+        world_env = int(os.environ['WORLD_SIZE'])
+        if world_env != n_gpus:
+            _fail(f'--gpus {n_gpus} but the launcher started {world_env} ranks')
         # DEEPEP_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share devices)
-        backend = os.environ.get('DEEPEP_BENCH_BACKEND', 'nccl')
-        dev = local_rank % torch.cuda.device_count()
-        torch.cuda.set_device(dev)
-        if backend == 'nccl':
+        if use_gpu:
+            n_dev = torch.cuda.device_count()
+            if backend == 'nccl' and n_dev < n_gpus:
+                _fail(f'--gpus {n_gpus} over RCCL needs {n_gpus} visible GPUs, this node shows {n_dev}')
+            dev = local_rank % n_dev
+            torch.cuda.set_device(dev)
+        if backend == 'nccl' and use_gpu:
             dist.init_process_group('nccl', device_id=torch.device('cuda', dev))
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group('gloo')
     else:
-        torch.cuda.set_device(0)
+        if n_gpus != 1:
+            _fail(f'--gpus {n_gpus} needs {n_gpus} rank processes (run `python bench.py --gpus {n_gpus}` or '
+                  f'torch.distributed.run --nproc-per-node {n_gpus}); this process is a world of one')
+        if use_gpu:
+            torch.cuda.set_device(0)
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
         os.environ.setdefault('MASTER_PORT', str(29500 + os.getpid() % 1000))
         dist.init_process_group('gloo', rank=0, world_size=1)
-    return dist.get_rank(), dist.get_world_size()
+    rank, world = dist.get_rank(), dist.get_world_size()
+    if world != n_gpus:
+        _fail(f'rank {rank}: the process group has {world} ranks, --gpus says {n_gpus}')
+    return rank, world
+
+
+def _launch_check(args) -> None:
+    """--launch-check: form the world exactly as the bench does (without touching a GPU when the
+    backend is gloo), verify it, and print the line's launch fields -- what the CPU tests run."""
+    rank, world = _init_dist(args.gpus, use_gpu=os.environ.get('DEEPEP_BENCH_BACKEND', 'nccl') == 'nccl')
+    seen = torch.zeros((world,), dtype=torch.int64)
+    seen[rank] = os.getpid()
+    dist.all_reduce(seen)
+    if rank == 0:
+        print(json.dumps({'launch_check': True, 'n_gpus': world, 'world_size_seen': world,
+                          'launcher': os.environ.get('DEEPEP_BENCH_LAUNCHER', 'external'),
+                          'distinct_rank_processes': len(set(seen.tolist())),
+                          'backend': dist.get_backend()}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
 
 
 _XGMI = {'enabled': os.environ.get('DEEPEP_BENCH_XGMI', '1') != '0', 'preflight': None}
@@ -302,6 +424,69 @@ def _bench_xgmi_dispatch(buf, x, topk_idx, topk_w, E, disp_bytes, time_dispatch,
                      'device barriers, receive-side kernels on the local window; per-rank wall time')
 
 
+def _bench_sync_free(buf, x, topk_idx, topk_w, E, weighted, dev, n_iter: int = 8):
+    """What dispatch(do_cpu_sync=False) costs over RCCL (buffer.hpp:1065-1070's no-sync mode): a fresh
+    dispatch plus the handle's FIRST combine (plan built on the device), per iteration, against the same
+    pair with the host-synced dispatch; and the bytes each exchange moves.  Without a CPU sync the host
+    knows no split sizes, so the dispatch all-to-all moves T_max rows to every rank and the combine plan
+    is worst-case padded (R x chunk tokens per chunk) -- the padding travels too.  The combine input is
+    the dispatch's own expanded output (its shape is the handle's).  Max over ranks.  Failures are
+    reported, never raised."""
+    from deepep_amd.handle import packed_row_layout
+    from deepep_amd.kernels import RowLayout
+    R, T_max = buf.num_ranks, buf.num_max_tokens_per_rank
+    xr, sf = (x if isinstance(x, tuple) else (x, None))
+    K = topk_idx.shape[1]
+    disp_row = RowLayout.make(xr.shape[1] * xr.element_size(), sf.shape[1] * sf.element_size() if sf is not None
+                              else 0, K).row_bytes
+    comb_row = packed_row_layout(xr.shape[1], K, True)[0]
+
+    def vmax(v: float) -> float:
+        t = torch.tensor([v], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def run(do_cpu_sync: bool):
+        h = None
+        for i in range(n_iter + 1):
+            if i == 1:
+                torch.cuda.synchronize()
+                dist.barrier()
+                t0 = time.perf_counter()
+            ex_x, _, ex_w, h, _ = buf.dispatch(x, topk_idx=topk_idx, topk_weights=topk_w, num_experts=E,
+                                               do_expand=True, do_cpu_sync=do_cpu_sync)
+            if not isinstance(ex_x, tuple):                  # FP8 rows are not a combine input
+                buf.combine(ex_x, h, topk_weights=ex_w, apply_topk_weights=weighted)
+            del ex_x, ex_w
+        torch.cuda.synchronize()
+        el = (time.perf_counter() - t0) / n_iter
+        plan = next((p for k, p in h._combine_plans.items() if k[0] == 'multi'), None)
+        comb_rows = sum(sum(ch.send_counts) for ch in plan.chunks) if plan is not None else None
+        return vmax(el * 1e3), comb_rows
+
+    try:
+        ms_sync, rows_sync = run(True)
+        ms_free, rows_free = run(False)
+        n_sent = int(sum(c for c in buf.dispatch(x, topk_idx=topk_idx, topk_weights=topk_w, num_experts=E,
+                                                 do_expand=True)[3]._send_counts))
+        moved = torch.tensor([n_sent * disp_row, R * T_max * disp_row, (rows_sync or 0) * comb_row,
+                              (rows_free or 0) * comb_row], dtype=torch.float64, device=dev)
+        dist.all_reduce(moved)
+        moved = [float(v) for v in moved.tolist()]
+        return dict(ms=round(ms_free, 3), synced_ms=round(ms_sync, 3),
+                    dispatch_exchange_bytes=moved[1], synced_dispatch_exchange_bytes=moved[0],
+                    combine_exchange_bytes=moved[3], synced_combine_exchange_bytes=moved[2],
+                    padding_factor_dispatch=round(moved[1] / max(moved[0], 1), 3),
+                    padding_factor_combine=round(moved[3] / max(moved[2], 1), 3),
+                    fp8_input=sf is not None,
+                    note='fresh dispatch(do_expand=True, do_cpu_sync=False) + the handle\'s first combine (plan '
+                         'built on the device), per iteration, RCCL transport, max over ranks; synced_* = the same '
+                         'pair with the host-synced dispatch; *_exchange_bytes = all ranks\' all-to-all bytes '
+                         '(sync-free: worst-case padded, incl. rows a rank keeps); fp8 input: dispatch only')
+    except Exception as e:          # noqa: BLE001 -- reported in the JSON line
+        return dict(error=f'{type(e).__name__}: {e}'[:300])
+
+
 def _hidden_of(x) -> int:
     return (x[0] if isinstance(x, tuple) else x).shape[1]
 
@@ -380,8 +565,10 @@ def _bench_single(y, handle, ex_w, weighted, total_bytes, steps, warmup, dev, re
             t_a = vmax(sum(ev[4 * i].elapsed_time(ev[4 * i + 1]) for i in range(n_ph)) / n_ph)
             t_x = vmax(sum(ev[4 * i + 1].elapsed_time(ev[4 * i + 2]) for i in range(n_ph)) / n_ph)
             t_b = vmax(sum(ev[4 * i + 2].elapsed_time(ev[4 * i + 3]) for i in range(n_ph)) / n_ph)
+            # the device-resident work of this recipe is the send-side pass (every valid expanded row copied
+            # unreduced into the send buffer) AND the one reduce: both count
             entry.update(phase_a_ms=round(t_a, 4), exchange_ms=round(t_x, 4), phase_b_ms=round(t_b, 4),
-                         reduce_only_gbps=round(total_bytes / (t_b * 1e-3) / 1e9, 1))
+                         reduce_only_gbps=round(total_bytes / ((t_a + t_b) * 1e-3) / 1e9, 1))
         else:
             entry['barrier_timeout'] = not agree(int(sb._sym.error_flag.item()) == 0)
         res[transport] = entry
@@ -393,7 +580,8 @@ def _bench_single(y, handle, ex_w, weighted, total_bytes, steps, warmup, dev, re
         res['calc_diff_vs_multi_reduction'] = d
     res['note'] = ('allow_multiple_reduction=False, same batch and bytes: rows unreduced to the source rank '
                    '(weighted: legacy low-latency fma chain), one reduce there; reduce_only = algorithmic bytes '
-                   'of all ranks / phase B (max over ranks)')
+                   'of all ranks / (phase A: the send-side pass over every expanded row + phase B: the reduce), '
+                   'unpipelined, max over ranks')
     return res
 
 
@@ -444,7 +632,16 @@ def main():
                     help='skip the per-launch flushed timing (keeps a rocprof kernel average to back-to-back launches)')
     ap.add_argument('--no-layout-ref', action='store_true',
                     help='skip the token-major layout reference (keeps a rocprof kernel average to the product input)')
+    ap.add_argument('--launch-check', action='store_true',
+                    help='form and verify the N-rank world, print its launch fields, measure nothing')
     args = ap.parse_args()
+    if args.gpus < 1:
+        _fail('--gpus must be >= 1')
+    if args.gpus > 1 and 'RANK' not in os.environ:
+        sys.exit(_launch_ranks(args.gpus))
+    if args.launch_check:
+        _launch_check(args)
+        return
 
     multi = 'RANK' in os.environ and int(os.environ.get('WORLD_SIZE', '1')) > 1
     if multi and _XGMI['enabled']:
@@ -802,6 +999,8 @@ def main():
                          'dispatch(handle=...) (no sync); bytes = x read once + expanded rows written')
     if world > 1 and _xgmi_enabled():
         dispatch['xgmi'] = _bench_xgmi_dispatch(buf, x_disp, topk_idx, topk_w, E, disp_bytes, time_dispatch, dev)
+    if world > 1:
+        dispatch['sync_free'] = _bench_sync_free(buf, x_disp, topk_idx, topk_w, E, weighted, dev)
     del x_disp
 
     loopback = None
@@ -838,23 +1037,25 @@ def main():
                              'batches back to back with the D2H overlapping the next H2D; serial = one chain')
         del host_y, host_out, dev_y
 
-    # EP > 1: both transports are complete implementations of the same combine, timed with the same
-    # protocol on the same batch; `value` is the faster one whose output matched the other bit for
-    # bit, and `config.transport` names it (both numbers stay in the line).
+    # EP > 1: `value` is the default configuration -- the RCCL all-to-all transport the north star names,
+    # phase A on the whole chip.  The other legs (phase A on a CU budget, the xGMI window transport, the
+    # single reduction) are complete implementations of the same combine timed with the same protocol on
+    # the same batch; they stay beside it in the line, and `fastest_leg` names the fastest one whose
+    # output matched the default bit for bit (information, never the headline).
     transport = buf.transport if world > 1 else None
-    rccl = None
+    rccl = fastest = None
     if world > 1:
         rccl = dict(value=round(value, 2), ms_per_step=round(ms_per_step, 4), phase_a_budget=rccl_budget)
-        if rccl_budget is not None and rccl_budget['bitwise_equal'] and rccl_budget['value'] > value:
-            value, ms_per_step = rccl_budget['value'], rccl_budget['ms_per_step']
-            transport = f'rccl, DEEPEP_PHASE_A_CUS={rccl_budget["phase_a_cus"]}'
-        if (xgmi is not None and 'value' in xgmi and xgmi['bitwise_equal_to_rccl'] and not xgmi['barrier_timeout']
-                and xgmi['value'] > value):
-            value, ms_per_step, transport = xgmi['value'], xgmi['ms_per_step'], 'xgmi'
-        xb_ = xgmi.get('phase_a_budget') if xgmi is not None else None
-        if (xb_ and xb_['bitwise_equal_to_rccl'] and not xb_['barrier_timeout'] and xb_['value'] > value):
-            value, ms_per_step = xb_['value'], xb_['ms_per_step']
-            transport = f'xgmi, DEEPEP_PHASE_A_CUS={xb_["phase_a_cus"]}'
+        legs = [('rccl', value)]
+        if rccl_budget is not None and rccl_budget['bitwise_equal']:
+            legs.append((f'rccl, DEEPEP_PHASE_A_CUS={rccl_budget["phase_a_cus"]}', rccl_budget['value']))
+        if xgmi is not None and 'value' in xgmi and xgmi['bitwise_equal_to_rccl'] and not xgmi['barrier_timeout']:
+            legs.append(('xgmi', xgmi['value']))
+            xb_ = xgmi.get('phase_a_budget')
+            if xb_ and xb_['bitwise_equal_to_rccl'] and not xb_['barrier_timeout']:
+                legs.append((f'xgmi, DEEPEP_PHASE_A_CUS={xb_["phase_a_cus"]}', xb_['value']))
+        best = max(legs, key=lambda kv: kv[1])
+        fastest = dict(leg=best[0], value=round(best[1], 2), vs_value=round(best[1] / value, 3))
 
     cpu_baseline = cpu_torch = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -876,7 +1077,11 @@ def main():
                        'parallelism': f'ep{world}', 'transport': transport},
             'roofline': roofline, 'cpu_baseline': cpu_baseline, 'cpu_torch': cpu_torch, 'loopback': loopback,
             'phases': phases, 'su_bandwidth': su_line, 'rccl': rccl, 'xgmi': xgmi, 'single_reduction': single,
+            'fastest_leg': fastest,
             'dispatch': dispatch, 'xgmi_preflight': _XGMI['preflight'],
+            'launch': {'world_size_seen': world, 'launcher': os.environ.get('DEEPEP_BENCH_LAUNCHER', 'external')
+                       if world > 1 else 'single process', 'backend': dist.get_backend(),
+                       'devices_visible': torch.cuda.device_count()},
         }
         print(json.dumps(line), flush=True)
     dist.barrier()

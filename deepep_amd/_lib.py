@@ -38,7 +38,7 @@ def binary_build_id(path: str) -> Optional[str]:
         data = f.read()
     i = data.find(b'DEEPEP_BUILD_ID=')
     return data[i + 16:i + 32].decode(errors='replace') if i >= 0 else None
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 MODE_LOCAL, MODE_EPILOGUE, MODE_FUSED = 0, 1, 2
 
@@ -118,7 +118,7 @@ SIGNATURES = {
     'deepep_sym_import': (_I, [_P, ctypes.POINTER(ctypes.c_void_p)]),
     'deepep_sym_close': (_I, [_P]),
     'deepep_sym_barrier': (_I, [_P, _I, _I, _I64, _I64, _P, _P]),
-    'deepep_sym_put': (_I, [_P, _I64, _P, _I, _I64, _P, _P]),
+    'deepep_sym_put': (_I, [_P, _I64, _P, _I, _I64, _I64, _P, _P]),
     'deepep_sym_signal': (_I, [_P, _I, _I, _I, _I64, _P]),
     'deepep_sym_wait': (_I, [_P, _I, _I, _I, _I64, _I64, _P, _P]),
     'deepep_stream_create_cu_budget': (_I, [_I, ctypes.POINTER(ctypes.c_void_p)]),

@@ -491,7 +491,13 @@ class ElasticBuffer(ExchangeMixin):
             # dispatch is then pack -> exchange -> copy, with no host sync (graph-capturable at EP = 1
             # and, over xGMI, at EP > 1),
             # as the reference's cached mode skips its notify phase (elastic.py:855-1033).
-            cached = handle if handle is not None and handle._send_counts is not None else None
+            # A handle from a dispatch without a CPU sync knows no counts on the host: its cached
+            # dispatches reuse its worst-case-sized tables (and, over RCCL, the padded exchange).
+            cached = handle if handle is not None and (handle._send_counts is not None or
+                                                       getattr(handle, '_sync_free', False)) else None
+            if handle is not None:
+                _assert(do_expand == handle.do_expand, 'do_expand must match the cached handle')
+            worst_handle = cached is not None and getattr(cached, '_sync_free', False)
             # dispatch(do_cpu_sync=False) issues kernels only, at every EP size (the reference's no-sync
             # mode, buffer.hpp:1065-1070): every receive-side launch is sized for the worst case
             # (R * T_max rows) and bounded on the device by the received count; over RCCL the rows travel in
@@ -501,7 +507,6 @@ class ElasticBuffer(ExchangeMixin):
             # EP > 1 over xGMI: the pack kernel stores every row straight into its destination's
             # symmetric window (dispatch.cuh:373-392's push), no RCCL exchange for the rows
             use_xgmi = R > 1 and self.transport == 'xgmi' and self.use_cuda
-            padded = sync_free and R > 1 and not use_xgmi        # worst-case-padded RCCL exchange
             peer_offsets = None
             host_notify = None                # one rank, host-synced: the counts' D2H, read after the copy launch
             counts = cached._counts if cached is not None else None
@@ -514,7 +519,6 @@ class ElasticBuffer(ExchangeMixin):
                       RowLayout.make(x_bytes.shape[1], sf_bytes.shape[1] if sf is not None else 0, K))
             sym = self._window(layout.row_bytes, slots=R, rows_per_slot=num_max_tokens_per_rank) if use_xgmi else None
             if cached is not None:
-                _assert(do_expand == handle.do_expand, 'do_expand must match the cached handle')
                 dst_slot = cached.dst_buffer_slot_idx
                 send_counts_l, recv_counts_l = cached._send_counts, cached._recv_counts
                 send_offsets = cached._send_offsets
@@ -522,6 +526,11 @@ class ElasticBuffer(ExchangeMixin):
                 if use_xgmi and peer_offsets is not None:
                     sym.barrier(stream)                           # peers finished reading their windows
                 use_xgmi = use_xgmi and peer_offsets is not None      # a handle made by the RCCL path
+                # a sync-free handle's receive rows are laid out by its transport (padded per source over
+                # RCCL, packed by the window notify over xGMI): it is reused on that transport only
+                _assert(not (worst_handle and R > 1) or use_xgmi == (peer_offsets is not None) and
+                        (use_xgmi or cached._row_map is not None),
+                        'a handle from dispatch(do_cpu_sync=False) is cached only on the transport that made it')
             else:
                 # --- send side: destination slots (deterministic ranks), one packed row per (token, dest),
                 # and the notify (dispatch.cuh:79-258): every destination d gets [tokens | tokens per local
@@ -559,8 +568,9 @@ class ElasticBuffer(ExchangeMixin):
                     self._a2a(recv_notify, notify)
                 if sync_free:
                     # no CPU sync: the sizes stay on the device; launches are sized for the worst case (one
-                    # rank: T rows both ways, which a cached dispatch over this handle reuses)
-                    send_counts_l = recv_counts_l = [T] if R == 1 else None
+                    # rank: T rows sent, T_max received -- the worst-case rows every launch and table of
+                    # this call is sized for, which a cached dispatch over this handle reuses)
+                    send_counts_l, recv_counts_l = ([T], [num_max_tokens_per_rank]) if R == 1 else (None, None)
                     expert_counts_l = own_tok = own_pairs = recv_blk = None
                 elif R == 1 and self.use_cuda:
                     # one rank: the counts only size the outputs, so they travel to pinned host memory
@@ -590,7 +600,9 @@ class ElasticBuffer(ExchangeMixin):
                 recv_counts_t = recv_notify[:, 0]                 # rows per source (a strided view)
             # received rows: known on the host, or the worst case (R * T_max) without a CPU sync (one
             # rank, counts still on their way to the host: all T tokens)
-            N = num_max_tokens_per_rank * R if sync_free else sum(recv_counts_l)
+            N = num_max_tokens_per_rank * R if sync_free or worst_handle else sum(recv_counts_l)
+            # worst-case-padded RCCL exchange (a sync-free call, or a cached call over its handle)
+            padded = (sync_free or worst_handle) and R > 1 and not use_xgmi
             pad_rows = num_max_tokens_per_rank if padded else 0
             row_map = None
             if use_xgmi:
@@ -630,7 +642,7 @@ class ElasticBuffer(ExchangeMixin):
                 inv, block_offsets = getattr(cached, '_copy_tables', (None, None))
                 copy_meta, copy_rows = getattr(cached, '_copy_meta', None) or (meta, N)
                 row_map = getattr(cached, '_row_map', None)
-                out_idx = None if do_expand else cached._recv_topk_idx.clone()
+                out_idx = None if do_expand else cached._recv_topk_idx[:N].clone()
                 aligned_l = cached.num_recv_tokens_per_expert_list
                 expert_counts = cached.num_unaligned_recv_tokens_per_expert
                 if cumulative_local_expert_recv_stats is not None:
@@ -682,7 +694,7 @@ class ElasticBuffer(ExchangeMixin):
             else:
                 num_expanded = N
                 # without a CPU sync the rows past the received ones are zeros (never written by the copy)
-                alloc = torch.zeros if sync_free else torch.empty
+                alloc = torch.zeros if sync_free or worst_handle else torch.empty
                 n_rows = N
             out_x = alloc((n_rows, H), dtype=x.dtype, device=dev)
             out_sf = alloc((n_rows, sf.shape[1]), dtype=sf.dtype, device=dev) if sf is not None else None
@@ -741,6 +753,7 @@ class ElasticBuffer(ExchangeMixin):
             handle._copy_tables = (inv, block_offsets)      # reused by cached dispatches
             handle._copy_meta = (copy_meta, copy_rows) if copy_rows != N else None
             handle._row_map = row_map
+            handle._sync_free = sync_free
         out_x = (out_x, out_sf) if out_sf is not None else out_x
         return out_x, out_idx, out_w, handle, EventOverlap(event)
 

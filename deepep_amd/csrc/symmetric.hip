@@ -312,11 +312,16 @@ int deepep_stream_destroy(deepep_stream_t stream) {
 }
 
 int deepep_sym_put(const void* src, int64_t bytes, const uint64_t* dest_bases, int num_ranks, int64_t dest_offset,
-                   const int32_t* error_flag, deepep_stream_t stream) {
+                   int64_t dest_extent, const int32_t* error_flag, deepep_stream_t stream) {
     if (num_ranks < 1 || num_ranks > 64 || bytes < 0 || bytes % 16 || bytes > (int64_t(1) << 30) || dest_offset < 0 ||
         dest_offset % 16 || (bytes > 0 && (src == nullptr || dest_bases == nullptr)) ||
         (reinterpret_cast<uintptr_t>(src) & 15))
         return deepep_amd_set_error(DEEPEP_ERR_INVALID_ARG, "sym_put: bad arguments");
+    // every store lands in [dest_bases[d] + dest_offset, + bytes): it must lie inside the destination's
+    // window (dest_extent bytes from its base), whatever the caller computed
+    if (dest_extent < 0 || dest_offset > dest_extent || bytes > dest_extent - dest_offset)
+        return deepep_amd_set_error(DEEPEP_ERR_INVALID_ARG, "sym_put: [dest_offset, dest_offset + bytes) lies outside "
+                                                            "the destination window (dest_extent)");
     if (bytes == 0) return DEEPEP_OK;
     hipLaunchKernelGGL(sym_put_kernel, dim3(num_ranks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
                        static_cast<const uint32_t*>(src), bytes, dest_bases, dest_offset, error_flag);

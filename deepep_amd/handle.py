@@ -122,11 +122,14 @@ def build_ep_plan(kern, handle: 'EPHandle', *, num_ranks: int, rank: int, single
     dev = handle.recv_src_metadata.device
     # A handle from a dispatch without a CPU sync: the counts live on the device only, so every chunk
     # is laid out for the worst case -- `padded` unit positions per source rank (a chunk's tokens, times
-    # K for the single reduction), the unused ones skipped by phase A (zero partials over RCCL, padding
-    # rows the scatter ignores over xGMI) -- and the RCCL exchange moves R x padded rows per chunk.
+    # min(K, experts per rank) for the single reduction: a token's lanes on one rank are distinct experts
+    # there, buffer.hpp:1067-1069's bound; a unit past it is rejected by the plan kernel, flagged, never
+    # stored), the unused ones skipped by phase A (zero partials over RCCL, padding rows the scatter
+    # ignores over xGMI) -- and the RCCL exchange moves R x padded rows per chunk.  Memory and traffic
+    # of that padding: DESIGN.md section 1.
     padded = 0
     if cnt.recv_tok is None:
-        padded = bpc * PLAN_BLOCK_TOKENS * (K if single else 1)
+        padded = bpc * PLAN_BLOCK_TOKENS * (min(K, handle.num_experts // R) if single else 1)
     # ---- expert side: phase-A units of every chunk, concatenated
     if padded:
         units = [[padded] * R for _ in range(C)]

@@ -143,7 +143,8 @@ class SymmetricBuffer:
                                f'{HEADER_BYTES - NOTIFY_OFFSET}-byte notify area in 16-byte units')
         handle = stream.cuda_stream if stream is not None else torch.cuda.current_stream().cuda_stream
         _lib.check(self.lib.deepep_sym_put(records.data_ptr(), n * 4, self.bases_dev.data_ptr(), self.num_ranks,
-                                           NOTIFY_OFFSET + self.rank * n * 4, self.error_flag.data_ptr(), handle),
+                                           NOTIFY_OFFSET + self.rank * n * 4, HEADER_BYTES + self.data_bytes,
+                                           self.error_flag.data_ptr(), handle),
                    'sym_put')
 
     def notify_area(self, n: int) -> torch.Tensor:

@@ -48,7 +48,7 @@ extern "C" {
 
 typedef struct ihipStream_t* deepep_stream_t;   /* == hipStream_t */
 
-#define DEEPEP_AMD_ABI_VERSION 12
+#define DEEPEP_AMD_ABI_VERSION 13
 
 #define DEEPEP_OK               0
 #define DEEPEP_ERR_INVALID_ARG  (-1)
@@ -379,12 +379,14 @@ int deepep_sym_close(void* ptr);
 
 /* Store src + d * bytes (bytes % 16 == 0) at dest_bases[d] + dest_offset for every d < num_ranks:
  * system-scope write-through stores into the peers' windows (dest_bases: device uint64 [num_ranks],
- * e.g. the window bases, so dest_offset addresses the header's notify area).  The dispatch notify's
- * transport: rank r puts its count record for every destination into slot r of that destination's
- * area, then a barrier makes them visible (dispatch.cuh:79-258's notify over NVLink).  Nothing is
- * stored once bit 2 of error_flag (device int or NULL) is set. */
+ * e.g. the window bases, so dest_offset addresses the header's notify area).  dest_extent: the bytes
+ * every destination window spans from its base (header + data); a put whose [dest_offset, dest_offset
+ * + bytes) does not lie inside it is rejected (DEEPEP_ERR_INVALID_ARG) before anything is launched.
+ * The dispatch notify's transport: rank r puts its count record for every destination into slot r of
+ * that destination's area, then a barrier makes them visible (dispatch.cuh:79-258's notify over
+ * NVLink).  Nothing is stored once bit 2 of error_flag (device int or NULL) is set. */
 int deepep_sym_put(const void* src, int64_t bytes, const uint64_t* dest_bases, int num_ranks, int64_t dest_offset,
-                   const int32_t* error_flag, deepep_stream_t stream);
+                   int64_t dest_extent, const int32_t* error_flag, deepep_stream_t stream);
 
 /* Group barrier on the stream: peer_flags (device, uint64 [num_ranks]) holds the address of every
  * rank's window header (above).  Every XCD's L2 is first written back (the stores into peer windows before

@@ -28,12 +28,20 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, '_build', 'liboracle.so')
+# DEEPEP_ORACLE_LIB=asan: the AddressSanitizer + UBSan build of the same source (`make asan`; the
+# process must have the ASan runtime preloaded -- tests/test_oracle_asan.py does that)
+_SANITIZED = os.environ.get('DEEPEP_ORACLE_LIB', '') == 'asan'
+_LIB_PATH = os.path.join(_HERE, '_build', 'liboracle_asan.so' if _SANITIZED else 'liboracle.so')
 _lib = None
 
 
 def build() -> str:
-    subprocess.run(['make', '-s', '-C', _HERE], check=True)
+    subprocess.run(['make', '-s', '-C', _HERE] + (['asan'] if _SANITIZED else []), check=True)
+    return _LIB_PATH
+
+
+def loaded_library() -> str:
+    """Path of the checker library this process uses."""
     return _LIB_PATH
 
 

@@ -116,6 +116,13 @@ def dispatch_mode_checks(buf, x, topk_idx, topk_weights, num_experts: int, num_m
         if rows(recv_x).shape[0] != worst or handle.recv_src_metadata.shape[0] != worst:
             fails.append('do_cpu_sync=False shapes are not worst-case')
     recv_w_full = recv_w
+    if not do_cpu_sync:
+        # cached calls over a no-CPU-sync handle return the handle's worst-case shapes, and the same bits
+        # as its first call (rows past the received ones: zeros / -1, as the first call's)
+        if not (same(c_x, recv_x) and torch.equal(c_idx, recv_idx)):
+            fails.append('cached dispatch over a no-CPU-sync handle differs from its first call')
+        if rows(ce_x).shape[0] != rows(ex_x).shape[0] or ce_w.shape != ex_w.shape:
+            fails.append('cached expanded dispatch over a no-CPU-sync handle changed shape')
     recv_x, recv_idx, recv_w = head(recv_x, n), recv_idx[:n], recv_w[:n]
     meta, ex_meta = handle.recv_src_metadata[:n], ex_handle.recv_src_metadata[:n]
     if not (same(head(c_x, n), recv_x) and torch.equal(c_idx[:n], recv_idx) and c_w is None):

@@ -33,7 +33,7 @@ def test_exports_every_declared_symbol(lib):
 
 
 def test_abi_version(lib):
-    assert lib.deepep_amd_abi_version() == 12
+    assert lib.deepep_amd_abi_version() == 13
 
 
 def test_build_id_matches_sources(lib):
@@ -105,6 +105,13 @@ def test_invalid_arguments_are_rejected_without_a_gpu(lib):
                                     64, 64, 96, 112, None, None) == -1
     assert lib.deepep_route_block_counts(16, 200, 8, 64, 8, 1, 16, 16, None) == -1
     assert lib.deepep_route_block_counts(None, 0, 8, 64, 8, 0, None, None, None) == 0     # nothing to count
+    # a window put must stay inside the destination window: offset + bytes past the extent, or an offset
+    # beyond it, is rejected before any launch (16-byte aligned fake pointers: nothing is dereferenced)
+    assert lib.deepep_sym_put(16, 64, 32, 2, 65536, 65536 + 48, None, None) == -1
+    assert b'outside' in lib.deepep_amd_last_error()
+    assert lib.deepep_sym_put(16, 16, 32, 2, 1 << 20, 1 << 19, None, None) == -1
+    assert lib.deepep_sym_put(16, 16, 32, 2, 0, -1, None, None) == -1
+    assert lib.deepep_sym_put(16, 0, 32, 2, 0, 0, None, None) == 0            # nothing to store
     # a CU budget is whole CUs per XCD; nonsense is rejected
     assert lib.deepep_stream_create_cu_budget(0, None) == -1
 

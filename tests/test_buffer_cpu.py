@@ -279,7 +279,7 @@ def test_random_routing_world(world, chunks):
     assert len(results) == world and not any(results.values()), results
 
 
-def _modes_worker(rank, world, port, alignment, do_cpu_sync, do_handle_copy, queue):
+def _modes_worker(rank, world, port, alignment, do_cpu_sync, do_handle_copy, queue, t_max_extra=0):
     import sys
     sys.path.insert(0, ROOT)
     try:
@@ -299,25 +299,30 @@ def _modes_worker(rank, world, port, alignment, do_cpu_sync, do_handle_copy, que
         idx[T // 2] = -1
         w = w.masked_fill(idx < 0, 0)
         x = torch.randn((T, H), generator=g).to(torch.bfloat16)
-        buf = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=T, hidden=H, num_topk=K)
+        T_max = T + t_max_extra
+        buf = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=T_max, hidden=H, num_topk=K)
         buf._kernels = OracleKernels()
-        queue.put((rank, dispatch_mode_checks(buf, x, idx, w, E, T, alignment, do_cpu_sync, do_handle_copy)))
+        queue.put((rank, dispatch_mode_checks(buf, x, idx, w, E, T_max, alignment, do_cpu_sync, do_handle_copy)))
         dist.barrier()
         dist.destroy_process_group()
     except Exception:
         queue.put((rank, [traceback.format_exc()]))
 
 
-@pytest.mark.parametrize('world,alignment,do_cpu_sync,do_handle_copy', [
-    (2, 1, True, True), (2, 4, True, False), (2, 8, False, True), (1, 8, False, True), (1, 1, False, False)])
-def test_dispatch_modes(world, alignment, do_cpu_sync, do_handle_copy):
+@pytest.mark.parametrize('world,alignment,do_cpu_sync,do_handle_copy,t_max_extra', [
+    (2, 1, True, True, 0), (2, 4, True, False, 0), (2, 8, False, True, 0), (1, 8, False, True, 0),
+    (1, 1, False, False, 0), (1, 1, False, True, 200), (2, 4, False, True, 200), (2, 1, True, True, 200)])
+def test_dispatch_modes(world, alignment, do_cpu_sync, do_handle_copy, t_max_extra):
     """Cached / cached-expanded-zero-padded / deterministic / counter / no-CPU-sync dispatch
     (tests/elastic/test_ep.py:143-177, 355-466) over 1 and 2 gloo ranks (one rank without a CPU sync
-    sizes its launches for all tokens and bounds them by the device count)."""
+    sizes its launches for the worst case and bounds them by the device count).  t_max_extra: a
+    num_max_tokens_per_rank well above the batch (ceil(T / 128) != ceil(T_max / 128)), so a cached
+    dispatch over a no-CPU-sync handle must reuse the handle's worst-case tables."""
     ctx = mp.get_context('spawn')
     queue = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_modes_worker, args=(r, world, port, alignment, do_cpu_sync, do_handle_copy, queue))
+    procs = [ctx.Process(target=_modes_worker, args=(r, world, port, alignment, do_cpu_sync, do_handle_copy, queue,
+                                                     t_max_extra))
              for r in range(world)]
     for p in procs:
         p.start()

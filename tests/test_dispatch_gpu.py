@@ -170,13 +170,16 @@ def test_dispatch_direct_copy_one_rank(hip, K, E, T, H, expanded, fp8):
         assert torch.equal(got['rsf'], exp['rsf'])
 
 
-@pytest.mark.parametrize('alignment,do_cpu_sync,do_handle_copy,fp8', [
-    (1, True, True, False), (128, True, False, False), (4, False, True, False), (1, True, True, True),
-    (1, False, False, True), (128, False, True, False)])
-def test_dispatch_modes_on_gpu(alignment, do_cpu_sync, do_handle_copy, fp8):
+@pytest.mark.parametrize('alignment,do_cpu_sync,do_handle_copy,fp8,t_max_extra', [
+    (1, True, True, False, 0), (128, True, False, False, 0), (4, False, True, False, 0), (1, True, True, True, 0),
+    (1, False, False, True, 0), (128, False, True, False, 0), (1, False, True, False, 300),
+    (4, False, True, True, 300), (1, True, True, False, 300)])
+def test_dispatch_modes_on_gpu(alignment, do_cpu_sync, do_handle_copy, fp8, t_max_extra):
     """ElasticBuffer.dispatch modes with the HIP kernels (EP = 1): cached, cached expanded with zero
     padding, handle copy, deterministic repeat, the per-expert counter, no CPU sync
-    (tests/elastic/test_ep.py:143-177, 355-466)."""
+    (tests/elastic/test_ep.py:143-177, 355-466).  t_max_extra > 0: num_max_tokens_per_rank above the
+    batch, so the worst-case tables of a no-CPU-sync handle have more 128-row blocks than the batch
+    (a cached dispatch must reuse them)."""
     import os
     import torch.distributed as dist
     from deepep_amd import ElasticBuffer
@@ -198,8 +201,8 @@ def test_dispatch_modes_on_gpu(alignment, do_cpu_sync, do_handle_copy, fp8):
     x = torch.randn((T, H), device='cuda', generator=g).to(torch.bfloat16)
     if fp8:
         x = per_token_cast_to_fp8(x)
-    buf = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=T, hidden=H, num_topk=K)
-    fails = dispatch_mode_checks(buf, x, idx, w, E, T, alignment, do_cpu_sync, do_handle_copy)
+    buf = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=T + t_max_extra, hidden=H, num_topk=K)
+    fails = dispatch_mode_checks(buf, x, idx, w, E, T + t_max_extra, alignment, do_cpu_sync, do_handle_copy)
     assert not fails, fails
 
 

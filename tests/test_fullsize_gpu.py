@@ -9,12 +9,12 @@ dispatch and the pipelined (4-chunk) combine.
       expert outputs the combine reduces
   C5  8 x 16384 tokens, skewed routing (get_unbalanced_scores, rank 0's experts ~4x the tokens)
 
-The reference's own test checks bitwise at 4096 tokens x 7168 x top-6 across 8 ranks
-(tests/elastic/test_ep.py:502-511, 577-580).  Here rank 0's WHOLE combined_x (all its tokens, with
-every expert rank's rows of them) is checked bitwise against the oracle (oracle.combine_ep_one: the
-arithmetic of oracle.combine_ep, pinned to refs.combine, restricted to one source rank and run on 16
-host threads); every other rank on a fixed subsample of 512 of its tokens with ALL of their partials;
-the top-k weight pass-through for every token of every rank.
+The reference's own test checks every rank's whole output bitwise at 4096 tokens x 7168 x top-6
+across 8 ranks (tests/elastic/test_ep.py:502-511, 577-580).  Here too: EVERY rank's whole combined_x
+(all its tokens, with every expert rank's rows of them) is checked bitwise against the oracle
+(oracle.combine_ep_one: the arithmetic of oracle.combine_ep, pinned to refs.combine, restricted to one
+source rank; the 8 ranks' checks run concurrently, 2 host threads each), and the top-k weight
+pass-through for every token of every rank.
 """
 import numpy as np
 import pytest
@@ -25,8 +25,6 @@ from tests.sim import FakeGroup, ThreadComm, run_threads
 
 pytestmark = pytest.mark.gpu
 
-SAMPLE = 512
-FULL_RANK = 0          # this rank's whole output is checked
 
 
 def _u16(t: torch.Tensor) -> np.ndarray:
@@ -84,12 +82,10 @@ def _rank(rank, world, T, H, K, E, skew, fp8, weighted, comm, shared, results):
         shared[rank] = dict(meta=handle.recv_src_metadata.cpu().numpy(), y=y, ex_w=ex_w, idx=idx.cpu().numpy(),
                             out=out, bias=b)
         comm.bar.wait()
-        # ---- the oracle on this rank's tokens (all of them on rank FULL_RANK, else a sample), with every
-        #      expert rank's rows of them
-        n_s = T if rank == FULL_RANK else SAMPLE
-        S = np.arange(T) if n_s == T else np.sort(np.random.default_rng(99 + rank).choice(T, n_s, replace=False))
-        pos = np.full(T, -1, np.int64)
-        pos[S] = np.arange(n_s)
+        # ---- the oracle on ALL of this rank's tokens, with every expert rank's rows of them
+        n_s = T
+        S = np.arange(T)
+        pos = np.arange(T, dtype=np.int64)
         x_sub, m_sub, w_sub = [], [], []
         for r in range(world):
             m = shared[r]['meta']
@@ -108,13 +104,12 @@ def _rank(rank, world, T, H, K, E, skew, fp8, weighted, comm, shared, results):
         bias_sub = (_u16(b[torch.from_numpy(S).cuda()]) if b is not None else None, None)
         exp, exp_w = oracle.combine_ep_one(rank, x_sub, m_sub, shared[rank]['idx'][S], E, n_s, expanded=True,
                                            topk_weights_per_rank=w_sub, bias=bias_sub, weighted=weighted,
-                                           threads=16 if n_s == T else 2)
+                                           threads=2)
         got = _u16(out[torch.from_numpy(S).cuda()])
         if not np.array_equal(got, exp):
             bad = np.argwhere(got != exp)
             failures.append(f'combined_x differs on {len(bad)} elements of {n_s} tokens, first {bad[:3].tolist()}')
-        if rank == FULL_RANK:
-            shared['full_checked'] = got.shape[0]
+        shared[('full_checked', rank)] = got.shape[0]
         if not np.array_equal(exp_w, w.cpu().numpy()[S]):
             failures.append('oracle weights of the sample')
         comm.bar.wait()
@@ -134,13 +129,13 @@ def _run(T, skew=1.0, fp8=False, weighted=False):
     comm.lock = threading.Lock()
     shared = {}
     results = run_threads(world, _rank, (world, T, H, K, E, skew, fp8, weighted, comm, shared), timeout=600)
-    full = shared.get('full_checked')
+    full = [shared.get(('full_checked', r)) for r in range(world)]
     del shared
     torch.cuda.empty_cache()
     assert len(results) == world, results
     bad = {r: f for r, f in results.items() if f}
     assert not bad, bad
-    assert full == T, f'rank {FULL_RANK} checked {full} of {T} tokens'
+    assert full == [T] * world, f'tokens checked per rank {full}, expected {T} each'
 
 
 @pytest.mark.parametrize('weighted', [False, True], ids=['plain_bias', 'gating_weighted'])

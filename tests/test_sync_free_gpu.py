@@ -262,6 +262,16 @@ def _dispatch_sync_free_rank(rank, world, T, H, K, E, comm, results):
                 failures.append(f'amr={amr}: combined_x')
             if amr and not np.array_equal(out_w.cpu().numpy(), expect[1]):
                 failures.append(f'amr={amr}: combined_topk_weights')
+            # a cached dispatch over the no-CPU-sync handle (the padded exchange again, the handle's tables):
+            # the same bits as its first call on every received row
+            comm.bar.wait()
+            c_x, _, c_w, _, _ = buf.dispatch(x, topk_weights=w, do_expand=True, handle=handle)
+            torch.cuda.synchronize()
+            valid = torch.from_numpy(meta[:n, 2:]).cuda()
+            valid = valid[valid >= 0].long()
+            if c_x.shape != ex_x.shape or not torch.equal(c_x[valid].view(torch.int16), ex_x[valid].view(torch.int16)) \
+                    or not torch.equal(c_w[valid], ex_w[valid]):
+                failures.append(f'amr={amr}: cached dispatch over the no-CPU-sync handle')
             comm.bar.wait()
         results[rank] = failures
     except Exception:
@@ -271,12 +281,14 @@ def _dispatch_sync_free_rank(rank, world, T, H, K, E, comm, results):
             comm.bar.abort()
 
 
-@pytest.mark.parametrize('world,T', [(4, 128), (8, 1088)])
-def test_dispatch_without_cpu_sync_ep_gt_1(world, T):
+@pytest.mark.parametrize('world,T,E', [(4, 128, 64), (8, 1088, 64), (8, 1088, 32)])
+def test_dispatch_without_cpu_sync_ep_gt_1(world, T, E):
     """EP > 1 dispatch(do_cpu_sync=False) + first combine over the (simulated) RCCL transport with no
     host synchronisation (csrc/elastic/buffer.hpp:1065-1070); T = 1088 gives a pipelined (multi-chunk)
-    padded combine.  Bitwise vs the oracle, plain and single reduction."""
-    H, K, E = 256, 8, 64
+    padded combine; E = 32 at EP = 8: 4 experts per rank < top-8, so the single reduction's padded
+    chunks hold min(K, experts per rank) rows per token.  Bitwise vs the oracle, plain and single
+    reduction; then a cached dispatch over the same handle."""
+    H, K = 256, 8
     comm = ThreadComm(world)
     results = run_threads(world, _dispatch_sync_free_rank, (world, T, H, K, E, comm))
     assert len(results) == world, results

@@ -184,3 +184,30 @@ def test_dispatch_pack_never_stores_past_its_destination(kern, peer):
     # a negative offset is rejected the same way: nothing lands in front of the buffer
     got, rec = pack([0, -3], n, n)
     assert rec[0] == FLAG_BAD_ADDRESS and rec[1] == FAULT_PACK_ROW and rec[3] == 1, rec
+
+
+def test_sym_put_never_stores_past_the_window(kern):
+    """deepep_sym_put (the window notify's put) checks its extent at the C-ABI: a put whose
+    [dest_offset, dest_offset + bytes) reaches past the destination window's extent is rejected before
+    any launch -- nothing is stored, the canaries after the window stay zero -- and an in-bounds put
+    lands exactly where it was asked to."""
+    R, window, tail = 2, 4096, 1024
+    big = torch.zeros((R, window + tail), dtype=torch.uint8, device='cuda')       # window + canary tail per rank
+    bases = torch.tensor([big[d].data_ptr() for d in range(R)], dtype=torch.int64, device='cuda')
+    src = torch.arange(R * 64, dtype=torch.int32, device='cuda').view(R, 64) + 1       # 256 bytes per rank
+    stream = torch.cuda.current_stream().cuda_stream
+    lib = kern.lib
+    # past the end: offset + bytes = window + 16
+    rc = lib.deepep_sym_put(src.data_ptr(), 256, bases.data_ptr(), R, window - 240, window, None, stream)
+    assert rc == -1                                   # DEEPEP_ERR_INVALID_ARG
+    assert b'outside' in lib.deepep_amd_last_error()
+    torch.cuda.synchronize()
+    assert int(big.count_nonzero()) == 0, 'a rejected put stored something'
+    # exactly at the end: accepted, stored in every destination, the tail untouched
+    rc = lib.deepep_sym_put(src.data_ptr(), 256, bases.data_ptr(), R, window - 256, window, None, stream)
+    assert rc == 0, lib.deepep_amd_last_error()
+    torch.cuda.synchronize()
+    for d in range(R):
+        assert torch.equal(big[d, window - 256:window].view(torch.int32), src[d])
+        assert int(big[d, window:].count_nonzero()) == 0
+        assert int(big[d, :window - 256].count_nonzero()) == 0

@@ -548,18 +548,46 @@ def test_lost_peer_times_out_instead_of_hanging():
         _lib.check(lib.deepep_sym_free(dead), 'sym_free')
 
 
-def _full_worker(rank, world, port, queue):
+_ROW_TABLE_ROWS = 4093        # prime: the expert-output row of (source token g, lane k) is table[hash(g, k)]
+
+
+def _row_table(H: int) -> np.ndarray:
+    """The rows every expert output is drawn from: [4093, H] random bf16 (bits), the same in every
+    process, so a rank can rebuild the expert outputs of its own tokens on every expert rank without
+    moving any rows (and check its combined output against the oracle)."""
+    rng = np.random.default_rng(20260)
+    import oracle
+    return oracle.f32_to_bf16(rng.standard_normal((_ROW_TABLE_ROWS, H)).astype(np.float32))
+
+
+def _row_of(key):
+    """Table row of key = global source token * K + lane (numpy or torch int64)."""
+    return (key * 2654435761) % _ROW_TABLE_ROWS
+
+
+def _full_worker(rank, world, port, queue, t_start):
     """BASELINE config 3 at full size over the xGMI transport: 8 processes sharing the GPU, HIP-IPC
-    windows, the pipelined combine (4 chunks) -- against the RCCL-path combine of the same handle and
-    inputs (the RCCL path is checked against the oracle at this size in tests/test_fullsize_gpu.py)."""
+    windows, the pipelined combine (4 chunks).  Each rank's WHOLE combined_x (and weight pass-through)
+    is compared bitwise with oracle.combine_ep_one (the CPU restatement pinned to refs.combine) AND with
+    the RCCL-path combine of the same handle and inputs.  The expert outputs are rows of a shared table
+    picked by (source token, lane), so every rank rebuilds the rows of its own tokens on every expert
+    rank from the gathered metadata, without moving rows between processes.  Every stage is reported
+    with its wall-clock time since the test started (a stuck child names where it stopped)."""
+    import time
+
+    def stage(what: str) -> None:
+        queue.put((rank, 'stage', f'{what} @{time.time() - t_start:.1f}s'))
+    stage('started (torch imported)')
     sys.path.insert(0, ROOT)
     try:
         os.environ['MASTER_ADDR'] = '127.0.0.1'
         os.environ['MASTER_PORT'] = str(port)
         import torch.distributed as dist
+        import oracle
         torch.cuda.set_device(0)
+        stage('device set')
         dist.init_process_group('gloo', rank=rank, world_size=world)
-        queue.put((rank, 'stage', 'gloo up'))
+        stage('gloo up')
         from deepep_amd import ElasticBuffer
         dev = torch.device('cuda', 0)
         T, H, K, E = 8192, 7168, 8, 256
@@ -568,13 +596,14 @@ def _full_worker(rank, world, port, queue):
         idx = idx.to(torch.int64)
         x = torch.randn((T, H), device=dev, generator=g).to(torch.bfloat16)
         bias = torch.randn((T, H), device=dev, generator=g).to(torch.bfloat16)
+        table = _row_table(H)
         bufs = {}
         for transport in ('xgmi', 'rccl'):
             os.environ['DEEPEP_TRANSPORT'] = transport
             bufs[transport] = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=T, hidden=H, num_topk=K,
                                             explicitly_destroy=True, num_gpu_timeout_secs=60)
         failures = []
-        queue.put((rank, 'stage', 'buffers built'))
+        stage('buffers built')
         ex_x, _, ex_w, handle, _ = bufs['xgmi'].dispatch(x, topk_idx=idx, topk_weights=w, num_experts=E,
                                                          do_expand=True)
         _, _, ex_w_r, handle_r, _ = bufs['rccl'].dispatch(x, topk_idx=idx, topk_weights=w, num_experts=E,
@@ -588,14 +617,55 @@ def _full_worker(rank, world, port, queue):
                             f'{int(bufs["xgmi"]._sym.error_flag.item())}')
             queue.put((rank, failures))               # the combine would run on that metadata: stop here
             return
-        y = torch.randn((handle.num_expanded_tokens, H), device=dev, generator=g).to(torch.bfloat16)
-        queue.put((rank, 'stage', 'dispatched'))
+        # expert outputs: expanded row meta[j, 2 + k] holds table[_row_of(meta[j, 0] * K + k)]
+        meta = handle.recv_src_metadata
+        slots = meta[:, 2:].long()
+        valid = slots >= 0
+        keys = (meta[:, :1].long() * K + torch.arange(K, device=dev).view(1, K))[valid]
+        tab = torch.from_numpy(table.view(np.int16)).to(dev).view(torch.bfloat16)
+        y = torch.zeros((handle.num_expanded_tokens, H), dtype=torch.bfloat16, device=dev)
+        y[slots[valid]] = tab[_row_of(keys)]
+        del tab, keys
+        # every expert rank's metadata rows of this rank's tokens (small: ~2 MB per rank)
+        meta_np = meta.cpu().numpy()
+        mine = {d: meta_np[meta_np[:, 1] // K == d] for d in range(world)}
+        gathered = [None] * world
+        dist.all_gather_object(gathered, mine)
+        idx_np, w_np = idx.cpu().numpy(), w.cpu().numpy()
+        x_sub, m_sub, w_sub = [], [], []
+        for e in range(world):
+            m = gathered[e][rank].copy()
+            sl = m[:, 2:]
+            ok = sl >= 0
+            tok = np.broadcast_to((m[:, :1] % T), sl.shape)[ok]
+            lane = np.broadcast_to(np.arange(K), sl.shape)[ok]
+            x_sub.append(table[_row_of((rank * T + tok).astype(np.int64) * K + lane)])
+            w_sub.append(w_np[tok, lane].astype(np.float32))
+            new = np.full(sl.shape, -1, np.int32)
+            new[ok] = np.arange(int(ok.sum()), dtype=np.int32)
+            m[:, 2:] = new
+            m_sub.append(m)
+        del gathered, mine
+        stage('dispatched, rows built')
         for weighted in (False, True):
             b = None if weighted else bias
             outs = {t: bf.combine(y, handle, topk_weights=ex_w, bias=b, apply_topk_weights=weighted)
                     for t, bf in bufs.items()}
             torch.cuda.synchronize()
-            queue.put((rank, 'stage', f'combined weighted={weighted}'))
+            stage(f'combined weighted={weighted}')
+            exp, exp_w = oracle.combine_ep_one(rank, x_sub, m_sub, idx_np, E, T, expanded=True,
+                                               topk_weights_per_rank=w_sub,
+                                               bias=(_u16(b) if b is not None else None, None),
+                                               weighted=weighted, threads=2)
+            stage(f'oracle weighted={weighted}')
+            for t in bufs:
+                got = _u16(outs[t][0])
+                if not np.array_equal(got, exp):
+                    bad_rows = np.nonzero((got != exp).any(axis=1))[0]
+                    failures.append(f'weighted={weighted}: {t} combined_x != oracle on {bad_rows.size} of {T} '
+                                    f'tokens, first {bad_rows[:4].tolist()}')
+                if not np.array_equal(outs[t][1].cpu().numpy(), exp_w):
+                    failures.append(f'weighted={weighted}: {t} weight pass-through != oracle')
             if bufs['xgmi']._num_chunks(handle) < 2:
                 failures.append('not pipelined')
             if not torch.equal(outs['xgmi'][0], outs['rccl'][0]):
@@ -631,18 +701,20 @@ def _full_worker(rank, world, port, queue):
         queue.put((rank, [traceback.format_exc()]))
 
 
+@pytest.mark.timeout(300)
 def test_xgmi_transport_full_size_config3():
     world = 8
     ctx = mp.get_context('spawn')
     queue = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_full_worker, args=(r, world, port, queue)) for r in range(world)]
-    for p in procs:
-        p.start()
     import queue as queue_mod
     import time
-    results, stages = {}, {}
-    deadline = time.time() + 150
+    t_start = time.time()
+    procs = [ctx.Process(target=_full_worker, args=(r, world, port, queue, t_start)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results, stages = {}, {r: 'not started (no marker yet)' for r in range(world)}
+    deadline = time.time() + 240
     try:
         while len(results) < world and time.time() < deadline:
             try:
@@ -669,5 +741,5 @@ def test_xgmi_transport_full_size_config3():
                 p.kill()
     if len(results) != world or any(results.values()):
         tails = {r: [f[-1500:] for f in fl] for r, fl in results.items()}
-        pytest.fail(f'{len(results)}/{world} ranks reported; last stage per rank {stages}; failures: {tails}',
-                    pytrace=False)
+        pytest.fail(f'{len(results)}/{world} ranks reported after {time.time() - t_start:.0f} s; last stage per '
+                    f'rank (wall clock since the start) {stages}; failures: {tails}', pytrace=False)

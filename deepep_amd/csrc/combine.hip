@@ -641,12 +641,7 @@ template <int kMode, bool kWeighted, int kVPT, bool kFull, int kAux>
 void launch_lds(const Params& p, bool lds, int waves, int group, hipStream_t stream) {
     const int nvec = p.hidden / 8;
     const int64_t items = static_cast<int64_t>(p.num_units) * ((nvec + 64 * kVPT - 1) / (64 * kVPT));
-    if constexpr (kAux == kAuxSC1NT) {          // the two default shapes only (fused / epilogue, phase A)
-        if (waves == 8) launch_shape<kMode, kWeighted, kVPT, kFull, kAux, true, 8, 8>(p, items, stream);
-        else launch_shape<kMode, kWeighted, kVPT, kFull, kAux, true, 4, 4>(p, items, stream);
-        return;
-    }
-    if constexpr (kAux == kAuxSC1 || kAux == kAuxSys) {
+    if constexpr (kAux == kAuxSC1 || kAux == kAuxSys || kAux == kAuxSC1NT) {
         if (lds) {
             if (waves == 8) {
                 if (group == 2) launch_shape<kMode, kWeighted, kVPT, kFull, kAux, true, 8, 2>(p, items, stream);

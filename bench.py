@@ -616,7 +616,7 @@ def _pmc_traffic(workload: str, build_id: str):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=200)
+    ap.add_argument('--steps', type=int, default=1000)
     ap.add_argument('--warmup', type=int, default=20)
     ap.add_argument('--tokens', type=int, default=8192)
     ap.add_argument('--hidden', type=int, default=7168)

@@ -30,8 +30,6 @@ for step in "$@"; do
                 run rocprofdef 900 rocprofv3 --kernel-trace --stats -d $OUT/profdef -o prof --output-format csv -- python3 bench.py
                 python tools/summarize_prof.py timed $OUT/profdef/prof_kernel_trace.csv "combine_rows_kernel<2," $OUT/profdef_timed.md "combine steps + kernel-alone loop (value; roofline.kernel_us),token-major layout reference (roofline.same_run_token_major_rows)" ;;
         kbench) run kbench 600 python tools/kbench.py ;;
-        kalign) run kalign 600 python tools/kbench_align.py ;;
-        kab)    run kab 600 python tools/kbench_ab.py ;;
         kuc)    run kuc 600 python tools/kbench_uc.py ;;
         pcopy)  [ -f tools/libprobe_copy.so ] || hipcc --offload-arch=gfx950 -O3 -fPIC -shared -o tools/libprobe_copy.so tools/probe_copy.hip
                 run pcopy 600 python tools/probe_copy.py ;;
@@ -40,10 +38,7 @@ for step in "$@"; do
         klayout) run klayout 300 python tools/klayout.py ;;
         kwin)   run kwin 300 python tools/kwin.py ;;
         klayoutruns) export KLAYOUT_RUNS=1; run klayoutruns 400 python tools/klayout.py; unset KLAYOUT_RUNS ;;
-        kwaves) run kwaves 600 python tools/kbench_waves.py ;;
-        kvar)   run kvar 300 python tools/kvar.py ;;
         kflush) run kflush 300 python tools/kflush.py ;;
-        probetok) run probetok 300 python tools/probe_tok.py ;;
         kplace) run kplace 300 python tools/kplace.py ;;
         kplacetlb) export KPLACE_ITERS=4 KPLACE_WARM=1 KPLACE_ROUNDS=1
                 run kplacetlb 300 rocprofv3 --kernel-trace --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum GRBM_UTCL2_BUSY GRBM_GUI_ACTIVE -d $OUT/kplacetlb -o pmc --output-format csv -- python3 tools/kplace.py

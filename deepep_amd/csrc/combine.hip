@@ -895,9 +895,15 @@ int launch_combine(int mode, int weighted, const Params& p_in, deepep_stream_t s
     sh.vpt = g_config.vec_per_lane > 0 ? g_config.vec_per_lane : (nvec >= 128 ? 2 : 1);
     if (sh.vpt != 1 && sh.vpt != 2) sh.vpt = 2;
     sh.lds = g_config.stage_lds >= 0 ? g_config.stage_lds != 0 : true;
-    // store policies: 0 plain, 1 nt, 2 sc1 (default), 3 system scope (peer windows), 4 sc1 nt
+    // store policies: 0 plain, 1 nt, 2 sc1 (fused / epilogue default), 3 system scope (peer windows),
+    // 4 sc1 nt (phase A default).  Phase A's packed send rows are written once and read back only by the
+    // exchange, so they stream past L2 (sc1 nt): EP = 8 rank share of config 3, tools/kphase_a.py,
+    // medians of 5 interleaved rounds, 4-wave workgroups x 4 rows in flight: 248.9 vs 251.4 us weighted,
+    // 252.1 vs 253.8 plain (profiles/r04a_kphasea.jsonl; round 3: 245.0-246.9 vs 248.3-248.6).  The fused
+    // and epilogue reduces keep sc1 (their output is written in token order; nt lost there).
+    const int auto_policy = mode == DEEPEP_MODE_LOCAL ? 4 : 2;
     sh.policy = p.out_rows != nullptr ? 3 : (g_config.store_policy == 3 ? 4 :
-                                              (g_config.store_policy >= 0 ? g_config.store_policy : 2));
+                                              (g_config.store_policy >= 0 ? g_config.store_policy : auto_policy));
     // units_per_block 4 / 8 forces the workgroup shape; 0 = automatic
     sh.waves = p.units_per_block == 4 ? 4 : (p.units_per_block == 8 ? 8 : (mode == DEEPEP_MODE_LOCAL ? 4 : 8));
     // rows in flight per lane: 8 for the fused / epilogue reduces (8 rows per token at EP = 1), 4 for

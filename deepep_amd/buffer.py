@@ -735,7 +735,8 @@ class ElasticBuffer(ExchangeMixin):
             # without a CPU sync N is already the worst case (buffer.hpp:1065-1070): metadata rows past the
             # received ones are -1 (dispatch_count), non-expanded outputs there are zeros / -1
             num_recv = N
-            cloned_idx = topk_idx.clone() if do_handle_copy else topk_idx
+            # the handle's own routing copy (do_handle_copy); a cached call keeps its handle, so nothing to copy
+            cloned_idx = topk_idx.clone() if do_handle_copy and cached is None else topk_idx
         event = None if sync_mode else self._epilogue([x, sf, topk_idx, topk_weights, out_x, out_sf, out_idx, out_w,
                                                        meta], compute_stream, allocate_on_comm_stream,
                                                       async_with_compute_stream)

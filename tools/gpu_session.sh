@@ -63,6 +63,8 @@ for step in "$@"; do
                 export DEEPEP_BENCH_BACKEND=gloo; run bench4gloo 900 python3 bench.py --gpus 4 --steps 4 --warmup 2; unset DEEPEP_BENCH_BACKEND ;;
         kphasea) run kphasea 300 python tools/kphase_a.py ;;
         khost)  run khost 300 python tools/khost.py ;;
+        kprefetch) [ -f tools/libprobe_prefetch.so ] || hipcc --offload-arch=gfx950 -O3 -fPIC -shared -o tools/libprobe_prefetch.so tools/probe_prefetch.hip
+                run kprefetch 400 python tools/kprefetch.py ;;
         bench2gloo) export DEEPEP_BENCH_BACKEND=gloo; run bench2gloo 600 python3 bench.py --gpus 2 --steps 10 --warmup 3; unset DEEPEP_BENCH_BACKEND ;;
         pmc)    for c in FETCH_SIZE WRITE_SIZE TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum; do
                     run pmc_$c 300 timeout -s KILL 120 rocprofv3 --pmc $c -d $OUT/pmc_$c -o pmc --output-format csv -- python3 tools/pmc_run.py

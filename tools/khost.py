@@ -48,6 +48,31 @@ def main():
         torch.cuda.synchronize()
         el = (time.perf_counter() - t0) / n
         print(json.dumps(dict(call=name, us=round(el * 1e6, 1), host_us=round(host / n * 1e6, 1))), flush=True)
+    # The bench's timed region (barrier + sync, K steps, sync + barrier + sync) at several K: the
+    # intercept is the region's fixed cost, which the driver's 20-step run spreads over its steps.
+    step = calls['combine (weighted)']
+    for K in (0, 1, 2, 5, 20, 100):
+        rows = []
+        for _ in range(7):
+            torch.cuda.synchronize()
+            dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            t_first = None
+            for i in range(K):
+                step()
+                if i == 0:
+                    t_first = time.perf_counter() - t0
+            torch.cuda.synchronize()
+            t_sync = time.perf_counter() - t0
+            dist.barrier()
+            t_bar = time.perf_counter() - t0
+            torch.cuda.synchronize()
+            rows.append((time.perf_counter() - t0, t_sync, t_bar, t_first or 0.0))
+        med = sorted(rows)[3]
+        print(json.dumps(dict(region_steps=K, region_us=round(med[0] * 1e6, 1), until_sync_us=round(med[1] * 1e6, 1),
+                              until_barrier_us=round(med[2] * 1e6, 1), first_call_host_us=round(med[3] * 1e6, 1))),
+              flush=True)
     for name, fn in calls.items():
         pr = cProfile.Profile()
         pr.enable()

@@ -909,7 +909,13 @@ int launch_combine(int mode, int weighted, const Params& p_in, deepep_stream_t s
     // rows in flight per lane: 8 for the fused / epilogue reduces (8 rows per token at EP = 1), 4 for
     // phase A (about 1.5 local rows per received token at EP = 8: 64 VGPRs and 8 waves per SIMD beat
     // deeper per-wave loads, tools/kphase.py 252-254 vs 256-260 us, tools/kphase_cu.py)
-    sh.group = g_config.rows_in_flight > 0 ? g_config.rows_in_flight : (mode == DEEPEP_MODE_LOCAL ? 4 : 8);
+    // A unit never has more valid rows than its table is wide, so the rows in flight are capped at the
+    // width rounded up to 2 / 4: registers for rows that never come only cost occupancy (top-2, config-2
+    // shape otherwise: 33.7 vs 40.1 us; top-4: 93.5 vs 95.9 us; tools/kshapes.py, profiles/r04e_kshapes_*, r04f_kshapes_*).
+    const int width = p.table == nullptr ? 1 : p.table_width;
+    const int width_cap = width <= 2 ? 2 : (width <= 4 ? 4 : 8);
+    sh.group = g_config.rows_in_flight > 0 ? g_config.rows_in_flight
+                                           : std::min(mode == DEEPEP_MODE_LOCAL ? 4 : 8, width_cap);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     // A forced streaming kernel (one wave per unit, chunks pipelined) applies only when the shape is
     // automatic: an explicit units_per_block / LDS / rows-in-flight setting selects the item kernel
@@ -955,8 +961,28 @@ int launch_combine(int mode, int weighted, const Params& p_in, deepep_stream_t s
     // 128 CUs 208 vs 235 us on a persistent grid, 32 CUs 603 vs 661 us; the whole chip is unchanged);
     // the streaming kernels and the forced persistent item kernel take a persistent grid sized to it.
     const int budget = budget_cus_of(s);
-    if (budget > 0 && g_config.rows_in_flight == 0) sh.group = 4;
+    if (budget > 0 && g_config.rows_in_flight == 0) sh.group = std::min(4, width_cap);
+    // The EP = 1 fused reduce over wide tables (top-k >= 5) and rows of at least 256 vectors: 1 vector per
+    // lane (1 KiB chunks), 2 rows in flight, 4-wave workgroups -- few registers, many waves.  Three boxes,
+    // same output buffer, medians of 3-5 interleaved rounds (tools/kshapes.py, profiles/r04e_kshapes_*, r04f_kshapes_*):
+    // config 2 172.4 / 171.1 / 173.9 us vs 175.1 / 173.9 / 175.5 (-0.9 to -1.6 %), hidden 4096 -0.9 to
+    // -2.8 %, hidden 2048 -1.4 to -2.2 %, hidden 5120 x top-6 -1.7 to -2.5 %.  Not for phase A (LOCAL:
+    // 295 vs 247 us, tools/kphase_a.py) nor narrower rows (hidden 1024: 2 vectors, 4 rows, 8 waves win).
+    const bool fused_wide = mode == DEEPEP_MODE_FUSED && width >= 5 && nvec >= 256 && budget == 0 &&
+                            g_config.vec_per_lane == 0 && g_config.rows_in_flight == 0 && g_config.stage_lds < 0 &&
+                            p.units_per_block == 0;
+    // hidden 1024 (one 2 KiB item per row): 4 rows in flight, 23.7 / 23.6 vs 25.1 / 25.2 us on two boxes
+    const bool fused_narrow = mode == DEEPEP_MODE_FUSED && width >= 5 && nvec >= 128 && nvec < 256 && budget == 0 &&
+                              g_config.vec_per_lane == 0 && g_config.rows_in_flight == 0 && g_config.stage_lds < 0 &&
+                              p.units_per_block == 0;
     auto launch_choice = [&](int c) {
+        if (c == 0 && fused_wide) {
+            sh.vpt = 1;
+            sh.group = 2;
+            sh.waves = 4;
+        } else if (c == 0 && fused_narrow) {
+            sh.group = 4;
+        }
         p.xcd_blocks = c == 4 ? 1 : 0;
         p.cap_cus = (c == 0 || c == 4 || c == 6) ? 0 : (budget > 0 ? budget : (c == 5 ? device_cus() : 0));
         // the persistent item grid exists for 8 rows in flight only (launch_shape): a capped launch always

@@ -40,50 +40,47 @@ def main():
     row_elems = H + 64                                  # the library's packed row: 14336 + 128 B
     s = torch.cuda.current_stream()
     bytes_a = n_exp * H * 2 + n_recv * (H * 2 + K * 4)
-    variants = []
-    for pol in (2, 3):                                  # launch-config store policy: 2 sc1, 3 sc1 nt
+    # (vpt, store policy, waves, rows in flight); (0, -1, 0, 0) = the automatic shape (sc1 nt, 4 waves,
+    # 4 rows, 2 vectors per lane)
+    variants = [(0, -1, 0, 0)]
+    for vpt in (1, 2):
         for upb in (4, 8):
-            for rif in (4, 8):
-                variants.append((pol, upb, rif))
-    ref = None
-    outs = {}
-    times = {v: [] for v in variants}
+            for rif in (2, 4, 8):
+                variants.append((vpt, 3, upb, rif))
+    variants.append((2, 2, 4, 4))                      # sc1 stores (round 3's default)
     rounds = int(os.environ.get('KPHASE_A_ROUNDS', 5))
+    # one send buffer for every variant (the output's placement alone moves a kernel, tools/koutplace.py)
+    packed = torch.zeros((n_recv, row_elems), dtype=torch.bfloat16, device='cuda')
+    pw = packed.view(torch.float32)[:, H // 2:H // 2 + K]
     for weighted in (True, False):
-        ref = None
+        def launch(upb):
+            kern.combine_reduce(MODE_LOCAL, y, packed[:, :H], n_recv, table=table_a,
+                                row_weights=w if weighted else None, wtable=table_a, wsrc=w,
+                                out_weights=pw, weights_pad=32, units_per_block=upb, stream=s)
+        kern.lib.deepep_set_launch_config(0, -1, -1, 0)
+        launch(0)
+        ref = packed.clone()
+        times = {v: [] for v in variants}
+        same = {v: True for v in variants}
         for rnd in range(rounds):
             for v in variants:
-                pol, upb, rif = v
-                assert kern.lib.deepep_set_launch_config(0, -1, pol, rif) == 0
-                packed = torch.zeros((n_recv, row_elems), dtype=torch.bfloat16, device='cuda')
-                pw = packed.view(torch.float32)[:, H // 2:H // 2 + K]
-
-                def launch():
-                    kern.combine_reduce(MODE_LOCAL, y, packed[:, :H], n_recv, table=table_a,
-                                        row_weights=w if weighted else None, wtable=table_a, wsrc=w,
-                                        out_weights=pw, weights_pad=32, units_per_block=upb, stream=s)
-                us = timeit(launch, s)
-                times[v].append(us)
-                if rnd == 0:
-                    if ref is None:
-                        ref = packed.clone()
-                    outs[v] = torch.equal(packed.view(torch.int16), ref.view(torch.int16))
-                del packed
+                vpt, pol, upb, rif = v
+                assert kern.lib.deepep_set_launch_config(vpt, -1, pol, rif) == 0
+                times[v].append(timeit(lambda: launch(upb), s))
+                same[v] = same[v] and torch.equal(packed.view(torch.int16), ref.view(torch.int16))
         kern.lib.deepep_set_launch_config(0, -1, -1, 0)
         res = []
         for v in variants:
             med = statistics.median(times[v])
             res.append((med, v))
-            print(json.dumps(dict(phase='A', weighted=weighted, store=('sc1', 'sc1 nt')[v[0] - 2], waves=v[1],
-                                  rows_in_flight=v[2], us_median=round(med, 1), us_all=[round(t, 1) for t in times[v]],
-                                  gbps=round(bytes_a / med / 1e3, 1), frac=round(bytes_a / med / 1e3 / 8000, 4),
-                                  bitwise_equal=outs[v])), flush=True)
-            times[v] = []
+            print(json.dumps(dict(phase='A', weighted=weighted, vpt=v[0], store={-1: 'auto', 2: 'sc1', 3: 'sc1 nt'}[v[1]],
+                                  waves=v[2], rows_in_flight=v[3], us_median=round(med, 1),
+                                  us_all=[round(t, 1) for t in times[v]], gbps=round(bytes_a / med / 1e3, 1),
+                                  frac=round(bytes_a / med / 1e3 / 8000, 4), bitwise_equal=same[v])), flush=True)
         best = min(res)
-        print(json.dumps(dict(phase='A_best', weighted=weighted, us=round(best[0], 1),
-                              store=('sc1', 'sc1 nt')[best[1][0] - 2], waves=best[1][1], rows_in_flight=best[1][2],
-                              units=n_recv, rows=n_exp, bytes=bytes_a)), flush=True)
-
+        print(json.dumps(dict(phase='A_best', weighted=weighted, us=round(best[0], 1), variant=best[1],
+                              auto_us=round(statistics.median(times[variants[0]]), 1), units=n_recv, rows=n_exp,
+                              bytes=bytes_a)), flush=True)
 
 if __name__ == '__main__':
     main()

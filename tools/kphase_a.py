@@ -18,7 +18,7 @@ def main():
     torch.cuda.set_device(0)
     from deepep_amd.kernels import HipKernels, MODE_LOCAL
     kern = HipKernels()
-    R, T, H, K, E = 8, 8192, 7168, 8, 256
+    R, T, H, K, E = int(os.environ.get('KPHASE_A_R', 8)), 8192, 7168, 8, 256
     epr = E // R
     g = torch.Generator(device='cuda').manual_seed(0)
     idx = torch.stack([torch.topk(torch.rand((T, E), device='cuda', generator=g), K, dim=-1)[1] for _ in range(R)])
@@ -73,12 +73,12 @@ def main():
         for v in variants:
             med = statistics.median(times[v])
             res.append((med, v))
-            print(json.dumps(dict(phase='A', weighted=weighted, vpt=v[0], store={-1: 'auto', 2: 'sc1', 3: 'sc1 nt'}[v[1]],
+            print(json.dumps(dict(phase='A', ranks=R, weighted=weighted, vpt=v[0], store={-1: 'auto', 2: 'sc1', 3: 'sc1 nt'}[v[1]],
                                   waves=v[2], rows_in_flight=v[3], us_median=round(med, 1),
                                   us_all=[round(t, 1) for t in times[v]], gbps=round(bytes_a / med / 1e3, 1),
                                   frac=round(bytes_a / med / 1e3 / 8000, 4), bitwise_equal=same[v])), flush=True)
         best = min(res)
-        print(json.dumps(dict(phase='A_best', weighted=weighted, us=round(best[0], 1), variant=best[1],
+        print(json.dumps(dict(phase='A_best', ranks=R, weighted=weighted, us=round(best[0], 1), variant=best[1],
                               auto_us=round(statistics.median(times[variants[0]]), 1), units=n_recv, rows=n_exp,
                               bytes=bytes_a)), flush=True)
 

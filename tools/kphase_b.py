@@ -21,12 +21,21 @@ def main():
     kern = HipKernels()
     T, H, K, E = 8192, 7168, 8, 256
     s = torch.cuda.current_stream()
-    for R in (2, 4, 8):
+    for R in (1, 2, 4, 8):
         g = torch.Generator(device='cuda').manual_seed(R)
-        idx = torch.topk(torch.rand((T, E), device='cuda', generator=g), K, dim=-1)[1]
-        table_b, _, back = epilogue_tables(idx, E, R)
-        n_back = sum(back)
-        recv = torch.randn((n_back, H + 64), device='cuda', generator=g).to(torch.bfloat16)
+        wts = None
+        if R == 1:
+            # the single reduction's reduce (one weighted EPILOGUE over a token's K unreduced rows in the
+            # [K, T] receive window), the bench's single_reduction_phase_b
+            table_b = (torch.arange(K, device='cuda').view(1, K) * T +
+                       torch.arange(T, device='cuda').view(T, 1)).to(torch.int32).contiguous()
+            recv = torch.randn((K * T, H + 64), device='cuda', generator=g).to(torch.bfloat16)
+            wts = torch.rand((K * T,), device='cuda', generator=g)
+        else:
+            idx = torch.topk(torch.rand((T, E), device='cuda', generator=g), K, dim=-1)[1]
+            table_b, _, back = epilogue_tables(idx, E, R)
+            n_back = sum(back)
+            recv = torch.randn((n_back, H + 64), device='cuda', generator=g).to(torch.bfloat16)
         out = torch.empty((T, H), dtype=torch.bfloat16, device='cuda')
         valid = int((table_b >= 0).sum())
         nbytes = valid * H * 2 + T * H * 2 + valid * 4
@@ -35,14 +44,14 @@ def main():
             for rows in (2, 4, 8):
                 for waves in (4, 8):
                     variants[f'vpt{vpt} rows{rows} waves{waves}'] = ((vpt, -1, -1, rows), waves)
-        kern.combine_reduce(MODE_EPILOGUE, recv[:, :H], out, T, table=table_b, stream=s)
+        kern.combine_reduce(MODE_EPILOGUE, recv[:, :H], out, T, table=table_b, row_weights=wts, stream=s)
         ref = out.clone()
         times, bitwise = {k: [] for k in variants}, {k: True for k in variants}
         for _ in range(int(os.environ.get('KPHASE_B_ROUNDS', 4))):
             for name, (cfg, upb) in variants.items():
                 assert kern.lib.deepep_set_launch_config(*cfg) == 0
                 times[name].append(timeit(lambda: kern.combine_reduce(MODE_EPILOGUE, recv[:, :H], out, T, table=table_b,
-                                                                      units_per_block=upb, stream=s), s, iters=30))
+                                                                      row_weights=wts, units_per_block=upb, stream=s), s, iters=30))
                 bitwise[name] = bitwise[name] and bool(torch.equal(out, ref))
         kern.lib.deepep_set_launch_config(0, -1, -1, 0)
         res = {k: dict(us=round(statistics.median(v), 2), frac=round(nbytes / statistics.median(v) / 8e6, 4),

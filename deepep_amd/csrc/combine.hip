@@ -172,6 +172,13 @@ constexpr int kAuxSys = 17;
 // Write-through streaming (sc1 nt): what the dispatch's blocked expanded copy stores with (dispatch.hip);
 // a launch-config option here (store_policy 3), measured against sc1 in tools/kbisect.py.
 constexpr int kAuxSC1NT = 18;
+// Phase A's default: per unit, sc1 when the unit reduces >= 3 rows, sc1 nt otherwise.  EP = 2 / 4 / 8 rank
+// shares of config 3 (tools/kphase_a.py, medians of 4-5 interleaved rounds, two boxes): 187.1-188.2 /
+// 201.7-203.3 / 237.9-238.1 us weighted vs 200.5-202.6 / 220.3-222.0 / 245.9-246.3 with sc1 nt everywhere
+// (the round-4 default) and 185.1-185.8 / 225.2-227.8 / 247.7-248.0 with sc1 everywhere (round 3).  A
+// threshold of 2 or 4 rows, or every 2nd / 4th unit streamed, lost at some EP size (profiles/r04g_kphasea_*).
+// Never passed to the store builtin itself.
+constexpr int kAuxPerUnit = 1003;     // 1000 + the row threshold
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void* row, int bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(row), 0, bytes, 0x00020000);
@@ -338,9 +345,21 @@ __device__ __forceinline__ void combine_item(const Params& p, int64_t it, int nc
         for (int v = 0; v < kVPT; ++v) result[v] = (u32x4){0x7fc07fc0u, 0x7fc07fc0u, 0x7fc07fc0u, 0x7fc07fc0u};
     }
     const __amdgpu_buffer_rsrc_t orow = row_rsrc(out_row, p.hidden * 2);
+    if constexpr (kStoreAux > 1000) {
+        if (n >= kStoreAux - 1000) {
 #pragma unroll
-    for (int v = 0; v < kVPT; ++v)
-        __builtin_amdgcn_raw_buffer_store_b128(result[v], orow, vidx[v] * 16, 0, kStoreAux);
+            for (int v = 0; v < kVPT; ++v)
+                __builtin_amdgcn_raw_buffer_store_b128(result[v], orow, vidx[v] * 16, 0, kAuxSC1);
+        } else {
+#pragma unroll
+            for (int v = 0; v < kVPT; ++v)
+                __builtin_amdgcn_raw_buffer_store_b128(result[v], orow, vidx[v] * 16, 0, kAuxSC1NT);
+        }
+    } else {
+#pragma unroll
+        for (int v = 0; v < kVPT; ++v)
+            __builtin_amdgcn_raw_buffer_store_b128(result[v], orow, vidx[v] * 16, 0, kStoreAux);
+    }
     if (wlane) store_weight(p, u, out_row, lane, wv);
 }
 
@@ -641,7 +660,7 @@ template <int kMode, bool kWeighted, int kVPT, bool kFull, int kAux>
 void launch_lds(const Params& p, bool lds, int waves, int group, hipStream_t stream) {
     const int nvec = p.hidden / 8;
     const int64_t items = static_cast<int64_t>(p.num_units) * ((nvec + 64 * kVPT - 1) / (64 * kVPT));
-    if constexpr (kAux == kAuxSC1 || kAux == kAuxSys || kAux == kAuxSC1NT) {
+    if constexpr (kAux == kAuxSC1 || kAux == kAuxSys || kAux == kAuxSC1NT || kAux > 1000) {
         if (lds) {
             if (waves == 8) {
                 if (group == 2) launch_shape<kMode, kWeighted, kVPT, kFull, kAux, true, 8, 2>(p, items, stream);
@@ -670,6 +689,10 @@ void launch_aux(const Params& p, const Shape& sh, hipStream_t stream) {
     else if (sh.policy == 1) launch_lds<kMode, kWeighted, kVPT, kFull, kAuxNT>(p, sh.lds, sh.waves, sh.group, stream);
     else if (sh.policy == 3) launch_lds<kMode, kWeighted, kVPT, kFull, kAuxSys>(p, sh.lds, sh.waves, sh.group, stream);
     else if (sh.policy == 4) launch_lds<kMode, kWeighted, kVPT, kFull, kAuxSC1NT>(p, sh.lds, sh.waves, sh.group, stream);
+    else if (sh.policy == 5) {
+        if constexpr (kMode == DEEPEP_MODE_LOCAL) launch_lds<kMode, kWeighted, kVPT, kFull, kAuxPerUnit>(p, sh.lds, sh.waves, sh.group, stream);
+        else launch_lds<kMode, kWeighted, kVPT, kFull, kAuxSC1>(p, sh.lds, sh.waves, sh.group, stream);
+    }
     else launch_lds<kMode, kWeighted, kVPT, kFull, kAuxSC1>(p, sh.lds, sh.waves, sh.group, stream);
 }
 
@@ -896,13 +919,13 @@ int launch_combine(int mode, int weighted, const Params& p_in, deepep_stream_t s
     if (sh.vpt != 1 && sh.vpt != 2) sh.vpt = 2;
     sh.lds = g_config.stage_lds >= 0 ? g_config.stage_lds != 0 : true;
     // store policies: 0 plain, 1 nt, 2 sc1 (fused / epilogue default), 3 system scope (peer windows),
-    // 4 sc1 nt (phase A default).  Phase A's packed send rows are written once and read back only by the
-    // exchange, so they stream past L2 (sc1 nt): EP = 8 rank share of config 3, tools/kphase_a.py,
-    // medians of 5 interleaved rounds, 4-wave workgroups x 4 rows in flight: 248.9 vs 251.4 us weighted,
-    // 252.1 vs 253.8 plain (profiles/r04a_kphasea.jsonl; round 3: 245.0-246.9 vs 248.3-248.6).  The fused
-    // and epilogue reduces keep sc1 (their output is written in token order; nt lost there).
-    const int auto_policy = mode == DEEPEP_MODE_LOCAL ? 4 : 2;
-    sh.policy = p.out_rows != nullptr ? 3 : (g_config.store_policy == 3 ? 4 :
+    // 4 sc1 nt, 5 per unit (phase A default: sc1 when the unit reduces >= 3 rows, else sc1 nt; measured at
+    // kAuxPerUnit).  Phase A's packed send rows are written once and read back only by the exchange; sc1 nt
+    // everywhere was round 4's first step (EP = 8: 248.9 vs 251.4 us with sc1, profiles/r04a_kphasea.jsonl),
+    // the per-unit mix beats both at EP = 2, 4 and 8.  The fused and epilogue reduces keep sc1 (their output
+    // is written in token order; nt, sc1 nt and mixes lost there, DESIGN.md 3, profiles/r04g_*).
+    const int auto_policy = mode == DEEPEP_MODE_LOCAL ? 5 : 2;
+    sh.policy = p.out_rows != nullptr ? 3 : (g_config.store_policy == 4 ? 5 : g_config.store_policy == 3 ? 4 :
                                               (g_config.store_policy >= 0 ? g_config.store_policy : auto_policy));
     // units_per_block 4 / 8 forces the workgroup shape; 0 = automatic
     sh.waves = p.units_per_block == 4 ? 4 : (p.units_per_block == 8 ? 8 : (mode == DEEPEP_MODE_LOCAL ? 4 : 8));
@@ -1051,7 +1074,7 @@ int deepep_last_kernel_choice(void) { return g_last_choice; }
 
 int deepep_set_launch_config(int vec_per_lane, int stage_lds, int store_policy, int rows_in_flight) {
     if (vec_per_lane < 0 || vec_per_lane > 2 || stage_lds < -1 || stage_lds > 1 || store_policy < -1 ||
-        store_policy > 3 || (rows_in_flight != 0 && rows_in_flight != 2 && rows_in_flight != 4 && rows_in_flight != 8))
+        store_policy > 4 || (rows_in_flight != 0 && rows_in_flight != 2 && rows_in_flight != 4 && rows_in_flight != 8))
         return set_error(DEEPEP_ERR_INVALID_ARG, "invalid launch configuration");
     g_config.vec_per_lane = vec_per_lane;
     g_config.stage_lds = stage_lds;

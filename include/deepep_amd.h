@@ -149,10 +149,14 @@ int deepep_build_local_plan(const int32_t* src_metadata, int num_recv_tokens, in
  *   vec_per_lane   16-byte vectors each lane loads per source row and item (1 or 2)
  *   stage_lds      1: stage the slot table / weights per workgroup in LDS; 0: per wave in registers
  *   store_policy   output store cache policy: 0 plain, 1 nt, 2 sc1 (write-through), 3 sc1 nt (the two
- *                  default shapes only: 8 x 8 rows in flight / 4 x 4)
+ *                  default shapes only: 8 x 8 rows in flight / 4 x 4), 4 per unit (sc1 when the unit
+ *                  reduces >= 3 rows, else sc1 nt; phase A only, other modes: sc1).  Automatic: per unit
+ *                  for phase A, sc1 for the fused and epilogue reduces.
  *   rows_in_flight source rows each lane loads before accumulating them (2, 4 or 8; LDS staging with
- *                  sc1 or system-scope stores only).  Automatic: 8 for the fused / epilogue reduces,
- *                  4 for phase A (DEEPEP_MODE_LOCAL) and for every launch on a CU-budget stream.
+ *                  sc1 or system-scope stores only).  Automatic: at most the slot table's width rounded
+ *                  up to 2 / 4 / 8; 2 (with 1 vector per lane, 4-wave workgroups) for the fused reduce
+ *                  over top-k >= 5, 8 for the epilogue, 4 for phase A (DEEPEP_MODE_LOCAL) and for every
+ *                  launch on a CU-budget stream.
  * The results are identical for every configuration; only the speed changes.
  */
 int deepep_set_launch_config(int vec_per_lane, int stage_lds, int store_policy, int rows_in_flight);

@@ -124,7 +124,8 @@ def test_kernel_units_per_block(kern, upb):
 
 
 @pytest.mark.parametrize('cfg', [(1, 0, 0, 0), (1, 1, 1, 0), (2, 0, 1, 0), (2, 1, 0, 0), (2, 0, 2, 0), (0, -1, -1, 0),
-                                 (0, -1, -1, 2), (0, -1, -1, 4), (1, 1, 2, 2)])
+                                 (0, -1, -1, 2), (0, -1, -1, 4), (1, 1, 2, 2), (2, 1, 3, 4), (0, -1, 4, 0),
+                                 (2, 1, 2, 8)])
 @pytest.mark.parametrize('upb', [0, 4, 8])
 def test_kernel_launch_configs_identical(kern, cfg, upb):
     """Every deepep_set_launch_config variant (vector width, LDS staging, store policy, rows in

@@ -43,11 +43,16 @@ def main():
     # (vpt, store policy, waves, rows in flight); (0, -1, 0, 0) = the automatic shape (sc1 nt, 4 waves,
     # 4 rows, 2 vectors per lane)
     variants = [(0, -1, 0, 0)]
-    for vpt in (1, 2):
-        for upb in (4, 8):
-            for rif in (2, 4, 8):
-                variants.append((vpt, 3, upb, rif))
-    variants.append((2, 2, 4, 4))                      # sc1 stores (round 3's default)
+    if os.environ.get('KPHASE_A_FULL') == '1':
+        for vpt in (1, 2):
+            for upb in (4, 8):
+                for rif in (2, 4, 8):
+                    variants.append((vpt, 3, upb, rif))
+    # store policies at the automatic shape (2 vectors, 4 waves, 4 rows): sc1, sc1 nt, per unit (sc1 when
+    # the unit reduces >= 3 rows, else sc1 nt; the default).  Round 4 also tried thresholds 2 / 4 and every
+    # 2nd / 4th unit streamed (profiles/r04g_kphasea_*).
+    for pol in (2, 3, 4):
+        variants.append((2, pol, 4, 4))
     rounds = int(os.environ.get('KPHASE_A_ROUNDS', 5))
     # one send buffer for every variant (the output's placement alone moves a kernel, tools/koutplace.py)
     packed = torch.zeros((n_recv, row_elems), dtype=torch.bfloat16, device='cuda')
@@ -73,7 +78,7 @@ def main():
         for v in variants:
             med = statistics.median(times[v])
             res.append((med, v))
-            print(json.dumps(dict(phase='A', ranks=R, weighted=weighted, vpt=v[0], store={-1: 'auto', 2: 'sc1', 3: 'sc1 nt'}[v[1]],
+            print(json.dumps(dict(phase='A', ranks=R, weighted=weighted, vpt=v[0], store={-1: 'auto', 2: 'sc1', 3: 'sc1 nt', 4: 'per unit >= 3'}[v[1]],
                                   waves=v[2], rows_in_flight=v[3], us_median=round(med, 1),
                                   us_all=[round(t, 1) for t in times[v]], gbps=round(bytes_a / med / 1e3, 1),
                                   frac=round(bytes_a / med / 1e3 / 8000, 4), bitwise_equal=same[v])), flush=True)

@@ -40,10 +40,16 @@ def main():
         valid = int((table_b >= 0).sum())
         nbytes = valid * H * 2 + T * H * 2 + valid * 4
         variants = {'auto': ((0, -1, -1, 0), 0)}
-        for vpt in (1, 2):
-            for rows in (2, 4, 8):
-                for waves in (4, 8):
-                    variants[f'vpt{vpt} rows{rows} waves{waves}'] = ((vpt, -1, -1, rows), waves)
+        if os.environ.get('KPHASE_B_SHAPES') == '1':
+            for vpt in (1, 2):
+                for rows in (2, 4, 8):
+                    for waves in (4, 8):
+                        variants[f'vpt{vpt} rows{rows} waves{waves}'] = ((vpt, -1, -1, rows), waves)
+        # store policies at the automatic shape: sc1 nt, per unit (sc1 when the token reduces >= 3 partial
+        # rows, else sc1 nt); round 4 also tried thresholds 2 / 4 and every 2nd / 4th token streamed
+        # (profiles/r04g_kphaseb.jsonl): none beat sc1
+        for pol, name in ((3, 'sc1nt'), (4, 'per unit >= 3')):
+            variants[name] = ((0, -1, pol, 0), 0)
         kern.combine_reduce(MODE_EPILOGUE, recv[:, :H], out, T, table=table_b, row_weights=wts, stream=s)
         ref = out.clone()
         times, bitwise = {k: [] for k in variants}, {k: True for k in variants}

@@ -38,7 +38,7 @@ def binary_build_id(path: str) -> Optional[str]:
         data = f.read()
     i = data.find(b'DEEPEP_BUILD_ID=')
     return data[i + 16:i + 32].decode(errors='replace') if i >= 0 else None
-ABI_VERSION = 14
+ABI_VERSION = 13
 
 MODE_LOCAL, MODE_EPILOGUE, MODE_FUSED = 0, 1, 2
 
@@ -92,7 +92,6 @@ SIGNATURES = {
                                    _P]),
     'deepep_build_local_plan': (_I, [_P, _I, _I, _I, _I, _P, _I, _I, _P, _P, _P]),
     'deepep_set_launch_config': (_I, [_I, _I, _I, _I]),
-    'deepep_set_dispatch_copy_policy': (_I, [_I]),
     'deepep_set_kernel_choice': (_I, [_I]),
     'deepep_last_kernel_choice': (_I, []),
     'deepep_combine_buffer_size': (_I64, [_I, _I, _I, _I, _I]),

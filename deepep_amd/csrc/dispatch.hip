@@ -613,27 +613,8 @@ copy_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int x_bytes, 
 // write-through (sc1 nt).  Measured at BASELINE config 2 (tools/probe_copy.py, two boxes): 151.4 vs
 // 163.5 us and 182.0 vs 213.6 us for the source-major copy (one load, up to K scattered stores).
 constexpr int kCopyAux = 18;                          // sc1 | nt
-constexpr int kAuxSC1 = 16;
 
-// Store policy of the expanded copy's rows (deepep_set_dispatch_copy_policy, tuning): 0 sc1 nt (the default),
-// 1 sc1, 2 nt, 3 plain, 4 sc1 on odd destination rows / sc1 nt on even ones, 5 sc1 on odd local experts,
-// 6 sc1 on every 4th destination row.
-int g_copy_policy = 0;
-
-template <int kPolicy>
-__device__ __forceinline__ void copy_store(const u32x4& v, __amdgpu_buffer_rsrc_t rs, int off, int64_t d, int e) {
-    if constexpr (kPolicy == 0) __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, kCopyAux);
-    else if constexpr (kPolicy == 1) __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, kAuxSC1);
-    else if constexpr (kPolicy == 2) __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 2);
-    else if constexpr (kPolicy == 3) __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 0);
-    else {
-        const bool sc1 = kPolicy == 4 ? (d & 1) != 0 : (kPolicy == 5 ? (e & 1) != 0 : (d & 3) == 0);
-        if (sc1) __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, kAuxSC1);
-        else __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, kCopyAux);
-    }
-}
-
-template <bool kDirect, int kPolicy>
+template <bool kDirect>
 __global__ void __launch_bounds__(256)
 copy_expanded_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int x_bytes, int sf_off, int sf_bytes,
                      int w_off, int N, int K, const int32_t* __restrict__ meta,
@@ -698,8 +679,8 @@ copy_expanded_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int 
             // the descriptor's range check drops the lanes past the row end
             const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(recv_x + d * x_bytes, 0, x_bytes,
                                                                                 0x00020000);
-            copy_store<kPolicy>(a[q][0], rs, v0 * 16, d, e);
-            copy_store<kPolicy>(a[q][1], rs, v1 * 16, d, e);
+            __builtin_amdgcn_raw_buffer_store_b128(a[q][0], rs, v0 * 16, 0, kCopyAux);
+            __builtin_amdgcn_raw_buffer_store_b128(a[q][1], rs, v1 * 16, 0, kCopyAux);
             if (c != 0) continue;
             if (recv_sf != nullptr) {
                 const uint8_t* sfs;
@@ -942,16 +923,8 @@ int deepep_dispatch_copy(const void* packed, int64_t row_bytes, int x_bytes, int
                                static_cast<uint8_t*>(recv_x), static_cast<uint8_t*>(recv_sf), recv_topk_weights,
                                num_out_rows, row_map, error_flag);
         };
-        switch (g_copy_policy) {
-#define DEEPEP_COPY(P) \
-            case P: if (x_direct != nullptr) launch(copy_expanded_kernel<true, P>); \
-                    else launch(copy_expanded_kernel<false, P>); break;
-            DEEPEP_COPY(1) DEEPEP_COPY(2) DEEPEP_COPY(3) DEEPEP_COPY(4) DEEPEP_COPY(5) DEEPEP_COPY(6)
-#undef DEEPEP_COPY
-            default:
-                if (x_direct != nullptr) launch(copy_expanded_kernel<true, 0>);
-                else launch(copy_expanded_kernel<false, 0>);
-        }
+        if (x_direct != nullptr) launch(copy_expanded_kernel<true>);
+        else launch(copy_expanded_kernel<false>);
         return launch_status("dispatch_copy");
     }
     const int64_t nchunks = std::max<int64_t>(1, (x_bytes / 16 + 127) / 128);
@@ -965,13 +938,6 @@ int deepep_dispatch_copy(const void* packed, int64_t row_bytes, int x_bytes, int
                        static_cast<uint8_t*>(recv_x), static_cast<uint8_t*>(recv_sf), recv_topk_weights,
                        num_out_rows, row_map, error_flag);
     return launch_status("dispatch_copy");
-}
-
-int deepep_set_dispatch_copy_policy(int policy) {
-    if (policy < 0 || policy > 6)
-        return deepep_amd_set_error(DEEPEP_ERR_INVALID_ARG, "dispatch copy policy must be 0..6");
-    g_copy_policy = policy;
-    return DEEPEP_OK;
 }
 
 }  // extern "C"

@@ -48,7 +48,7 @@ extern "C" {
 
 typedef struct ihipStream_t* deepep_stream_t;   /* == hipStream_t */
 
-#define DEEPEP_AMD_ABI_VERSION 14
+#define DEEPEP_AMD_ABI_VERSION 13
 
 #define DEEPEP_OK               0
 #define DEEPEP_ERR_INVALID_ARG  (-1)
@@ -160,14 +160,6 @@ int deepep_build_local_plan(const int32_t* src_metadata, int num_recv_tokens, in
  * The results are identical for every configuration; only the speed changes.
  */
 int deepep_set_launch_config(int vec_per_lane, int stage_lds, int store_policy, int rows_in_flight);
-
-/*
- * Tuning / diagnostics (process-global): the store policy of the dispatch's expanded copy
- * (deepep_dispatch_copy with inv): 0 sc1 nt (the default), 1 sc1, 2 nt, 3 plain, 4 sc1 on odd destination
- * rows, 5 sc1 on odd local experts, 6 sc1 on every 4th destination row (sc1 nt elsewhere).  Identical bytes
- * for every policy.  ABI v14.
- */
-int deepep_set_dispatch_copy_policy(int policy);
 
 /*
  * Kernel for deepep_combine_reduce / _scatter when the shape is automatic (units_per_block 0, default

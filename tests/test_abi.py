@@ -33,7 +33,7 @@ def test_exports_every_declared_symbol(lib):
 
 
 def test_abi_version(lib):
-    assert lib.deepep_amd_abi_version() == 14
+    assert lib.deepep_amd_abi_version() == 13
 
 
 def test_build_id_matches_sources(lib):

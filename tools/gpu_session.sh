@@ -66,7 +66,6 @@ for step in "$@"; do
         kshapes) run kshapes 400 python tools/kshapes.py ;;
         koutplace) run koutplace 300 python tools/koutplace.py ;;
         kphaseb) run kphaseb 300 python tools/kphase_b.py ;;
-        kcopypol) run kcopypol 300 python tools/kcopy_policy.py ;;
         kprefetch) [ -f tools/libprobe_prefetch.so ] || hipcc --offload-arch=gfx950 -O3 -fPIC -shared -o tools/libprobe_prefetch.so tools/probe_prefetch.hip
                 run kprefetch 400 python tools/kprefetch.py ;;
         bench2gloo) export DEEPEP_BENCH_BACKEND=gloo; run bench2gloo 600 python3 bench.py --gpus 2 --steps 10 --warmup 3; unset DEEPEP_BENCH_BACKEND ;;

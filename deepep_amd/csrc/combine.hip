@@ -172,12 +172,12 @@ constexpr int kAuxSys = 17;
 // Write-through streaming (sc1 nt): what the dispatch's blocked expanded copy stores with (dispatch.hip);
 // a launch-config option here (store_policy 3), measured against sc1 in tools/kbisect.py.
 constexpr int kAuxSC1NT = 18;
-// Phase A's default: per unit, sc1 when the unit reduces >= 3 rows, sc1 nt otherwise.  EP = 2 / 4 / 8 rank
-// shares of config 3 (tools/kphase_a.py, medians of 4-5 interleaved rounds, two boxes): 187.1-188.2 /
-// 201.7-203.3 / 237.9-238.1 us weighted vs 200.5-202.6 / 220.3-222.0 / 245.9-246.3 with sc1 nt everywhere
-// (the round-4 default) and 185.1-185.8 / 225.2-227.8 / 247.7-248.0 with sc1 everywhere (round 3).  A
-// threshold of 2 or 4 rows, or every 2nd / 4th unit streamed, lost at some EP size (profiles/r04g_kphasea_*).
-// Never passed to the store builtin itself.
+// Per unit (launch-config store policy 4): sc1 when the unit reduces >= 3 rows, sc1 nt otherwise.  Phase A at
+// EP = 2 / 4 / 8 (tools/kphase_a.py, profiles/r04g_kphasea_*, r04i_kphasea_cache_state.jsonl): back to back
+// into the same send rows it beats sc1 nt everywhere by 3.5-12 %, but how much depends on what the caches
+// hold: after a 512 MB write flush (dirty lines, as a GEMM that has just written the expert rows leaves them)
+// it is 7 % slower at EP = 2 and 4 and equal at EP = 8; sc1 nt is within 2 % in every state.  So phase A keeps
+// sc1 nt by default.  Never passed to the store builtin itself.
 constexpr int kAuxPerUnit = 1003;     // 1000 + the row threshold
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void* row, int bytes) {
@@ -919,12 +919,12 @@ int launch_combine(int mode, int weighted, const Params& p_in, deepep_stream_t s
     if (sh.vpt != 1 && sh.vpt != 2) sh.vpt = 2;
     sh.lds = g_config.stage_lds >= 0 ? g_config.stage_lds != 0 : true;
     // store policies: 0 plain, 1 nt, 2 sc1 (fused / epilogue default), 3 system scope (peer windows),
-    // 4 sc1 nt, 5 per unit (phase A default: sc1 when the unit reduces >= 3 rows, else sc1 nt; measured at
-    // kAuxPerUnit).  Phase A's packed send rows are written once and read back only by the exchange; sc1 nt
-    // everywhere was round 4's first step (EP = 8: 248.9 vs 251.4 us with sc1, profiles/r04a_kphasea.jsonl),
-    // the per-unit mix beats both at EP = 2, 4 and 8.  The fused and epilogue reduces keep sc1 (their output
-    // is written in token order; nt, sc1 nt and mixes lost there, DESIGN.md 3, profiles/r04g_*).
-    const int auto_policy = mode == DEEPEP_MODE_LOCAL ? 5 : 2;
+    // 4 sc1 nt (phase A default), 5 per unit (kAuxPerUnit; opt-in).  Phase A's packed send rows are written
+    // once and read back only by the exchange, so they stream past L2 (sc1 nt): EP = 8, back to back, 248.9 vs
+    // 251.4 us with sc1 (profiles/r04a_kphasea.jsonl), and the only policy within 2 % of the best in every
+    // cache state measured (r04i_kphasea_cache_state.jsonl).  The fused and epilogue reduces keep sc1 (their
+    // output is written in token order; sc1 is best or tied in every cache state, r04i_kshapes_cache_state.jsonl).
+    const int auto_policy = mode == DEEPEP_MODE_LOCAL ? 4 : 2;
     sh.policy = p.out_rows != nullptr ? 3 : (g_config.store_policy == 4 ? 5 : g_config.store_policy == 3 ? 4 :
                                               (g_config.store_policy >= 0 ? g_config.store_policy : auto_policy));
     // units_per_block 4 / 8 forces the workgroup shape; 0 = automatic

@@ -150,7 +150,7 @@ int deepep_build_local_plan(const int32_t* src_metadata, int num_recv_tokens, in
  *   stage_lds      1: stage the slot table / weights per workgroup in LDS; 0: per wave in registers
  *   store_policy   output store cache policy: 0 plain, 1 nt, 2 sc1 (write-through), 3 sc1 nt (the two
  *                  default shapes only: 8 x 8 rows in flight / 4 x 4), 4 per unit (sc1 when the unit
- *                  reduces >= 3 rows, else sc1 nt; phase A only, other modes: sc1).  Automatic: per unit
+ *                  reduces >= 3 rows, else sc1 nt; phase A only, other modes: sc1).  Automatic: sc1 nt
  *                  for phase A, sc1 for the fused and epilogue reduces.
  *   rows_in_flight source rows each lane loads before accumulating them (2, 4 or 8; LDS staging with
  *                  sc1 or system-scope stores only).  Automatic: at most the slot table's width rounded

@@ -66,6 +66,14 @@ for step in "$@"; do
         kshapes) run kshapes 400 python tools/kshapes.py ;;
         koutplace) run koutplace 300 python tools/koutplace.py ;;
         kphaseb) run kphaseb 300 python tools/kphase_b.py ;;
+        pmcpolicy) # phase A's store policies at EP = 4 under memory-side and L2 counters (one pass per counter set)
+                i=0
+                for cs in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum"; do
+                    i=$((i+1))
+                    run pmcpol_$i 200 timeout -s KILL 150 rocprofv3 --pmc $cs -d $OUT/pmcpol_$i -o pmc --output-format csv -- python3 tools/pmc_policy.py 4
+                done
+                run pmcpolfold 60 python tools/summarize_prof.py policy $OUT/pmc_policy.json $OUT/pmc_policy_meta.json \
+                    $(find $OUT/pmcpol_1 $OUT/pmcpol_2 $OUT/pmcpol_3 $OUT/pmcpol_4 -name '*counter_collection.csv') ;;
         kprefetch) [ -f tools/libprobe_prefetch.so ] || hipcc --offload-arch=gfx950 -O3 -fPIC -shared -o tools/libprobe_prefetch.so tools/probe_prefetch.hip
                 run kprefetch 400 python tools/kprefetch.py ;;
         bench2gloo) export DEEPEP_BENCH_BACKEND=gloo; run bench2gloo 600 python3 bench.py --gpus 2 --steps 10 --warmup 3; unset DEEPEP_BENCH_BACKEND ;;

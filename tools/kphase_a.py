@@ -82,6 +82,42 @@ def main():
                                   waves=v[2], rows_in_flight=v[3], us_median=round(med, 1),
                                   us_all=[round(t, 1) for t in times[v]], gbps=round(bytes_a / med / 1e3, 1),
                                   frac=round(bytes_a / med / 1e3 / 8000, 4), bitwise_equal=same[v])), flush=True)
+        if os.environ.get('KPHASE_A_FLUSH') == '1':
+            # the cache state before a launch: back to back into the same rows (the loop above), back to back
+            # alternating between two send buffers, and single launches after a 512 MB read / write flush
+            flush = torch.empty((512 << 20) // 4, dtype=torch.int32, device='cuda')
+            sink = torch.empty((1,), dtype=torch.int64, device='cuda')
+            packed2 = torch.zeros_like(packed)
+            pw2 = packed2.view(torch.float32)[:, H // 2:H // 2 + K]
+
+            def launch_into(pk, pkw):
+                kern.combine_reduce(MODE_LOCAL, y, pk[:, :H], n_recv, table=table_a,
+                                    row_weights=w if weighted else None, wtable=table_a, wsrc=w,
+                                    out_weights=pkw, weights_pad=32, stream=s)
+            for pol in (2, 3, 4):
+                assert kern.lib.deepep_set_launch_config(0, -1, pol, 0) == 0
+                flip = [0]
+
+                def alt():
+                    flip[0] ^= 1
+                    launch_into(packed2 if flip[0] else packed, pw2 if flip[0] else pw)
+                row = dict(alternating_buffers=round(timeit(alt, s, iters=30), 1))
+                for mode, pre in (('read_flush', lambda: torch.sum(flush, dim=0, dtype=torch.int64, out=sink)),
+                                  ('write_flush', lambda: flush.fill_(1))):
+                    ts = []
+                    for _ in range(20):
+                        pre()
+                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        e0.record(s)
+                        launch_into(packed, pw)
+                        e1.record(s)
+                        torch.cuda.synchronize()
+                        ts.append(e0.elapsed_time(e1) * 1e3)
+                    row[mode] = round(statistics.median(ts), 1)
+                print(json.dumps(dict(phase='A_cache_state', ranks=R, weighted=weighted,
+                                      store={2: 'sc1', 3: 'sc1 nt', 4: 'per unit >= 3'}[pol], **row)), flush=True)
+            kern.lib.deepep_set_launch_config(0, -1, -1, 0)
+            del flush, packed2
         best = min(res)
         print(json.dumps(dict(phase='A_best', ranks=R, weighted=weighted, us=round(best[0], 1), variant=best[1],
                               auto_us=round(statistics.median(times[variants[0]]), 1), units=n_recv, rows=n_exp,

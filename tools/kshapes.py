@@ -91,6 +91,36 @@ def main():
         for name in variants:
             us = statistics.median(times[name])
             res[name] = dict(us=round(us, 2), frac=round(nbytes / us / 1e6 / 8.0, 4), bitwise=bitwise[name])
+        if os.environ.get('KSHAPES_CACHE_STATE') == '1':
+            # store policies of the automatic shape under different cache states: back to back into one
+            # output, alternating between two outputs, single launches after a 512 MB read / write flush
+            flush = torch.empty((512 << 20) // 4, dtype=torch.int32, device='cuda')
+            sink = torch.empty((1,), dtype=torch.int64, device='cuda')
+            out2, ow2 = torch.empty_like(ref), torch.empty_like(ref_w)
+            for pol, pname in ((-1, 'sc1 (auto)'), (3, 'sc1 nt'), (1, 'nt'), (0, 'plain')):
+                assert lib.deepep_set_launch_config(0, -1, pol, 0) == 0
+                flip = [0]
+
+                def alt():
+                    flip[0] ^= 1
+                    run(y, ex_w, table, out2 if flip[0] else out, ow2 if flip[0] else ow)()
+                row = dict(same_output=round(timeit(run(y, ex_w, table, out, ow), s, iters=iters), 2),
+                           alternating_outputs=round(timeit(alt, s, iters=iters), 2))
+                for mode, pre in (('read_flush', lambda: torch.sum(flush, dim=0, dtype=torch.int64, out=sink)),
+                                  ('write_flush', lambda: flush.fill_(1))):
+                    ts = []
+                    for _ in range(15):
+                        pre()
+                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        e0.record(s)
+                        run(y, ex_w, table, out, ow)()
+                        e1.record(s)
+                        torch.cuda.synchronize()
+                        ts.append(e0.elapsed_time(e1) * 1e3)
+                    row[mode] = round(statistics.median(ts), 2)
+                res[f'cache state, {pname}'] = row
+            lib.deepep_set_launch_config(0, -1, -1, 0)
+            del flush, out2, ow2
         best = min((k for k in res if k.startswith('vpt')), key=lambda k: res[k]['us'])
         res['best'] = dict(variant=best, vs_auto=round(res[best]['us'] / res['auto']['us'], 4))
         lib.deepep_set_launch_config(0, -1, -1, 0)

@@ -161,13 +161,13 @@ __device__ __forceinline__ u32x4 acc_pack(const float* acc) {
 
 // Output stores: buffer_store_dwordx4 with a per-row descriptor (the hardware range check
 // drops the lanes past the row end).  The cache policy is a template parameter; measured on
-// MI355X (tools/probe.hip, 8192 x 7168 x top-8): sc1 (write-through, line dropped from L2)
+// MI355X (a round-1 gather probe, 8192 x 7168 x top-8): sc1 (write-through, line dropped from L2)
 // 164.6 us, plain 166.2 us, nt 171.8 us for the gather + store pattern; write-only 8.0 / 7.4 /
 // 5.9 TB/s.  sc1 is the default.
 constexpr int kAuxNT = 2, kAuxSC1 = 16;      // (sc0 = 1)
 // Stores into a peer's symmetric window (the xGMI transport) are system-scope write-through
 // (sc0 sc1): they must be visible to another GPU once the kernel has completed, whatever MTYPE the
-// importing process maps the window with.  Same speed as sc1 (tools/probe_ld.hip).
+// importing process maps the window with.  Same speed as sc1 (a round-1 load/store policy probe).
 constexpr int kAuxSys = 17;
 // Write-through streaming (sc1 nt): what the dispatch's blocked expanded copy stores with (dispatch.hip);
 // a launch-config option here (store_policy 3), measured against sc1 in tools/kbisect.py.
@@ -449,7 +449,7 @@ combine_rows_kernel(const Params p) {
 // stored, so each wave keeps its rows streaming and writes its output row front to back.  The
 // arithmetic per chunk is exactly combine_rows_kernel's (same init, order, rounding), so the two
 // kernels give identical bits; measured on config 2: 161.3 us vs 171.3 us on one box
-// (tools/probe_tok.py).
+// (DESIGN.md section 3).
 constexpr int kStreamWidth = 8;
 
 template <int kMode, bool kWeighted, int kVPT, int kStoreAux>
@@ -931,7 +931,7 @@ int launch_combine(int mode, int weighted, const Params& p_in, deepep_stream_t s
     sh.waves = p.units_per_block == 4 ? 4 : (p.units_per_block == 8 ? 8 : (mode == DEEPEP_MODE_LOCAL ? 4 : 8));
     // rows in flight per lane: 8 for the fused / epilogue reduces (8 rows per token at EP = 1), 4 for
     // phase A (about 1.5 local rows per received token at EP = 8: 64 VGPRs and 8 waves per SIMD beat
-    // deeper per-wave loads, tools/kphase.py 252-254 vs 256-260 us, tools/kphase_cu.py)
+    // deeper per-wave loads, tools/kphase.py 252-254 vs 256-260 us)
     // A unit never has more valid rows than its table is wide, so the rows in flight are capped at the
     // width rounded up to 2 / 4: registers for rows that never come only cost occupancy (top-2, config-2
     // shape otherwise: 33.7 vs 40.1 us; top-4: 93.5 vs 95.9 us; tools/kshapes.py, profiles/r04e_kshapes_*, r04f_kshapes_*).
@@ -980,7 +980,7 @@ int launch_combine(int mode, int weighted, const Params& p_in, deepep_stream_t s
     // 6: the item kernel on its full grid (what the default does on a CU-budget stream too)
     // On a CU-budget stream the item kernel keeps its full grid (the CU mask alone holds it to the
     // budget) with 4 rows in flight per lane: 64 VGPRs, 8 waves per SIMD, so a budgeted CU keeps more
-    // bytes in flight than with 8 rows at 5 waves (config 2, tools/kcu2.py, profiles/r02n_kcu2.jsonl:
+    // bytes in flight than with 8 rows at 5 waves (config 2, profiles/r02n_kcu2.jsonl:
     // 128 CUs 208 vs 235 us on a persistent grid, 32 CUs 603 vs 661 us; the whole chip is unchanged);
     // the streaming kernels and the forced persistent item kernel take a persistent grid sized to it.
     const int budget = budget_cus_of(s);

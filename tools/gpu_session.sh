@@ -39,11 +39,6 @@ for step in "$@"; do
         kwin)   run kwin 300 python tools/kwin.py ;;
         klayoutruns) export KLAYOUT_RUNS=1; run klayoutruns 400 python tools/klayout.py; unset KLAYOUT_RUNS ;;
         kflush) run kflush 300 python tools/kflush.py ;;
-        kplace) run kplace 300 python tools/kplace.py ;;
-        kplacetlb) export KPLACE_ITERS=4 KPLACE_WARM=1 KPLACE_ROUNDS=1
-                run kplacetlb 300 rocprofv3 --kernel-trace --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum GRBM_UTCL2_BUSY GRBM_GUI_ACTIVE -d $OUT/kplacetlb -o pmc --output-format csv -- python3 tools/kplace.py
-                run kplacetlb2 300 rocprofv3 --kernel-trace --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum GRBM_UTCL2_BUSY GRBM_GUI_ACTIVE -d $OUT/kplacetlb2 -o pmc --output-format csv -- python3 tools/kplace.py
-                unset KPLACE_ITERS KPLACE_WARM KPLACE_ROUNDS ;;
         kphase) run kphase 300 python tools/kphase.py ;;
         profphase) run profphase 300 rocprofv3 --kernel-trace --stats -d $OUT/profphase -o prof --output-format csv -- python3 tools/kphase_prof.py ;;
         kcu)    run kcu 300 python tools/kcu.py ;;
@@ -51,12 +46,7 @@ for step in "$@"; do
         koverlap) run koverlap 300 python tools/koverlap.py ;;
         kdispprof) export KDISPATCH_CPROFILE=1; run kdispprof 300 python tools/kdispatch.py; unset KDISPATCH_CPROFILE ;;
         profdisp) run profdisp 300 rocprofv3 --kernel-trace -d $OUT/profdisp -o prof --output-format csv -- python3 tools/kdispatch.py ;;
-        kcu2)   run kcu2 300 python tools/kcu2.py ;;
-        kphasecu) run kphasecu 300 python tools/kphase_cu.py ;;
         cumask) run cumask 120 python tools/probe_cumask.py ;;
-        cubw)   run cubw 300 python tools/probe_cubw.py ;;
-        cubwspread) export CUBW_SPREAD=1; run cubwspread 300 python tools/probe_cubw.py; unset CUBW_SPREAD ;;
-        probeld) run probeld 300 python tools/probe_ld.py ;;
         pmclist) run pmclist 120 rocprofv3 --list-avail ;;
         smi)    run smi 60 rocm-smi --showclocks --showpower --showtemp ;;
         bench4gloo) # the driver's plain command form: bench.py starts its own 4 ranks (sharing the one GPU over gloo)
@@ -104,15 +94,9 @@ for step in "$@"; do
                 run pmccal_ws 300 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE TCC_EA0_WRREQ_sum -d $OUT/pmccal_ws -o pmc --output-format csv -- python3 tools/pmc_phases.py
                 run pmccal_rq 300 timeout -s KILL 120 rocprofv3 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum -d $OUT/pmccal_rq -o pmc --output-format csv -- python3 tools/pmc_phases.py
                 run pmccal_fs 300 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmccal_fs -o pmc --output-format csv -- python3 tools/pmc_phases.py ;;
-        pmccopy) # counter calibration on the dispatch copy's pattern against torch copies of known bytes
-                run pmccopy_ws 300 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE TCC_EA0_WRREQ_sum -d $OUT/pmccopy_ws -o pmc --output-format csv -- python3 tools/pmc_copycal.py
-                run pmccopy_rq 300 timeout -s KILL 120 rocprofv3 --pmc TCC_EA0_WRREQ_64B_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_DRAM_sum TCC_EA0_RDREQ_DRAM_sum -d $OUT/pmccopy_rq -o pmc --output-format csv -- python3 tools/pmc_copycal.py
-                run pmccopy_fs 300 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmccopy_fs -o pmc --output-format csv -- python3 tools/pmc_copycal.py ;;
         pmcplain) for c in FETCH_SIZE WRITE_SIZE; do
                     run pmcp_$c 300 timeout -s KILL 120 rocprofv3 --pmc $c -d $OUT/pmcp_$c -o pmc --output-format csv -- python3 tools/pmc_run.py --plain
                 done ;;
-        probe)  run probe 600 python tools/probe.py ;;
-        probeburst) export PROBE_BURST=1; run probeburst 600 python tools/probe.py; unset PROBE_BURST ;;
         *) echo "unknown step $step" ;;
     esac
 done

@@ -56,6 +56,11 @@ for step in "$@"; do
         kshapes) run kshapes 400 python tools/kshapes.py ;;
         koutplace) run koutplace 300 python tools/koutplace.py ;;
         kphaseb) run kphaseb 300 python tools/kphase_b.py ;;
+        tlb)    # six separate processes: the fused kernel back to back under the UTCL1 translation counters (is a
+                # fast process one with fewer TLB misses?)
+                for i in 1 2 3 4 5 6; do
+                    run tlb$i 150 timeout -s KILL 120 rocprofv3 --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum GRBM_GUI_ACTIVE -d $OUT/tlb$i -o pmc --output-format csv -- python3 tools/pmc_run.py --b2b
+                done ;;
         pmcpolicy) # phase A's store policies at EP = 4 under memory-side and L2 counters (one pass per counter set)
                 i=0
                 for cs in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum"; do

@@ -49,6 +49,22 @@ def main():
     for i in range(6):
         outs[f'alloc{i}'] = torch.empty((T, H), dtype=torch.bfloat16, device='cuda')
     y2 = y.clone()
+    if os.environ.get('KOUT_INPUTS') == '1':
+        # input placement: the same rows cloned into fresh allocations, one output (round 1 saw up to 10 %)
+        clones = [y] + [y.clone() for _ in range(7)]
+        times = {i: [] for i in range(len(clones))}
+        out = outs['alloc0']
+        ow0 = torch.empty((T, K), dtype=torch.float32, device='cuda')
+        for _ in range(int(os.environ.get('KOUT_ROUNDS', 4))):
+            for i, yy in enumerate(clones):
+                times[i].append(timeit(lambda yy=yy: kern.combine_reduce(MODE_FUSED, yy, out, T, table=table,
+                                                                         row_weights=ex_w, wtable=table, wsrc=ex_w,
+                                                                         out_weights=ow0, stream=s), s, iters=30))
+        for i in times:
+            print(json.dumps(dict(input_clone=i, us=round(statistics.median(times[i]), 2),
+                                  frac=round(nbytes / statistics.median(times[i]) / 8e6, 4),
+                                  addr_mod_1G=clones[i].data_ptr() % (1 << 30))), flush=True)
+        del clones
     ow = torch.empty((T, K), dtype=torch.float32, device='cuda')
     variants = {}
     for name, out in outs.items():

@@ -1,6 +1,7 @@
 """Launch the fused combine kernel a few times on BASELINE config 2 (for rocprofv3 --pmc passes).
 
-usage: rocprofv3 --pmc FETCH_SIZE -d OUT -o pmc --output-format csv -- python3 tools/pmc_run.py [--plain]
+usage: rocprofv3 --pmc FETCH_SIZE -d OUT -o pmc --output-format csv -- python3 tools/pmc_run.py [--plain] [--b2b]
+--b2b: 20 launches back to back without the flush (the bench's loop), for per-process counter comparisons.
 """
 import os
 import sys
@@ -33,8 +34,10 @@ def main():
     out_w = torch.empty((T, K), dtype=torch.float32, device='cuda')
     # flush the 256 MiB Infinity Cache between launches, as the reference's bench does (testing.py:12-21)
     flush = torch.empty(512 * 1024 * 1024 // 4, dtype=torch.int32, device='cuda')
-    for _ in range(5):
-        flush.zero_()
+    b2b = '--b2b' in sys.argv
+    for _ in range(20 if b2b else 5):
+        if not b2b:
+            flush.zero_()
         buf.kernels.combine_reduce(MODE_FUSED, y, out, T, table=plan.local_table,
                                    row_weights=ex_w if weighted else None,
                                    wtable=plan.local_table, wsrc=ex_w, out_weights=out_w)

@@ -19,7 +19,7 @@ run() {   # run <name> <timeout> <cmd...>
 for step in "$@"; do
     case $step in
         tests)  run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 170 --timeout-method thread ;;
-        xgmistress) export DEEPEP_XGMI_STRESS=1; run xgmistress 300 python -u -m pytest tests/test_xgmi_gpu.py -k full_size -x -q --timeout 170 --timeout-method thread; unset DEEPEP_XGMI_STRESS ;;
+        xgmistress) run xgmistress 300 python -u -m pytest tests/test_xgmi_gpu.py -k full_size -x -q --timeout 170 --timeout-method thread ;;
         smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench)  run bench 600 python bench.py ;;
         benchc4) run bench_c4 600 python bench.py --fp8-dispatch --no-cpu-baseline --no-loopback ;;

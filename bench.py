@@ -218,6 +218,72 @@ def _xgmi_enabled() -> bool:
     return _XGMI['enabled']
 
 
+_T_START = time.perf_counter()
+# N > 1: the secondary legs (phase-A budget, xGMI, single reduction, dispatch, sync-free) start only while the
+# run is inside a soft time budget, checked at every leg boundary with the MAX over ranks (every rank skips
+# the same legs); and a watchdog ends the run at a hard deadline with the line built so far (the headline
+# `value` first), so that a leg that hangs on a node never costs the whole line.  The driver's run of
+# `python bench.py --gpus 8` must fit its time limit.
+SOFT_BUDGET_S = float(os.environ.get('DEEPEP_BENCH_SOFT_S', 300))
+HARD_DEADLINE_S = float(os.environ.get('DEEPEP_BENCH_HARD_S', 480))
+
+
+class _Line:
+    """Rank 0's result line, filled leg by leg; `emit()` prints it once (normally at the end, or from the
+    watchdog at the hard deadline with `incomplete` naming the leg that was running)."""
+
+    def __init__(self, rank: int):
+        self.rank, self.fields, self.leg, self.skipped = rank, None, 'setup', []
+        self._printed = False
+        self._lock = __import__('threading').Lock()
+
+    def emit(self, incomplete: str = None) -> None:
+        with self._lock:
+            if self._printed or self.rank != 0 or self.fields is None:
+                return
+            self._printed = True
+            line = dict(self.fields)
+            line['launch'] = dict(line.get('launch') or {}, wall_s=round(time.perf_counter() - _T_START, 1))
+            if self.skipped:
+                line['skipped_legs'] = list(self.skipped)
+            if incomplete:
+                line['incomplete'] = incomplete
+            print(json.dumps(line), flush=True)
+
+    def start_watchdog(self) -> None:
+        import threading
+
+        def fire():
+            self.emit(incomplete=f'hard deadline {HARD_DEADLINE_S:.0f} s hit during leg "{self.leg}"; the '
+                                 f'fields present were measured before it')
+            print(f'[bench] rank {self.rank}: hard deadline during leg {self.leg}, exiting', file=sys.stderr,
+                  flush=True)
+            os._exit(0)
+        t = threading.Timer(max(1.0, HARD_DEADLINE_S - (time.perf_counter() - _T_START)), fire)
+        t.daemon = True
+        t.start()
+
+
+def _within_budget(dev, world: int) -> bool:
+    """True while the slowest rank is inside the soft budget (a collective every rank reaches)."""
+    el = torch.tensor([time.perf_counter() - _T_START], dtype=torch.float64, device=dev if world > 1 else 'cpu')
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    return float(el.item()) < SOFT_BUDGET_S
+
+
+def _memory(dev, world: int) -> dict:
+    """Peak device memory (allocator) and host RSS of the worst rank."""
+    import resource
+    v = torch.tensor([torch.cuda.max_memory_allocated(dev) / 2 ** 30, torch.cuda.max_memory_reserved(dev) / 2 ** 30,
+                      resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2 ** 20], dtype=torch.float64,
+                     device=dev if world > 1 else 'cpu')
+    if world > 1:
+        dist.all_reduce(v, op=dist.ReduceOp.MAX)
+    return dict(device_max_allocated_gib=round(float(v[0]), 2), device_max_reserved_gib=round(float(v[1]), 2),
+                host_max_rss_gib=round(float(v[2]), 2), note='max over ranks')
+
+
 def _cpu_threads() -> int:
     """Host threads for the CPU baseline: the GPU box's CPU share per GPU (16; os.cpu_count() there
     reports the whole machine's CPUs, many times as many -- both are in the line)."""
@@ -710,33 +776,39 @@ def main():
     value = total_bytes * args.steps / elapsed / 1e9
     ms_per_step = elapsed * 1e3 / args.steps
 
-    # N > 1: the same loop with phase A held to 128 CUs (DEEPEP_PHASE_A_CUS) -- do RCCL's kernels and
-    # phase B of the earlier chunks gain more from the freed CUs than phase A loses?
-    rccl_budget = None
-    if world > 1 and buf._num_chunks(handle) > 1:
-        ref_out, _, _ = step()
-        buf.phase_a_cus = 128
-        same_b = bool(torch.equal(step()[0], ref_out))
-        del ref_out
-        for _ in range(args.warmup):
-            step()
-        torch.cuda.synchronize()
-        dist.barrier()
-        torch.cuda.synchronize()
-        t0b = time.perf_counter()
-        for _ in range(args.steps):
-            step()
-        torch.cuda.synchronize()
-        dist.barrier()
-        torch.cuda.synchronize()
-        el_b = torch.tensor([time.perf_counter() - t0b], dtype=torch.float64, device=dev)
-        dist.all_reduce(el_b, op=dist.ReduceOp.MAX)
-        same = torch.tensor([1 if same_b else 0], dtype=torch.int32, device=dev)
-        dist.all_reduce(same, op=dist.ReduceOp.MIN)
-        el_b = float(el_b.item())
-        rccl_budget = dict(phase_a_cus=128, value=round(total_bytes * args.steps / el_b / 1e9, 2),
-                           ms_per_step=round(el_b * 1e3 / args.steps, 4), bitwise_equal=bool(same.item()))
-        buf.phase_a_cus = 0
+    line = _Line(rank)
+    res = dict(roofline=None, cpu_baseline=None, cpu_torch=None, loopback=None, phases=None, su_bandwidth=None,
+               rccl=None, xgmi=None, single_reduction=None, fastest_leg=None, dispatch=None)
+
+    def publish():
+        line.fields = {
+            'metric': 'combine GB/s (device-resident BF16 top-k weighted reduce) at 1/2/4/8 MI355X',
+            'value': round(value, 2), 'unit': 'GB/s', 'n_gpus': world, 'steps': args.steps,
+            'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 4), 'higher_is_better': True,
+            'scaling': 'weak', 'vs_baseline': None, 'dtype': 'bf16', 'data': 'synthetic',
+            'config': {'workload': f'EP={world} combine, {T} tokens/rank x hidden {H} x top-{K}, '
+                                   f'{E} experts, {"skewed x%g" % args.skew if args.skew != 1.0 else "uniform"} routing, '
+                                   f'{"FP8 dispatch, " if args.fp8_dispatch else ""}expanded layout, '
+                                   f'{"gating-weighted" if weighted else "plain (reference semantics)"}',
+                       'tokens_per_rank': T, 'hidden': H, 'topk': K, 'experts': E, 'accumulate': 'fp32',
+                       'parallelism': f'ep{world}', 'transport': buf.transport if world > 1 else None},
+            **res, 'xgmi_preflight': _XGMI['preflight'],
+            'launch': {'world_size_seen': world, 'launcher': os.environ.get('DEEPEP_BENCH_LAUNCHER', 'external')
+                       if world > 1 else 'single process', 'backend': dist.get_backend(),
+                       'devices_visible': torch.cuda.device_count(), 'soft_budget_s': SOFT_BUDGET_S,
+                       'hard_deadline_s': HARD_DEADLINE_S},
+        }
+    publish()
+    if world > 1:
+        line.start_watchdog()
+
+    def leg(name: str, secondary: bool = True) -> bool:
+        """Enter leg `name`; a secondary leg runs only inside the soft budget (every rank agrees)."""
+        line.leg = name
+        if secondary and world > 1 and not _within_budget(dev, world):
+            line.skipped.append(f'{name} (soft budget {SOFT_BUDGET_S:.0f} s spent)')
+            return False
+        return True
 
     # Dominant kernel, timed alone on the comm stream (launches back to back, same arguments)
     roofline = None
@@ -858,10 +930,7 @@ def main():
         roofline = dict(bound='hbm', achieved=round(achieved, 1), peak=HBM_PEAK_GBPS, unit='GB/s',
                         frac=round(achieved / HBM_PEAK_GBPS, 4), traffic=traffic, traffic_build_id=traffic_build,
                         traffic_note=traffic_note, build_id=build_id,
-                        kernel=('combine_rows_kernel<FUSED>', 'combine_stream_kernel<FUSED, 2 vectors/lane>',
-                                'combine_stream_kernel<FUSED, 1 vector/lane>',
-                                'combine_stream_kernel<FUSED, persistent grid>',
-                                'combine_rows_kernel<FUSED, XCD-contiguous>')[kern.lib.deepep_last_kernel_choice()],
+                        kernel='combine_rows_kernel<FUSED>',
                         kernel_us=round(kern_us, 2),
                         kernel_us_flushed_median=None if kern_us_flushed is None else round(kern_us_flushed, 2),
                         kernel_us_read_flushed_median=(None if kern_us_read_flushed is None
@@ -869,9 +938,11 @@ def main():
                         bytes_per_launch=bytes_rank, in_region_us_per_step=round(comm_ms * 1e3, 2),
                         same_run_d2d_copy_gbps=round(copy_gbps, 1), same_run_token_major_rows=token_major,
                         single_reduction_phase_b=single_b)
+        res['roofline'] = roofline
+        publish()
 
     phases = su_line = None
-    if world > 1:
+    if world > 1 and leg('phases', secondary=False):
         n_ph = max(5, args.steps // 2)
 
         def phase_events(unpipelined: bool):
@@ -949,26 +1020,66 @@ def main():
                       reduce_only_gbps=round(total_bytes / (float(vals[0]) * 1e-3) / 1e9, 1),
                       exchange_gbps_per_rank=round(float(xb.item()) / world / (float(vals[1]) * 1e-3) / 1e9, 1),
                       pipeline_chunks=buf._num_chunks(handle), transport=buf.transport,
+                      local_bypass=buf.local_bypass,
                       note='phase_*_ms / exchange_ms: the step unpipelined (1 chunk); pipelined_phase_*_ms: the sum of the '
                            'per-chunk launches inside the pipelined step (`value`); max over ranks; reduce_only = algorithmic bytes of all ranks / (phase A + phase B); '
-                           'exchange = off-rank partial rows + weights / exchange time, per rank')
+                           'exchange = off-rank partial rows + weights / exchange time, per rank (local_bypass: the '
+                           'own-rank partials are written in place, the all-to-all has a zero diagonal)')
+        res.update(roofline=roofline, phases=phases, su_bandwidth=su_line)
+        publish()
+
+    # N > 1: the same loop with phase A held to 128 CUs (DEEPEP_PHASE_A_CUS) -- do RCCL's kernels and
+    # phase B of the earlier chunks gain more from the freed CUs than phase A loses?
+    rccl_budget = None
+    if world > 1 and buf._num_chunks(handle) > 1 and leg('rccl_phase_a_budget'):
+        ref_out, _, _ = step()
+        buf.phase_a_cus = 128
+        same_b = bool(torch.equal(step()[0], ref_out))
+        del ref_out
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0b = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        el_b = torch.tensor([time.perf_counter() - t0b], dtype=torch.float64, device=dev)
+        dist.all_reduce(el_b, op=dist.ReduceOp.MAX)
+        same = torch.tensor([1 if same_b else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(same, op=dist.ReduceOp.MIN)
+        el_b = float(el_b.item())
+        rccl_budget = dict(phase_a_cus=128, value=round(total_bytes * args.steps / el_b / 1e9, 2),
+                           ms_per_step=round(el_b * 1e3 / args.steps, 4), bitwise_equal=bool(same.item()))
+        buf.phase_a_cus = 0
+    if world > 1:
+        res['rccl'] = dict(value=round(value, 2), ms_per_step=round(ms_per_step, 4), phase_a_budget=rccl_budget)
+        publish()
 
     xgmi = None
     if world > 1 and not _xgmi_enabled() and _XGMI['preflight'] is not None:
         xgmi = dict(skipped='xgmi_preflight failed on at least one rank (see xgmi_preflight)')
-    if world > 1 and _xgmi_enabled():
+    if world > 1 and _xgmi_enabled() and leg('xgmi'):
         xgmi = _bench_xgmi(buf, y, handle, ex_w, weighted, total_bytes, args.steps, args.warmup, dev)
+        res['xgmi'] = xgmi
+        publish()
     single = None
-    if world > 1 and os.environ.get('DEEPEP_BENCH_SINGLE', '1') != '0':
+    if world > 1 and os.environ.get('DEEPEP_BENCH_SINGLE', '1') != '0' and leg('single_reduction'):
         ref_multi, _, _ = buf.combine(y, handle, topk_weights=ex_w, apply_topk_weights=weighted)
         single = _bench_single(y, handle, ex_w, weighted, total_bytes, args.steps, args.warmup, dev, ref_multi)
         del ref_multi
+        res['single_reduction'] = single
+        publish()
 
     # Handle producer: dispatch of the same batch, expanded layout.  Includes its
     # host syncs (received-token counts), as the reference's dispatch with do_cpu_sync=True.
     torch.cuda.synchronize()
     dist.barrier()
     n_disp = 50
+    run_dispatch = leg('dispatch')
     x_disp = torch.randn((T, H), device=dev).to(torch.bfloat16)
     if args.fp8_dispatch:
         from workloads import per_token_cast_to_fp8
@@ -989,18 +1100,24 @@ def main():
         torch.cuda.synchronize()
         return t_d, (time.perf_counter() - t_c) / n_disp
 
-    t_d, t_c = time_dispatch(buf)
-    elem = 1 if args.fp8_dispatch else 2
-    disp_bytes = T * H * elem + handle.num_expanded_tokens * H * elem     # read x once, write every expanded row
-    dispatch = dict(ms=round(t_d * 1e3, 3), gbps=round(disp_bytes / t_d / 1e9, 1),
-                    cached_ms=round(t_c * 1e3, 3), cached_gbps=round(disp_bytes / t_c / 1e9, 1),
-                    transport=buf.transport if world > 1 else 'local',
-                    note='ElasticBuffer.dispatch(do_expand=True) wall time incl. host count syncs; cached = '
-                         'dispatch(handle=...) (no sync); bytes = x read once + expanded rows written')
-    if world > 1 and _xgmi_enabled():
-        dispatch['xgmi'] = _bench_xgmi_dispatch(buf, x_disp, topk_idx, topk_w, E, disp_bytes, time_dispatch, dev)
-    if world > 1:
-        dispatch['sync_free'] = _bench_sync_free(buf, x_disp, topk_idx, topk_w, E, weighted, dev)
+    dispatch = None
+    if run_dispatch:
+        t_d, t_c = time_dispatch(buf)
+        elem = 1 if args.fp8_dispatch else 2
+        disp_bytes = T * H * elem + handle.num_expanded_tokens * H * elem     # read x once, write every expanded row
+        dispatch = dict(ms=round(t_d * 1e3, 3), gbps=round(disp_bytes / t_d / 1e9, 1),
+                        cached_ms=round(t_c * 1e3, 3), cached_gbps=round(disp_bytes / t_c / 1e9, 1),
+                        transport=buf.transport if world > 1 else 'local',
+                        note='ElasticBuffer.dispatch(do_expand=True) wall time incl. host count syncs; cached = '
+                             'dispatch(handle=...) (no sync); bytes = x read once + expanded rows written')
+        res['dispatch'] = dispatch
+        publish()
+        if world > 1 and _xgmi_enabled() and leg('dispatch_xgmi'):
+            dispatch['xgmi'] = _bench_xgmi_dispatch(buf, x_disp, topk_idx, topk_w, E, disp_bytes, time_dispatch, dev)
+            publish()
+        if world > 1 and os.environ.get('DEEPEP_BENCH_SYNC_FREE', '1') != '0' and leg('dispatch_sync_free'):
+            dispatch['sync_free'] = _bench_sync_free(buf, x_disp, topk_idx, topk_w, E, weighted, dev)
+            publish()
     del x_disp
 
     loopback = None
@@ -1042,10 +1159,8 @@ def main():
     # single reduction) are complete implementations of the same combine timed with the same protocol on
     # the same batch; they stay beside it in the line, and `fastest_leg` names the fastest one whose
     # output matched the default bit for bit (information, never the headline).
-    transport = buf.transport if world > 1 else None
-    rccl = fastest = None
+    line.leg = 'summary'
     if world > 1:
-        rccl = dict(value=round(value, 2), ms_per_step=round(ms_per_step, 4), phase_a_budget=rccl_budget)
         legs = [('rccl', value)]
         if rccl_budget is not None and rccl_budget['bitwise_equal']:
             legs.append((f'rccl, DEEPEP_PHASE_A_CUS={rccl_budget["phase_a_cus"]}', rccl_budget['value']))
@@ -1055,35 +1170,18 @@ def main():
             if xb_ and xb_['bitwise_equal_to_rccl'] and not xb_['barrier_timeout']:
                 legs.append((f'xgmi, DEEPEP_PHASE_A_CUS={xb_["phase_a_cus"]}', xb_['value']))
         best = max(legs, key=lambda kv: kv[1])
-        fastest = dict(leg=best[0], value=round(best[1], 2), vs_value=round(best[1] / value, 3))
+        res['fastest_leg'] = dict(leg=best[0], value=round(best[1], 2), vs_value=round(best[1] / value, 3))
 
-    cpu_baseline = cpu_torch = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line.leg = 'cpu_baseline'
         plan = handle._combine_plans[('multi', 1)]
-        cpu_baseline = _cpu_baseline(y, plan.local_table, ex_w, weighted, args.cpu_seconds)
-        cpu_torch = _cpu_torch(T, H, K, args.cpu_seconds)
-
-    if rank == 0:
-        line = {
-            'metric': 'combine GB/s (device-resident BF16 top-k weighted reduce) at 1/2/4/8 MI355X',
-            'value': round(value, 2), 'unit': 'GB/s', 'n_gpus': world, 'steps': args.steps,
-            'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 4), 'higher_is_better': True,
-            'scaling': 'weak', 'vs_baseline': None, 'dtype': 'bf16', 'data': 'synthetic',
-            'config': {'workload': f'EP={world} combine, {T} tokens/rank x hidden {H} x top-{K}, '
-                                   f'{E} experts, {"skewed x%g" % args.skew if args.skew != 1.0 else "uniform"} routing, '
-                                   f'{"FP8 dispatch, " if args.fp8_dispatch else ""}expanded layout, '
-                                   f'{"gating-weighted" if weighted else "plain (reference semantics)"}',
-                       'tokens_per_rank': T, 'hidden': H, 'topk': K, 'experts': E, 'accumulate': 'fp32',
-                       'parallelism': f'ep{world}', 'transport': transport},
-            'roofline': roofline, 'cpu_baseline': cpu_baseline, 'cpu_torch': cpu_torch, 'loopback': loopback,
-            'phases': phases, 'su_bandwidth': su_line, 'rccl': rccl, 'xgmi': xgmi, 'single_reduction': single,
-            'fastest_leg': fastest,
-            'dispatch': dispatch, 'xgmi_preflight': _XGMI['preflight'],
-            'launch': {'world_size_seen': world, 'launcher': os.environ.get('DEEPEP_BENCH_LAUNCHER', 'external')
-                       if world > 1 else 'single process', 'backend': dist.get_backend(),
-                       'devices_visible': torch.cuda.device_count()},
-        }
-        print(json.dumps(line), flush=True)
+        res['cpu_baseline'] = _cpu_baseline(y, plan.local_table, ex_w, weighted, args.cpu_seconds)
+        res['cpu_torch'] = _cpu_torch(T, H, K, args.cpu_seconds)
+    res['loopback'] = loopback
+    memory = _memory(dev, world)
+    publish()
+    line.fields['launch']['memory'] = memory
+    line.emit()
     dist.barrier()
     dist.destroy_process_group()
 

@@ -38,7 +38,7 @@ def binary_build_id(path: str) -> Optional[str]:
         data = f.read()
     i = data.find(b'DEEPEP_BUILD_ID=')
     return data[i + 16:i + 32].decode(errors='replace') if i >= 0 else None
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 MODE_LOCAL, MODE_EPILOGUE, MODE_FUSED = 0, 1, 2
 
@@ -64,7 +64,7 @@ def describe_error_record(rec) -> str:
 # deepep_plan_* (include/deepep_amd.h)
 PLAN_BLOCK_TOKENS = 64
 DISPATCH_BLOCK_ROWS = 128          # DEEPEP_DISPATCH_BLOCK_ROWS: receive-side block of the dispatch
-PLAN_EXPANDED, PLAN_SINGLE, PLAN_INTERLEAVE, PLAN_RANK_LAYOUT, PLAN_WINDOW = 1, 2, 4, 8, 16
+PLAN_EXPANDED, PLAN_SINGLE, PLAN_INTERLEAVE, PLAN_RANK_LAYOUT, PLAN_WINDOW, PLAN_LOCAL_BYPASS = 1, 2, 4, 8, 16, 32
 
 _lib = None
 _lock = threading.Lock()
@@ -91,9 +91,7 @@ SIGNATURES = {
                                    _I, _P,
                                    _P]),
     'deepep_build_local_plan': (_I, [_P, _I, _I, _I, _I, _P, _I, _I, _P, _P, _P]),
-    'deepep_set_launch_config': (_I, [_I, _I, _I, _I]),
-    'deepep_set_kernel_choice': (_I, [_I]),
-    'deepep_last_kernel_choice': (_I, []),
+    'deepep_set_launch_config': (_I, [_I, _I]),
     'deepep_combine_buffer_size': (_I64, [_I, _I, _I, _I, _I]),
     'deepep_dispatch_route': (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P]),
     'deepep_dispatch_notify': (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _I64, _P]),
@@ -111,7 +109,7 @@ SIGNATURES = {
     'deepep_route_block_counts': (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P]),
     'deepep_plan_expert': (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _I, _I, _I, _P, _P, _P, _I64, _I64, _P, _P, _I,
                                 _P]),
-    'deepep_plan_source': (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I64, _I64, _P, _I, _P, _I, _P]),
+    'deepep_plan_source': (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I64, _I64, _P, _I, _P, _I, _P]),
     'deepep_sym_alloc': (_I, [_I64, ctypes.POINTER(ctypes.c_void_p)]),
     'deepep_sym_free': (_I, [_P]),
     'deepep_sym_export': (_I, [_P, _P]),

@@ -150,6 +150,9 @@ class ElasticBuffer(ExchangeMixin):
         # (phase A stores straight into the owners' symmetric windows, deepep_amd/symmetric.py)
         self.transport = os.environ.get('DEEPEP_TRANSPORT', 'rccl')
         _assert(self.transport in ('rccl', 'xgmi'), 'DEEPEP_TRANSPORT must be rccl or xgmi')
+        # RCCL combine: this rank's own partials are written in place instead of travelling through the
+        # all-to-all's diagonal (DEEPEP_LOCAL_BYPASS=0 turns it off, to measure what it saves)
+        self.local_bypass = os.environ.get('DEEPEP_LOCAL_BYPASS', '1') != '0'
         # xGMI combine: CUs for phase A while phase B of earlier chunks runs (0 = the whole chip)
         self.phase_a_cus = int(os.environ.get('DEEPEP_PHASE_A_CUS', 0))
         # CU footprint of a combine called with num_sms=0: 'chip' (default) takes the whole GPU -- the
@@ -789,7 +792,7 @@ class ElasticBuffer(ExchangeMixin):
         if R == 1:
             key = ('single' if single_reduction else 'multi', 1)
         elif window is None:
-            key = ('single' if single_reduction else 'multi', R, num_chunks, hidden)
+            key = ('single' if single_reduction else 'multi', R, num_chunks, hidden, self.local_bypass)
         else:
             for k in [k for k in handle._combine_plans if k[0] == 'xgmi' and k[-1] in self._old_sym_gens]:
                 del handle._combine_plans[k]          # plans that address an earlier (freed) window
@@ -797,6 +800,7 @@ class ElasticBuffer(ExchangeMixin):
         plan = handle._combine_plans.get(key)
         stream = torch.cuda.current_stream() if self.use_cuda else None
         if plan is not None:
+            plan.poll()                               # a plan entry its kernels rejected: raise
             if self.use_cuda and not self._capturing and plan.ready is not None and plan.ready[0] != stream:
                 # built on another stream: order this use after it (once per call, cheap)
                 stream.wait_event(plan.ready[1])
@@ -815,12 +819,14 @@ class ElasticBuffer(ExchangeMixin):
         else:
             _assert(handle._counts is not None, 'the EP > 1 combine needs a handle made by this build\'s dispatch')
             plan = build_ep_plan(self.kernels, handle, num_ranks=R, rank=self.rank_idx, single=single_reduction,
-                                 num_chunks=num_chunks, hidden=hidden, window=window, stream=stream)
+                                 num_chunks=num_chunks, hidden=hidden, window=window, stream=stream,
+                                 local_bypass=self.local_bypass)
         if not self._capturing:
             if self.use_cuda:
                 ev = torch.cuda.Event()
                 ev.record(stream)
                 plan.ready = (stream, ev)
+                plan.publish(stream)
             handle._combine_plans[key] = plan
         return plan
 

@@ -8,16 +8,16 @@
 //   weighted variant     legacy low-latency combine        csrc/kernels/legacy/internode_ll.cu:1072-1135
 //
 // How (MI355X-first, not a translation of the TMA/warp design):
-//   * the work is split into items = (output row, column chunk of 64 lanes x 2 x 16 B); one wave64
-//     owns one item and a 512-thread workgroup owns 8 consecutive items (7 items per token at
-//     hidden 7168), so the grid is ~7K workgroups with no tail imbalance;
+//   * the work is split into items = (output row, column chunk of 64 lanes x vpt x 16 B); one wave64
+//     owns one item and a workgroup of 4 or 8 waves owns that many consecutive items, so the grid is
+//     tens of thousands of workgroups with no tail imbalance;
 //   * the item's row of the slot table (and, weighted, the gating weights) is staged once per
 //     workgroup in LDS, one entry per lane; the valid slots are visited in ascending order through
 //     the wave's ballot mask (= the reference's compacted slot order);
-//   * each lane keeps 8 rows x 2 x 16 B of non-temporal global_load_dwordx4 in flight (every
+//   * each lane keeps 2-8 rows x vpt x 16 B of non-temporal global_load_dwordx4 in flight (every
 //     expanded row is read exactly once), accumulates bf16 -> fp32 in registers in the reference's
-//     order, rounds once with v_cvt_pk_bf16_f32 (RNE) and writes 2 x 16 B with a write-through
-//     (sc1) buffer store.
+//     order, rounds once with v_cvt_pk_bf16_f32 (RNE) and writes vpt x 16 B with a write-through
+//     buffer store.
 //   No MFMA: this is an HBM-bound gather + elementwise add (roofline and measurements in DESIGN.md).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -25,6 +25,7 @@
 #include <stdarg.h>
 
 #include <algorithm>
+#include <atomic>
 #include <map>
 #include <mutex>
 
@@ -66,14 +67,6 @@ __device__ __forceinline__ u32x4 load16(const u32x4* p) {
         return *p;
 }
 
-template <bool kNT>
-__device__ __forceinline__ void store16(u32x4* p, const u32x4& v) {
-    if constexpr (kNT)
-        __builtin_nontemporal_store(v, p);
-    else
-        *p = v;
-}
-
 struct Params {
     const uint16_t* src;
     int64_t num_src_rows;
@@ -99,8 +92,6 @@ struct Params {
     int32_t* error_flag;
     const uint64_t* out_rows;    // scatter (phase A over xGMI): byte address of unit u's output row, or NULL
     int64_t weights_offset;      // scatter: byte offset of the weights inside the output row
-    int xcd_blocks;              // item kernel: 1 = XCD-contiguous workgroup order (see xcd_block)
-    int cap_cus;                 // > 0: persistent grid, at most the workgroups this many CUs hold at once
     const uint64_t* win_bases;   // scatter: the windows every out_rows[u] must lie in (lane l < win_count: window l)
     int win_count;
     uint64_t win_limit;          // scatter: largest offset of a row start inside a window (extent - row bytes)
@@ -123,15 +114,6 @@ __device__ __forceinline__ uint64_t checked_row(const Params& p, int64_t u, int 
         deepep::record_fault(p.error_flag, DEEPEP_FLAG_BAD_ADDRESS, DEEPEP_FAULT_SCATTER_ROW, u, -1, a,
                              static_cast<int64_t>(p.win_limit >> 4));
     return 0ull;
-}
-
-// Workgroups are dealt round-robin to the 8 XCDs (workgroup b runs on XCD b % 8).  With
-// xcd_blocks, workgroup b takes block xcd_block(b) instead, so each XCD works through one
-// contiguous eighth of the items (its L2 and its share of the memory traffic stay on neighbouring
-// tokens) -- a bijection on [0, n) for any n.
-__device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t n) {
-    const int64_t per = n / 8, rem = n % 8, xcd = b % 8, idx = b / 8;
-    return xcd * per + (xcd < rem ? xcd : rem) + idx;
 }
 
 // acc[8*v + e] += element e of the 16-byte vector (8 bf16)
@@ -159,26 +141,17 @@ __device__ __forceinline__ u32x4 acc_pack(const float* acc) {
     return r;
 }
 
-// Output stores: buffer_store_dwordx4 with a per-row descriptor (the hardware range check
-// drops the lanes past the row end).  The cache policy is a template parameter; measured on
-// MI355X (a round-1 gather probe, 8192 x 7168 x top-8): sc1 (write-through, line dropped from L2)
-// 164.6 us, plain 166.2 us, nt 171.8 us for the gather + store pattern; write-only 8.0 / 7.4 /
-// 5.9 TB/s.  sc1 is the default.
-constexpr int kAuxNT = 2, kAuxSC1 = 16;      // (sc0 = 1)
-// Stores into a peer's symmetric window (the xGMI transport) are system-scope write-through
-// (sc0 sc1): they must be visible to another GPU once the kernel has completed, whatever MTYPE the
-// importing process maps the window with.  Same speed as sc1 (a round-1 load/store policy probe).
-constexpr int kAuxSys = 17;
-// Write-through streaming (sc1 nt): what the dispatch's blocked expanded copy stores with (dispatch.hip);
-// a launch-config option here (store_policy 3), measured against sc1 in tools/kbisect.py.
-constexpr int kAuxSC1NT = 18;
-// Per unit (launch-config store policy 4): sc1 when the unit reduces >= 3 rows, sc1 nt otherwise.  Phase A at
-// EP = 2 / 4 / 8 (tools/kphase_a.py, profiles/r04g_kphasea_*, r04i_kphasea_cache_state.jsonl): back to back
-// into the same send rows it beats sc1 nt everywhere by 3.5-12 %, but how much depends on what the caches
-// hold: after a 512 MB write flush (dirty lines, as a GEMM that has just written the expert rows leaves them)
-// it is 7 % slower at EP = 2 and 4 and equal at EP = 8; sc1 nt is within 2 % in every state.  So phase A keeps
-// sc1 nt by default.  Never passed to the store builtin itself.
-constexpr int kAuxPerUnit = 1003;     // 1000 + the row threshold
+// Output stores: buffer_store_dwordx4 with a per-row descriptor (the hardware range check drops the
+// lanes past the row end).  Three cache policies ship, one per kind of output:
+//   sc1     (write-through, line not kept in L2): the fused and epilogue reduces, whose output is
+//           written in token order -- best or tied in every cache state measured;
+//   sc1 nt  (write-through streaming): phase A's send rows, written once and read back only by the
+//           exchange -- within 2 % of the best policy in every cache state at EP = 2 / 4 / 8;
+//   sc0 sc1 (system scope): phase A into a peer's symmetric window over xGMI, visible to the owning
+//           GPU once the kernel has completed, whatever MTYPE the importing process maps it with.
+// (plain, nt and a per-unit sc1 / sc1 nt mix lost or were cache-state dependent; their measurements
+// are in CHANGELOG.md, the code in git history.)
+constexpr int kAuxSC1 = 16, kAuxSys = 17, kAuxSC1NT = 18;
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void* row, int bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(row), 0, bytes, 0x00020000);
@@ -345,31 +318,16 @@ __device__ __forceinline__ void combine_item(const Params& p, int64_t it, int nc
         for (int v = 0; v < kVPT; ++v) result[v] = (u32x4){0x7fc07fc0u, 0x7fc07fc0u, 0x7fc07fc0u, 0x7fc07fc0u};
     }
     const __amdgpu_buffer_rsrc_t orow = row_rsrc(out_row, p.hidden * 2);
-    if constexpr (kStoreAux > 1000) {
-        if (n >= kStoreAux - 1000) {
 #pragma unroll
-            for (int v = 0; v < kVPT; ++v)
-                __builtin_amdgcn_raw_buffer_store_b128(result[v], orow, vidx[v] * 16, 0, kAuxSC1);
-        } else {
-#pragma unroll
-            for (int v = 0; v < kVPT; ++v)
-                __builtin_amdgcn_raw_buffer_store_b128(result[v], orow, vidx[v] * 16, 0, kAuxSC1NT);
-        }
-    } else {
-#pragma unroll
-        for (int v = 0; v < kVPT; ++v)
-            __builtin_amdgcn_raw_buffer_store_b128(result[v], orow, vidx[v] * 16, 0, kStoreAux);
-    }
+    for (int v = 0; v < kVPT; ++v)
+        __builtin_amdgcn_raw_buffer_store_b128(result[v], orow, vidx[v] * 16, 0, kStoreAux);
     if (wlane) store_weight(p, u, out_row, lane, wv);
 }
 
-// A workgroup of kWaves waves takes kWaves consecutive items (a virtual block); the unit's slot table
-// row (and its gating weights) is staged once per workgroup in LDS (kLDS) or per wave in registers.
-// The grid is one workgroup per virtual block, or -- on a CU-budget stream, or when forced -- capped
-// at the workgroups the (budgeted) CUs hold at once, each walking virtual blocks grid-stride
-// (p.persistent): the waves then stay resident instead of a launch per 2 KiB item.
-template <int kMode, bool kWeighted, int kVPT, bool kFull, int kStoreAux, bool kLDS, int kWaves = 4, int kGroup = 8,
-          bool kPersistent = false>
+// A workgroup of kWaves waves takes kWaves consecutive items; the slot-table rows of the units those
+// items belong to (and their gating weights) are staged once per workgroup in LDS, one entry per lane.
+// One workgroup per kWaves items: 28,672 workgroups at config 2, no tail imbalance.
+template <int kMode, bool kWeighted, int kVPT, bool kFull, int kStoreAux, int kWaves, int kGroup>
 __global__ void __launch_bounds__(64 * kWaves)
 combine_rows_kernel(const Params p) {
     constexpr int kChunkVecs = 64 * kVPT;
@@ -379,210 +337,38 @@ combine_rows_kernel(const Params p) {
     const int nvec = p.hidden >> 3;                          // 16-byte vectors per row
     const int nchunks = (nvec + kChunkVecs - 1) / kChunkVecs;
     const int64_t items = static_cast<int64_t>(p.num_units) * nchunks;
-    const int64_t nblocks = (items + kWaves - 1) / kWaves;
     const int width = p.table == nullptr ? 1 : p.table_width;
-
-    auto load_slot = [&](int64_t u, int j) -> int32_t {
+    const int64_t it0 = static_cast<int64_t>(blockIdx.x) * kWaves;
+    const int64_t it = it0 + wave;
+    const int64_t u_first = it0 / nchunks;
+    const int nu = static_cast<int>(min(it0 + kWaves - 1, items - 1) / nchunks - u_first) + 1;
+    if (tid < nu * width) {                                  // nu * width <= kWaves * 32 threads
+        const int ul = tid / width, j = tid - ul * width;
+        const int64_t u = u_first + ul;
         int32_t s = p.table == nullptr ? static_cast<int32_t>(u) : p.table[u * p.table_stride + j];
         if (s >= p.num_src_rows) {                           // never dereference a bad slot
-            if (p.error_flag != nullptr) atomicOr(p.error_flag, 1);
+            if (p.error_flag != nullptr) atomicOr(p.error_flag, DEEPEP_FLAG_BAD_SLOT);
             s = -1;
         }
-        return s;
-    };
-
-    auto block = [&](int64_t vb) {
-        const int64_t blk = p.xcd_blocks ? xcd_block(vb, nblocks) : vb;
-        const int64_t it0 = blk * kWaves;
-        const int64_t it = it0 + wave;
-        int32_t my_slot = -1;
-        float my_w = 0.0f;
-        if constexpr (kLDS) {
-            if (vb != blockIdx.x) __syncthreads();          // the previous block's waves read s_slot
-            const int64_t u_first = it0 / nchunks;
-            const int nu = static_cast<int>(min(it0 + kWaves - 1, items - 1) / nchunks - u_first) + 1;
-            if (tid < nu * width) {                         // nu * width <= kWaves * 32 threads
-                const int ul = tid / width, j = tid - ul * width;
-                const int32_t s = load_slot(u_first + ul, j);
-                s_slot[ul][j] = s;
-                if constexpr (kWeighted) s_w[ul][j] = s >= 0 ? p.row_weights[s] : 0.0f;
-            }
-            __syncthreads();
-            if (it < items && lane < width) {
-                const int ul = static_cast<int>(it / nchunks - u_first);
-                my_slot = s_slot[ul][lane];
-                if constexpr (kWeighted) my_w = s_w[ul][lane];
-            }
-        } else {
-            if (it < items && lane < width) {
-                my_slot = load_slot(it / nchunks, lane);
-                if constexpr (kWeighted) my_w = my_slot >= 0 ? p.row_weights[my_slot] : 0.0f;
-            }
-        }
-        if (it < items)
-            combine_item<kMode, kWeighted, kVPT, kFull, kStoreAux, kGroup>(p, it, nchunks, nvec, lane, my_slot, my_w);
-    };
-    if constexpr (kPersistent && !kLDS) {
-        // per-wave items, grid-stride, with the NEXT item's slots loading while this item's rows are
-        // gathered: a wave never waits on a slot-table load between two rounds of row loads
-        const int64_t stride = static_cast<int64_t>(gridDim.x) * kWaves;
-        int64_t it = static_cast<int64_t>(blockIdx.x) * kWaves + wave;
-        int32_t next = (it < items && lane < width) ? load_slot(it / nchunks, lane) : -1;
-        for (; it < items; it += stride) {
-            const int32_t my_slot = next;
-            float my_w = 0.0f;
-            if constexpr (kWeighted) my_w = my_slot >= 0 ? p.row_weights[my_slot] : 0.0f;
-            next = (it + stride < items && lane < width) ? load_slot((it + stride) / nchunks, lane) : -1;
-            combine_item<kMode, kWeighted, kVPT, kFull, kStoreAux, kGroup>(p, it, nchunks, nvec, lane, my_slot, my_w);
-        }
-    } else if constexpr (kPersistent) {
-        for (int64_t vb = blockIdx.x; vb < nblocks; vb += gridDim.x) block(vb);
-    } else {
-        block(blockIdx.x);                          // one virtual block per workgroup
+        s_slot[ul][j] = s;
+        if constexpr (kWeighted) s_w[ul][j] = s >= 0 ? p.row_weights[s] : 0.0f;
     }
-}
-
-// Streaming variant: one wave owns a whole unit (all of its column chunks), for slot tables of at
-// most kStreamWidth entries and hidden sizes that are a whole number of chunks.  The unit's slots,
-// weights and weight pass-through are handled once; then the chunks are walked in order with the
-// loads of chunk c + 1 (every valid row, kVPT x 16 B per lane) issued before chunk c is summed and
-// stored, so each wave keeps its rows streaming and writes its output row front to back.  The
-// arithmetic per chunk is exactly combine_rows_kernel's (same init, order, rounding), so the two
-// kernels give identical bits; measured on config 2: 161.3 us vs 171.3 us on one box
-// (DESIGN.md section 3).
-constexpr int kStreamWidth = 8;
-
-template <int kMode, bool kWeighted, int kVPT, int kStoreAux>
-__global__ void __launch_bounds__(256)
-combine_stream_kernel(const Params p) {
-    constexpr int kChunkVecs = 64 * kVPT;
-    const int lane = static_cast<int>(threadIdx.x) & 63;
-    const int nchunks = (p.hidden >> 3) / kChunkVecs;
-    const int width = p.table == nullptr ? 1 : p.table_width;
-    // one unit per wave, or (a grid capped at the resident capacity) units strided over the waves
-    const int64_t stride = static_cast<int64_t>(gridDim.x) * 4;
-    // a timed-out barrier (see combine_rows_kernel): no peer stores, NaN output
-    const bool aborted = p.error_flag != nullptr && (__hip_atomic_load(p.error_flag, __ATOMIC_RELAXED,
-                                                                       __HIP_MEMORY_SCOPE_AGENT) & 2);
-    if (aborted && p.out_rows != nullptr) return;
-    for (int64_t u = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6); u < p.num_units; u += stride) {
+    __syncthreads();
+    if (it >= items) return;
     int32_t my_slot = -1;
     float my_w = 0.0f;
     if (lane < width) {
-        my_slot = p.table == nullptr ? static_cast<int32_t>(u) : p.table[u * p.table_stride + lane];
-        if (my_slot >= p.num_src_rows) {                     // never dereference a bad slot
-            if (p.error_flag != nullptr) atomicOr(p.error_flag, 1);
-            my_slot = -1;
-        }
-        if constexpr (kWeighted) my_w = my_slot >= 0 ? p.row_weights[my_slot] : 0.0f;
+        const int ul = static_cast<int>(it / nchunks - u_first);
+        my_slot = s_slot[ul][lane];
+        if constexpr (kWeighted) my_w = s_w[ul][lane];
     }
-    if (aborted) my_slot = -1;
-    const uint64_t valid = __ballot(my_slot >= 0);
-    const int n = __popcll(valid);
-
-    uint16_t* const out_row = p.out_rows != nullptr ? reinterpret_cast<uint16_t*>(checked_row(p, u, lane, true))
-                                                     : p.out + u * p.out_stride;
-    if (out_row == nullptr) continue;                    // rejected / outside every window: flagged
-
-    const bool wlane = p.num_weights > 0 && lane < p.weights_pad;     // top-k weight pass-through, once per unit
-    const float wv = wlane ? pass_through_weight<kWeighted>(p, u, lane, my_slot, my_w) : 0.0f;
-
-    // the valid lanes in ascending order (n <= kStreamWidth) with their row pointers and weights
-    const u32x4* rows[kStreamWidth];
-    float wj[kStreamWidth];
-    {
-        uint64_t rem = valid;
-#pragma unroll
-        for (int j = 0; j < kStreamWidth; ++j) {
-            const int l = rem != 0ull ? static_cast<int>(__builtin_ctzll(rem)) : 0;
-            const int32_t sj = __builtin_amdgcn_readlane(my_slot, l);
-            rows[j] = reinterpret_cast<const u32x4*>(p.src + static_cast<int64_t>(sj < 0 ? 0 : sj) * p.src_stride);
-            wj[j] = kWeighted ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_w), l)) : 0.0f;
-            rem &= rem - 1ull;
-        }
-    }
-    const bool has_bias0 = p.bias0 != nullptr, has_bias1 = p.bias1 != nullptr;
-    const bool has_bias = has_bias0 || has_bias1;
-    bool copy_row = false;
-    float init;
-    if constexpr (kMode == DEEPEP_MODE_LOCAL || kMode == DEEPEP_MODE_FUSED) {
-        copy_row = !kWeighted && n == 1;
-        init = (!kWeighted && n == 2) ? -0.0f : 0.0f;
-    } else {
-        init = (!kWeighted && !has_bias && n == 2) ? -0.0f : 0.0f;
-    }
-    const __amdgpu_buffer_rsrc_t orow = row_rsrc(out_row, p.hidden * 2);
-
-    auto issue = [&](int c, u32x4 (&v)[kStreamWidth][kVPT]) {
-#pragma unroll
-        for (int j = 0; j < kStreamWidth; ++j)
-            if (j < n) {
-#pragma unroll
-                for (int q = 0; q < kVPT; ++q) v[j][q] = load16<true>(rows[j] + c * kChunkVecs + q * 64 + lane);
-            }
-    };
-    auto finish = [&](int c, u32x4 (&v)[kStreamWidth][kVPT]) {
-        u32x4 result[kVPT];
-#pragma unroll
-        for (int q = 0; q < kVPT; ++q) {
-            const int vi = c * kChunkVecs + q * 64 + lane;
-            float acc[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) acc[e] = init;
-            if constexpr (kMode == DEEPEP_MODE_EPILOGUE) {     // bias0 then bias1 before the partials
-                if (has_bias0) acc_add(acc, *(reinterpret_cast<const u32x4*>(p.bias0 + u * p.hidden) + vi));
-                if (has_bias1) acc_add(acc, *(reinterpret_cast<const u32x4*>(p.bias1 + u * p.hidden) + vi));
-            }
-            if (copy_row) {
-                result[q] = v[0][q];
-            } else {
-#pragma unroll
-                for (int j = 0; j < kStreamWidth; ++j)
-                    if (j < n) {
-                        if constexpr (kWeighted) acc_fma(acc, v[j][q], wj[j]);
-                        else acc_add(acc, v[j][q]);
-                    }
-                result[q] = acc_pack(acc);
-            }
-            if constexpr (kMode == DEEPEP_MODE_FUSED) {
-                float a[8];
-#pragma unroll
-                for (int e = 0; e < 8; ++e) a[e] = 0.0f;
-                if (has_bias0) acc_add(a, *(reinterpret_cast<const u32x4*>(p.bias0 + u * p.hidden) + vi));
-                if (has_bias1) acc_add(a, *(reinterpret_cast<const u32x4*>(p.bias1 + u * p.hidden) + vi));
-                if (n > 0) acc_add(a, result[q]);
-                result[q] = acc_pack(a);
-            }
-            if (aborted) result[q] = (u32x4){0x7fc07fc0u, 0x7fc07fc0u, 0x7fc07fc0u, 0x7fc07fc0u};
-            __builtin_amdgcn_raw_buffer_store_b128(result[q], orow, vi * 16, 0, kStoreAux);
-        }
-    };
-    u32x4 va[kStreamWidth][kVPT], vb[kStreamWidth][kVPT];
-    issue(0, va);
-    for (int c = 0; c < nchunks; c += 2) {
-        if (c + 1 < nchunks) issue(c + 1, vb);
-        finish(c, va);
-        if (c + 1 >= nchunks) break;
-        if (c + 2 < nchunks) issue(c + 2, va);
-        finish(c + 1, vb);
-    }
-    if (wlane) store_weight(p, u, out_row, lane, wv);
-    }
+    combine_item<kMode, kWeighted, kVPT, kFull, kStoreAux, kGroup>(p, it, nchunks, nvec, lane, my_slot, my_w);
 }
 
-int device_cus() {
-    static int cus = 0;
-    if (cus == 0) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
-                                                    hipSuccess)
-            cus = 256;
-    }
-    return cus;
-}
-
-// CU-budget streams created by deepep_stream_create_cu_budget (symmetric.hip) and their CU counts:
-// a launch on one takes a persistent grid sized to the budget.
+// CU-budget streams created by deepep_stream_create_cu_budget (symmetric.hip) and their CU counts: a
+// launch on one keeps its full grid (the CU mask alone holds it to the budget) with at most 4 rows in
+// flight per lane -- 64 VGPRs, 8 waves per SIMD, more bytes in flight per budgeted CU than 8 rows at 5
+// waves (config 2: 128 CUs 208 vs 235 us, 32 CUs 603 vs 661 us, profiles/r02n_kcu2.jsonl).
 std::mutex g_budget_mutex;
 std::map<hipStream_t, int> g_budget_cus;
 
@@ -593,119 +379,42 @@ int budget_cus_of(hipStream_t s) {
     return it == g_budget_cus.end() ? 0 : it->second;
 }
 
-// persistent: the grid is capped at the workgroups the chip holds at once (occupancy x CUs), so
-// there is no partial last round of long-lived waves; otherwise one unit per wave
-template <int kMode, bool kWeighted, int kVPT, int kAux>
-void launch_stream_policy(const Params& p, bool persistent, hipStream_t stream) {
-    const auto kernel = combine_stream_kernel<kMode, kWeighted, kVPT, kAux>;
-    int64_t blocks = (p.num_units + 3) / 4;
-    if (persistent || p.cap_cus > 0) {
-        static int per_cu = 0;                    // per template instance
-        if (per_cu == 0 && hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess)
-            per_cu = 1;
-        blocks = std::min<int64_t>(blocks, std::max(1, per_cu) * static_cast<int64_t>(p.cap_cus > 0 ? p.cap_cus
-                                                                                                    : device_cus()));
-    }
-    hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream, p);
-}
-
-template <int kMode, bool kWeighted, int kVPT>
-void launch_stream(const Params& p, int policy, bool persistent, hipStream_t stream) {
-    if (policy == 0) launch_stream_policy<kMode, kWeighted, kVPT, 0>(p, persistent, stream);
-    else if (policy == 1) launch_stream_policy<kMode, kWeighted, kVPT, kAuxNT>(p, persistent, stream);
-    else if (policy == 3) launch_stream_policy<kMode, kWeighted, kVPT, kAuxSys>(p, persistent, stream);
-    else launch_stream_policy<kMode, kWeighted, kVPT, kAuxSC1>(p, persistent, stream);
-}
-
-struct LaunchConfig {
-    int vec_per_lane = 0;        // 0: auto (16-byte vectors per lane per source row and item)
-    int stage_lds = -1;          // -1: auto (1 = LDS staging per workgroup, 0 = per-wave registers)
-    int store_policy = -1;       // -1: auto (0 plain, 1 nt, 2 sc1)
-    int rows_in_flight = 0;      // 0: auto (source rows loaded per lane before accumulating: 2, 4 or 8)
-};
-LaunchConfig g_config;
-
-// Item kernel vs streaming kernel.  Both give identical bits; which is faster depends on the box
-// (config 2: the streaming kernel ran 161 us against 171 us on one MI355X and 187-197 us against
-// 175 us on most others).  The item kernel is the default; nothing is timed
-// inside a call (a per-shape autotune used to, with a host sync in the call path).
-// deepep_set_kernel_choice forces another candidate.
-int g_kernel_choice = -1;        // -1 default (the item kernel), else a candidate of launch_combine
-int g_last_choice = 0;
-
-template <int kMode, bool kWeighted, int kVPT, bool kFull, int kAux, bool kLDS, int kWaves, int kGroup>
-void launch_shape(const Params& p, int64_t items, hipStream_t stream) {
-    const int64_t blocks = (items + kWaves - 1) / kWaves;
-    if constexpr (kGroup == 8) {
-        if (p.cap_cus > 0) {                      // persistent: what the (budgeted) CUs hold at once
-            const auto kernel = combine_rows_kernel<kMode, kWeighted, kVPT, kFull, kAux, kLDS, kWaves, kGroup, true>;
-            static int per_cu = 0;                // per template instance
-            if (per_cu == 0 &&
-                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 64 * kWaves, 0) != hipSuccess)
-                per_cu = 1;
-            const int64_t grid = std::min<int64_t>(blocks, static_cast<int64_t>(std::max(1, per_cu)) * p.cap_cus);
-            hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>(grid)), dim3(64 * kWaves), 0, stream, p);
-            return;
-        }
-    }
-    hipLaunchKernelGGL((combine_rows_kernel<kMode, kWeighted, kVPT, kFull, kAux, kLDS, kWaves, kGroup, false>),
-                       dim3(static_cast<unsigned>(blocks)), dim3(64 * kWaves), 0, stream, p);
-}
-
-// Workgroup shape and rows in flight.  The fused / epilogue reduces (8 rows per token at EP = 1):
-// 8 waves x 8 rows in flight (measured on two boxes: 157.5-159.7 us vs 159.6-161.1 us with 4 waves,
-// 169 us with 16, 180 us with 12).  Phase A of EP > 1 (1.5 local rows per received token at EP = 8)
-// gains from occupancy instead: see launch_combine for the automatic choice.
-template <int kMode, bool kWeighted, int kVPT, bool kFull, int kAux>
-void launch_lds(const Params& p, bool lds, int waves, int group, hipStream_t stream) {
-    const int nvec = p.hidden / 8;
-    const int64_t items = static_cast<int64_t>(p.num_units) * ((nvec + 64 * kVPT - 1) / (64 * kVPT));
-    if constexpr (kAux == kAuxSC1 || kAux == kAuxSys || kAux == kAuxSC1NT || kAux > 1000) {
-        if (lds) {
-            if (waves == 8) {
-                if (group == 2) launch_shape<kMode, kWeighted, kVPT, kFull, kAux, true, 8, 2>(p, items, stream);
-                else if (group == 4) launch_shape<kMode, kWeighted, kVPT, kFull, kAux, true, 8, 4>(p, items, stream);
-                else launch_shape<kMode, kWeighted, kVPT, kFull, kAux, true, 8, 8>(p, items, stream);
-            } else {
-                if (group == 2) launch_shape<kMode, kWeighted, kVPT, kFull, kAux, true, 4, 2>(p, items, stream);
-                else if (group == 4) launch_shape<kMode, kWeighted, kVPT, kFull, kAux, true, 4, 4>(p, items, stream);
-                else launch_shape<kMode, kWeighted, kVPT, kFull, kAux, true, 4, 8>(p, items, stream);
-            }
-            return;
-        }
-    }
-    if (lds) launch_shape<kMode, kWeighted, kVPT, kFull, kAux, true, 4, 8>(p, items, stream);
-    else launch_shape<kMode, kWeighted, kVPT, kFull, kAux, false, 4, 8>(p, items, stream);
-}
+// The one tuning knob left (diagnostics; deepep_set_launch_config): vectors per lane (bits 0-3) and rows
+// in flight (bits 4-7), 0 = automatic.  One atomic word, read once per launch, so a launch never sees
+// half of another thread's update.
+std::atomic<uint32_t> g_launch_config{0};
 
 struct Shape {
-    int vpt, policy, waves, group;
-    bool lds;
+    int vpt, waves, group;
 };
 
-template <int kMode, bool kWeighted, int kVPT, bool kFull>
-void launch_aux(const Params& p, const Shape& sh, hipStream_t stream) {
-    if (sh.policy == 0) launch_lds<kMode, kWeighted, kVPT, kFull, 0>(p, sh.lds, sh.waves, sh.group, stream);
-    else if (sh.policy == 1) launch_lds<kMode, kWeighted, kVPT, kFull, kAuxNT>(p, sh.lds, sh.waves, sh.group, stream);
-    else if (sh.policy == 3) launch_lds<kMode, kWeighted, kVPT, kFull, kAuxSys>(p, sh.lds, sh.waves, sh.group, stream);
-    else if (sh.policy == 4) launch_lds<kMode, kWeighted, kVPT, kFull, kAuxSC1NT>(p, sh.lds, sh.waves, sh.group, stream);
-    else if (sh.policy == 5) {
-        if constexpr (kMode == DEEPEP_MODE_LOCAL) launch_lds<kMode, kWeighted, kVPT, kFull, kAuxPerUnit>(p, sh.lds, sh.waves, sh.group, stream);
-        else launch_lds<kMode, kWeighted, kVPT, kFull, kAuxSC1>(p, sh.lds, sh.waves, sh.group, stream);
-    }
-    else launch_lds<kMode, kWeighted, kVPT, kFull, kAuxSC1>(p, sh.lds, sh.waves, sh.group, stream);
+template <int kMode, bool kWeighted, int kVPT, bool kFull, int kAux, int kWaves>
+void launch_group(const Params& p, int group, hipStream_t stream) {
+    const int nvec = p.hidden / 8;
+    const int64_t items = static_cast<int64_t>(p.num_units) * ((nvec + 64 * kVPT - 1) / (64 * kVPT));
+    const dim3 grid(static_cast<unsigned>((items + kWaves - 1) / kWaves)), block(64 * kWaves);
+    if (group == 2)
+        hipLaunchKernelGGL((combine_rows_kernel<kMode, kWeighted, kVPT, kFull, kAux, kWaves, 2>), grid, block, 0, stream, p);
+    else if (group == 4)
+        hipLaunchKernelGGL((combine_rows_kernel<kMode, kWeighted, kVPT, kFull, kAux, kWaves, 4>), grid, block, 0, stream, p);
+    else
+        hipLaunchKernelGGL((combine_rows_kernel<kMode, kWeighted, kVPT, kFull, kAux, kWaves, 8>), grid, block, 0, stream, p);
 }
 
-template <int kMode, bool kWeighted>
-void launch_vpt(const Params& p, const Shape& sh, hipStream_t stream) {
+template <int kMode, bool kWeighted, int kAux>
+void launch_shape(const Params& p, const Shape& sh, hipStream_t stream) {
     const int nvec = p.hidden / 8;
+#define DEEPEP_WAVES(VPT, FULL)                                                            \
+    (sh.waves == 4 ? launch_group<kMode, kWeighted, VPT, FULL, kAux, 4>(p, sh.group, stream) \
+                   : launch_group<kMode, kWeighted, VPT, FULL, kAux, 8>(p, sh.group, stream))
     if (sh.vpt == 1) {
-        if (nvec % 64 == 0) launch_aux<kMode, kWeighted, 1, true>(p, sh, stream);
-        else launch_aux<kMode, kWeighted, 1, false>(p, sh, stream);
+        if (nvec % 64 == 0) DEEPEP_WAVES(1, true);
+        else DEEPEP_WAVES(1, false);
     } else {
-        if (nvec % 128 == 0) launch_aux<kMode, kWeighted, 2, true>(p, sh, stream);
-        else launch_aux<kMode, kWeighted, 2, false>(p, sh, stream);
+        if (nvec % 128 == 0) DEEPEP_WAVES(2, true);
+        else DEEPEP_WAVES(2, false);
     }
+#undef DEEPEP_WAVES
 }
 
 bool aligned16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15u) == 0; }
@@ -830,8 +539,6 @@ int deepep_combine_reduce(int mode, int weighted,
     p.error_flag = error_flag;
     p.out_rows = nullptr;
     p.weights_offset = 0;
-    p.xcd_blocks = 0;
-    p.cap_cus = 0;
     p.win_bases = nullptr;
     p.win_count = 0;
     p.win_limit = 0;
@@ -897,8 +604,6 @@ int deepep_combine_reduce_scatter(int weighted,
     p.error_flag = error_flag;
     p.out_rows = out_rows;
     p.weights_offset = weights_offset;
-    p.xcd_blocks = 0;
-    p.cap_cus = 0;
     p.win_bases = window_bases;
     p.win_count = num_windows;
     p.win_limit = static_cast<uint64_t>(window_bytes - row_extent);
@@ -909,118 +614,48 @@ int deepep_combine_reduce_scatter(int weighted,
 
 namespace {
 
-int launch_combine(int mode, int weighted, const Params& p_in, deepep_stream_t stream) {
-    Params p = p_in;
-    // Launch shape: one wave per (unit, 64 x vpt x 16-byte column chunk) item; at hidden 7168 a
-    // token is 7 items of 2 KiB per source row.
+int launch_combine(int mode, int weighted, const Params& p, deepep_stream_t stream) {
+    // Launch shape: one wave per (unit, 64 x vpt x 16-byte column chunk) item, `waves` items per
+    // workgroup, `group` source rows loaded per lane before any is accumulated.  Measured per shape
+    // class (tools/kshapes.py, tools/kphase_a.py, tools/kphase_b.py):
+    //   fused reduce over top-k >= 5, rows >= 256 vectors: 1 KiB chunks, 2 rows, 4 waves -- few registers,
+    //     many waves (config 2: -0.9 to -1.6 % against 2 KiB / 8 rows / 8 waves on three boxes);
+    //   fused over top-k >= 5, rows of 128-255 vectors: 2 KiB chunks, 4 rows, 8 waves;
+    //   epilogue (phase B) and the other fused shapes: 2 KiB chunks, 8 rows, 8 waves;
+    //   phase A (LOCAL, ~1.5 local rows per received token at EP = 8): 2 KiB chunks, 4 rows, 4 waves
+    //     (64 VGPRs, 8 waves per SIMD; 1 KiB chunks lose there, 297-330 vs 249.6 us);
+    // rows in flight are capped at the slot table's width rounded up to 2 / 4 (top-2: 33.7 vs 40.1 us),
+    // and at 4 on a CU-budget stream.
+    const uint32_t cfg = g_launch_config.load(std::memory_order_relaxed);
+    const int cfg_vpt = static_cast<int>(cfg & 15u), cfg_rows = static_cast<int>((cfg >> 4) & 15u);
     const int nvec = p.hidden / 8;
-    Shape sh;
-    sh.vpt = g_config.vec_per_lane > 0 ? g_config.vec_per_lane : (nvec >= 128 ? 2 : 1);
-    if (sh.vpt != 1 && sh.vpt != 2) sh.vpt = 2;
-    sh.lds = g_config.stage_lds >= 0 ? g_config.stage_lds != 0 : true;
-    // store policies: 0 plain, 1 nt, 2 sc1 (fused / epilogue default), 3 system scope (peer windows),
-    // 4 sc1 nt (phase A default), 5 per unit (kAuxPerUnit; opt-in).  Phase A's packed send rows are written
-    // once and read back only by the exchange, so they stream past L2 (sc1 nt): EP = 8, back to back, 248.9 vs
-    // 251.4 us with sc1 (profiles/r04a_kphasea.jsonl), and the only policy within 2 % of the best in every
-    // cache state measured (r04i_kphasea_cache_state.jsonl).  The fused and epilogue reduces keep sc1 (their
-    // output is written in token order; sc1 is best or tied in every cache state, r04i_kshapes_cache_state.jsonl).
-    const int auto_policy = mode == DEEPEP_MODE_LOCAL ? 4 : 2;
-    sh.policy = p.out_rows != nullptr ? 3 : (g_config.store_policy == 4 ? 5 : g_config.store_policy == 3 ? 4 :
-                                              (g_config.store_policy >= 0 ? g_config.store_policy : auto_policy));
-    // units_per_block 4 / 8 forces the workgroup shape; 0 = automatic
-    sh.waves = p.units_per_block == 4 ? 4 : (p.units_per_block == 8 ? 8 : (mode == DEEPEP_MODE_LOCAL ? 4 : 8));
-    // rows in flight per lane: 8 for the fused / epilogue reduces (8 rows per token at EP = 1), 4 for
-    // phase A (about 1.5 local rows per received token at EP = 8: 64 VGPRs and 8 waves per SIMD beat
-    // deeper per-wave loads, tools/kphase.py 252-254 vs 256-260 us)
-    // A unit never has more valid rows than its table is wide, so the rows in flight are capped at the
-    // width rounded up to 2 / 4: registers for rows that never come only cost occupancy (top-2, config-2
-    // shape otherwise: 33.7 vs 40.1 us; top-4: 93.5 vs 95.9 us; tools/kshapes.py, profiles/r04e_kshapes_*, r04f_kshapes_*).
     const int width = p.table == nullptr ? 1 : p.table_width;
     const int width_cap = width <= 2 ? 2 : (width <= 4 ? 4 : 8);
-    sh.group = g_config.rows_in_flight > 0 ? g_config.rows_in_flight
-                                           : std::min(mode == DEEPEP_MODE_LOCAL ? 4 : 8, width_cap);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    // A forced streaming kernel (one wave per unit, chunks pipelined) applies only when the shape is
-    // automatic: an explicit units_per_block / LDS / rows-in-flight setting selects the item kernel
-    // (which also serves tables wider than kStreamWidth and ragged hidden sizes).
-    const bool stream_ok = (p.table == nullptr || p.table_width <= kStreamWidth) && nvec % (64 * sh.vpt) == 0 &&
-                           p.units_per_block == 0 && g_config.stage_lds < 0 && g_config.rows_in_flight == 0;
-    auto launch_items = [&]() {
-        if (mode == DEEPEP_MODE_LOCAL) {
-            if (weighted) launch_vpt<DEEPEP_MODE_LOCAL, true>(p, sh, s);
-            else launch_vpt<DEEPEP_MODE_LOCAL, false>(p, sh, s);
-        } else if (mode == DEEPEP_MODE_EPILOGUE) {
-            if (weighted) launch_vpt<DEEPEP_MODE_EPILOGUE, true>(p, sh, s);
-            else launch_vpt<DEEPEP_MODE_EPILOGUE, false>(p, sh, s);
-        } else {
-            if (weighted) launch_vpt<DEEPEP_MODE_FUSED, true>(p, sh, s);
-            else launch_vpt<DEEPEP_MODE_FUSED, false>(p, sh, s);
-        }
-    };
-    auto launch_streaming = [&](int vpt, bool persistent) {
-#define DEEPEP_STREAM(M, W) \
-        (vpt == 1 ? launch_stream<M, W, 1>(p, sh.policy, persistent, s) \
-                  : launch_stream<M, W, 2>(p, sh.policy, persistent, s))
-        if (mode == DEEPEP_MODE_LOCAL) {
-            if (weighted) DEEPEP_STREAM(DEEPEP_MODE_LOCAL, true); else DEEPEP_STREAM(DEEPEP_MODE_LOCAL, false);
-        } else if (mode == DEEPEP_MODE_EPILOGUE) {
-            if (weighted) DEEPEP_STREAM(DEEPEP_MODE_EPILOGUE, true); else DEEPEP_STREAM(DEEPEP_MODE_EPILOGUE, false);
-        } else {
-            if (weighted) DEEPEP_STREAM(DEEPEP_MODE_FUSED, true); else DEEPEP_STREAM(DEEPEP_MODE_FUSED, false);
-        }
-#undef DEEPEP_STREAM
-    };
-    // candidates: 0 item kernel, 1 streaming kernel (sh.vpt vectors per lane), 2 streaming kernel with
-    // 1 vector per lane (half the registers, more waves per SIMD), 3 streaming kernel on a persistent
-    // grid (sh.vpt vectors per lane)
-    // 4: the item kernel with XCD-contiguous workgroup order -- it lost
-    // on every measurement (config 2 188.4 vs 175.3 us, EP = 8 phase A 318 vs 301, phase B 126 vs
-    // 115): neighbouring items spread over all XCDs stream better
-    // 5: the item kernel on a persistent grid (as many workgroups as the chip holds at once)
-    // 6: the item kernel on its full grid (what the default does on a CU-budget stream too)
-    // On a CU-budget stream the item kernel keeps its full grid (the CU mask alone holds it to the
-    // budget) with 4 rows in flight per lane: 64 VGPRs, 8 waves per SIMD, so a budgeted CU keeps more
-    // bytes in flight than with 8 rows at 5 waves (config 2, profiles/r02n_kcu2.jsonl:
-    // 128 CUs 208 vs 235 us on a persistent grid, 32 CUs 603 vs 661 us; the whole chip is unchanged);
-    // the streaming kernels and the forced persistent item kernel take a persistent grid sized to it.
     const int budget = budget_cus_of(s);
-    if (budget > 0 && g_config.rows_in_flight == 0) sh.group = std::min(4, width_cap);
-    // The EP = 1 fused reduce over wide tables (top-k >= 5) and rows of at least 256 vectors: 1 vector per
-    // lane (1 KiB chunks), 2 rows in flight, 4-wave workgroups -- few registers, many waves.  Three boxes,
-    // same output buffer, medians of 3-5 interleaved rounds (tools/kshapes.py, profiles/r04e_kshapes_*, r04f_kshapes_*):
-    // config 2 172.4 / 171.1 / 173.9 us vs 175.1 / 173.9 / 175.5 (-0.9 to -1.6 %), hidden 4096 -0.9 to
-    // -2.8 %, hidden 2048 -1.4 to -2.2 %, hidden 5120 x top-6 -1.7 to -2.5 %.  Not for phase A (LOCAL:
-    // 295 vs 247 us, tools/kphase_a.py) nor narrower rows (hidden 1024: 2 vectors, 4 rows, 8 waves win).
-    const bool fused_wide = mode == DEEPEP_MODE_FUSED && width >= 5 && nvec >= 256 && budget == 0 &&
-                            g_config.vec_per_lane == 0 && g_config.rows_in_flight == 0 && g_config.stage_lds < 0 &&
-                            p.units_per_block == 0;
-    // hidden 1024 (one 2 KiB item per row): 4 rows in flight, 23.7 / 23.6 vs 25.1 / 25.2 us on two boxes
-    const bool fused_narrow = mode == DEEPEP_MODE_FUSED && width >= 5 && nvec >= 128 && nvec < 256 && budget == 0 &&
-                              g_config.vec_per_lane == 0 && g_config.rows_in_flight == 0 && g_config.stage_lds < 0 &&
-                              p.units_per_block == 0;
-    auto launch_choice = [&](int c) {
-        if (c == 0 && fused_wide) {
-            sh.vpt = 1;
-            sh.group = 2;
-            sh.waves = 4;
-        } else if (c == 0 && fused_narrow) {
-            sh.group = 4;
-        }
-        p.xcd_blocks = c == 4 ? 1 : 0;
-        p.cap_cus = (c == 0 || c == 4 || c == 6) ? 0 : (budget > 0 ? budget : (c == 5 ? device_cus() : 0));
-        // the persistent item grid exists for 8 rows in flight only (launch_shape): a capped launch always
-        // takes it, so a forced choice 5 never silently runs the full grid
-        if (p.cap_cus > 0 && (c == 0 || c == 4 || c == 5 || c == 6)) sh.group = 8;
-        // a persistent grid stages slots per wave (no workgroup barrier between a wave's items), so
-        // each wave streams at its own pace
-        sh.lds = g_config.stage_lds >= 0 ? g_config.stage_lds != 0 : p.cap_cus == 0;
-        if (c == 0 || c == 4 || c == 5 || c == 6) launch_items();
-        else launch_streaming(c == 2 ? 1 : sh.vpt, c == 3);
-    };
-    const int forced = g_kernel_choice;
-    const int choice = (forced == 5 || forced == 6) ? forced : ((stream_ok && forced >= 0) ? forced : 0);
-    g_last_choice = choice;
-    launch_choice(choice);
+    Shape sh;
+    sh.vpt = nvec >= 128 ? 2 : 1;
+    sh.waves = mode == DEEPEP_MODE_LOCAL ? 4 : 8;
+    sh.group = std::min(mode == DEEPEP_MODE_LOCAL || budget > 0 ? 4 : 8, width_cap);
+    const bool automatic = cfg == 0 && p.units_per_block == 0 && budget == 0;
+    if (automatic && mode == DEEPEP_MODE_FUSED && width >= 5 && nvec >= 256) {
+        sh.vpt = 1;
+        sh.group = 2;
+        sh.waves = 4;
+    } else if (automatic && mode == DEEPEP_MODE_FUSED && width >= 5 && nvec >= 128) {
+        sh.group = 4;
+    }
+    if (cfg_vpt != 0) sh.vpt = cfg_vpt;
+    if (cfg_rows != 0) sh.group = cfg_rows;
+    if (p.units_per_block == 4 || p.units_per_block == 8) sh.waves = p.units_per_block;
+
+#define DEEPEP_POLICY(M, AUX) \
+    (weighted ? launch_shape<M, true, AUX>(p, sh, s) : launch_shape<M, false, AUX>(p, sh, s))
+    if (mode == DEEPEP_MODE_LOCAL && p.out_rows != nullptr) DEEPEP_POLICY(DEEPEP_MODE_LOCAL, kAuxSys);
+    else if (mode == DEEPEP_MODE_LOCAL) DEEPEP_POLICY(DEEPEP_MODE_LOCAL, kAuxSC1NT);
+    else if (mode == DEEPEP_MODE_EPILOGUE) DEEPEP_POLICY(DEEPEP_MODE_EPILOGUE, kAuxSC1);
+    else DEEPEP_POLICY(DEEPEP_MODE_FUSED, kAuxSC1);
+#undef DEEPEP_POLICY
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess)
         return set_error(DEEPEP_ERR_HIP, "combine launch failed: %s", hipGetErrorString(err));
@@ -1064,22 +699,12 @@ int deepep_build_local_plan(const int32_t* src_metadata, int num_recv_tokens, in
     return DEEPEP_OK;
 }
 
-int deepep_set_kernel_choice(int choice) {
-    if (choice < -1 || choice > 6) return set_error(DEEPEP_ERR_INVALID_ARG, "kernel choice must be -1 or 0..6");
-    g_kernel_choice = choice;
-    return DEEPEP_OK;
-}
-
-int deepep_last_kernel_choice(void) { return g_last_choice; }
-
-int deepep_set_launch_config(int vec_per_lane, int stage_lds, int store_policy, int rows_in_flight) {
-    if (vec_per_lane < 0 || vec_per_lane > 2 || stage_lds < -1 || stage_lds > 1 || store_policy < -1 ||
-        store_policy > 4 || (rows_in_flight != 0 && rows_in_flight != 2 && rows_in_flight != 4 && rows_in_flight != 8))
-        return set_error(DEEPEP_ERR_INVALID_ARG, "invalid launch configuration");
-    g_config.vec_per_lane = vec_per_lane;
-    g_config.stage_lds = stage_lds;
-    g_config.store_policy = store_policy;
-    g_config.rows_in_flight = rows_in_flight;
+int deepep_set_launch_config(int vec_per_lane, int rows_in_flight) {
+    if (vec_per_lane < 0 || vec_per_lane > 2 ||
+        (rows_in_flight != 0 && rows_in_flight != 2 && rows_in_flight != 4 && rows_in_flight != 8))
+        return set_error(DEEPEP_ERR_INVALID_ARG, "invalid launch configuration (vec_per_lane 0-2, rows_in_flight 0/2/4/8)");
+    g_launch_config.store(static_cast<uint32_t>(vec_per_lane) | (static_cast<uint32_t>(rows_in_flight) << 4),
+                          std::memory_order_relaxed);
     return DEEPEP_OK;
 }
 

@@ -15,6 +15,7 @@
 // whole number of blocks, so every chunk's exchange sizes are sums of block counts.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <climits>
 #include <stdio.h>
 
 #include "../../include/deepep_amd.h"
@@ -69,11 +70,25 @@ block_counts_kernel(const int64_t* __restrict__ topk_idx, int T, int K, int epr,
     }
 }
 
+// Order of the peer groups inside a chunk's rows.  Without the local bypass: rank order.  With it
+// (DEEPEP_PLAN_LOCAL_BYPASS, the RCCL transport): the expert side puts its own rank's units last -- the
+// send rows of the other ranks stay one contiguous, rank-ordered all-to-all input with a zero diagonal
+// split, and the own units land right after them -- and the source side puts the rows of its own rank
+// first, followed by the all-to-all output in rank order; the two layouts meet in one allocation
+// [send rows | own rows | received rows], so phase B reads the own partials where phase A wrote them
+// (the reference's own-slot store is local too, combine.cuh:96-101).
+__device__ __forceinline__ int send_order(int l, int rank, int R, bool bypass) {
+    return !bypass ? l : (l == rank ? R - 1 : (l > rank ? l - 1 : l));
+}
+__device__ __forceinline__ int recv_order(int l, int rank, bool bypass) {
+    return !bypass ? l : (l == rank ? 0 : (l < rank ? l + 1 : l));
+}
+
 // ---------------------------------------------------------------- expert side
 // One wave per segment (source rank s, block b): the received rows of s's tokens [64 b, 64 b + 64),
 // contiguous in receive order (grouped by source rank, ascending token).  Unit order inside chunk c:
-// grouped by source rank (the RCCL send buffer), or round-robin over the source ranks (interleave:
-// the xGMI stores then reach every peer at once) -- unit p of source s goes to position
+// grouped by source rank in send_order (the RCCL send buffer), or round-robin over the source ranks
+// (interleave: the xGMI stores then reach every peer at once) -- unit p of source s goes to position
 // sum_{s'} min(n_{s'}, p + [s' < s]), the stable sort of (p * R + s).
 __global__ void __launch_bounds__(64)
 plan_expert_kernel(const int32_t* __restrict__ meta, int num_recv, int K, int R, int rank, int t_max,
@@ -88,6 +103,7 @@ plan_expert_kernel(const int32_t* __restrict__ meta, int num_recv, int K, int R,
     if (seg_len == 0) return;                                   // wave-uniform
     const bool single = flags & DEEPEP_PLAN_SINGLE, expanded = flags & DEEPEP_PLAN_EXPANDED;
     const bool interleave = flags & DEEPEP_PLAN_INTERLEAVE, rank_layout = flags & DEEPEP_PLAN_RANK_LAYOUT;
+    const bool bypass = (flags & DEEPEP_PLAN_LOCAL_BYPASS) && !interleave;
     const int32_t* cnt = single ? recv_pairs : recv_tok;
     const int cb0 = (b / bpc) * bpc, cb1 = min(cb0 + bpc, nb);
     // lane l < R: rows received from l (all blocks), units of l before the chunk, units of l in it
@@ -111,7 +127,9 @@ plan_expert_kernel(const int32_t* __restrict__ meta, int num_recv, int K, int R,
     // source's count stay the caller's fill and are skipped
     const int chunk_base = padded > 0 ? (b / bpc) * R * padded : wave_sum(before_l);
     const int chunk_units = padded > 0 ? R * padded : wave_sum(n_l);     // units of the whole chunk
-    const int grouped_base = padded > 0 ? s * padded : wave_sum(lane < s ? n_l : 0);
+    const int os = send_order(s, rank, R, bypass);
+    const int grouped_base = padded > 0 ? os * padded
+                                        : wave_sum(lane < R && send_order(lane, rank, R, bypass) < os ? n_l : 0);
     p0 = __shfl(p0, s, 64);
     auto position = [&](int p) -> int {                         // unit p of source s inside the chunk
         if (padded > 0) return interleave ? p * R + s : grouped_base + p;
@@ -143,15 +161,18 @@ plan_expert_kernel(const int32_t* __restrict__ meta, int num_recv, int K, int R,
         }
         return bases[src] + static_cast<uint64_t>(off);
     };
-    auto in_chunk = [&](int64_t pos) -> bool {
-        if (pos >= 0 && pos < chunk_units) return true;
+    // A unit is stored only inside its chunk and -- padded -- inside its own source's `padded` positions:
+    // counts that disagree with the metadata (or a token whose lanes on this rank exceed the padding,
+    // handle.build_ep_plan) must never overwrite another source's units.
+    auto in_chunk = [&](int p, int64_t pos) -> bool {
+        if (pos >= 0 && pos < chunk_units && (padded == 0 || p < padded)) return true;
         deepep::record_fault(err, DEEPEP_FLAG_BAD_SLOT, DEEPEP_FAULT_PLAN_UNIT, chunk_base + pos, s, 0, chunk_units);
         return false;
     };
     if (!single) {
         if (!active) return;
         const int pos = position(p0 + lane);
-        if (!in_chunk(pos)) return;
+        if (!in_chunk(p0 + lane, pos)) return;
         const int64_t u = chunk_base + pos;
         if (expanded) {
             for (int k = 0; k < K; ++k) table_a[u * K + k] = m[2 + k];
@@ -174,8 +195,8 @@ plan_expert_kernel(const int32_t* __restrict__ meta, int num_recv, int K, int R,
     for (int k = 0; k < K; ++k) {
         const int32_t slot = m[2 + k];
         if (slot < 0) continue;
-        const int pos = position(p++);
-        if (!in_chunk(pos)) return;
+        const int pos = position(p);
+        if (!in_chunk(p++, pos)) return;
         const int64_t u = chunk_base + pos;
         table_a[u] = slot;
         if (out_rows != nullptr) out_rows[u] = window_row(u, k);
@@ -188,7 +209,7 @@ plan_expert_kernel(const int32_t* __restrict__ meta, int num_recv, int K, int R,
 // combine_reduce_epilogue.cuh:74-95), then -1; the weight table points at each lane's weight inside
 // the packed row of its rank's partial.  Single reduction: the row of every (t, k).
 __global__ void __launch_bounds__(64)
-plan_source_kernel(const int64_t* __restrict__ topk_idx, int T, int K, int epr, int R, int t_max,
+plan_source_kernel(const int64_t* __restrict__ topk_idx, int T, int K, int epr, int R, int rank, int t_max,
                    const int32_t* __restrict__ dst_slot, const int32_t* __restrict__ send_tok,
                    const int32_t* __restrict__ send_pairs, int nb, int bpc, int flags, int64_t row_floats,
                    int64_t w_off, int32_t* __restrict__ table_b, int width, int32_t* __restrict__ wtable, int padded) {
@@ -197,9 +218,11 @@ plan_source_kernel(const int64_t* __restrict__ topk_idx, int T, int K, int epr, 
     const int t = b * kBlk + lane;
     const bool single = flags & DEEPEP_PLAN_SINGLE, window = flags & DEEPEP_PLAN_WINDOW;
     const bool rank_layout = flags & DEEPEP_PLAN_RANK_LAYOUT;
+    const bool bypass = (flags & DEEPEP_PLAN_LOCAL_BYPASS) && !window;
     const int cb0 = (b / bpc) * bpc, cb1 = min(cb0 + bpc, nb);
     if (!window) {
-        // receive buffer of chunk c: grouped by expert rank d, each group in ascending (token[, lane])
+        // receive buffer of chunk c: grouped by expert rank d in recv_order, each group in ascending
+        // (token[, lane])
         int n_l = 0, extra = 0;
         if (lane < R) {
             const int32_t* cl = (single ? send_pairs : send_tok) + static_cast<int64_t>(lane) * nb;
@@ -210,9 +233,16 @@ plan_source_kernel(const int64_t* __restrict__ topk_idx, int T, int K, int epr, 
                 for (int j = 0; j < cb0; ++j) extra -= cl[j];                 // dst_slot counts from token 0
             }
         }
-        const int incl = wave_incl_scan(lane < R ? n_l : 0, lane);
-        // padded: expert rank d's rows of the chunk start at d * padded (a worst-case-padded exchange)
-        if (lane < R) s_base[lane] = (padded > 0 ? lane * padded : incl - n_l) + extra;
+        // rows of the expert ranks before this lane's rank in recv_order (a wave-uniform loop)
+        const int me = recv_order(lane, rank, bypass);
+        int before = 0;
+        for (int l = 0; l < R; ++l) {
+            const int nl = __shfl(n_l, l, 64);
+            if (recv_order(l, rank, bypass) < me) before += nl;
+        }
+        // padded: expert rank d's rows of the chunk start at recv_order(d) * padded (a worst-case-padded
+        // exchange)
+        if (lane < R) s_base[lane] = (padded > 0 ? me * padded : before) + extra;
         __syncthreads();
     }
     int rk[kMaxTopk];
@@ -233,9 +263,15 @@ plan_source_kernel(const int64_t* __restrict__ topk_idx, int T, int K, int epr, 
 #pragma unroll
                 for (int k = 0; k < kMaxTopk; ++k) c += rk[k] == d;
                 int off = s_base[d] + wave_incl_scan(c, lane) - c;
+                // padded: rows past destination d's `padded` rows of the chunk belong to the next
+                // destination -- a unit plan_expert rejected (flagged there); such a lane reads nothing
+                const int lim = padded > 0 ? recv_order(d, rank, bypass) * padded + padded : INT32_MAX;
 #pragma unroll
                 for (int k = 0; k < kMaxTopk; ++k)
-                    if (rk[k] == d) row[k] = off++;
+                    if (rk[k] == d) {
+                        row[k] = off < lim ? off : -1;
+                        ++off;
+                    }
             }
         }
         if (t < T)
@@ -323,14 +359,14 @@ int deepep_plan_expert(const int32_t* src_metadata, int num_recv, int num_topk, 
 }
 
 int deepep_plan_source(const int64_t* topk_idx, int num_tokens, int num_topk, int num_experts, int num_ranks,
-                       int num_max_tokens, const int32_t* dst_slot, const int32_t* send_tok,
+                       int rank, int num_max_tokens, const int32_t* dst_slot, const int32_t* send_tok,
                        const int32_t* send_pairs, int num_blocks, int blocks_per_chunk, int flags,
                        int64_t row_floats, int64_t weights_offset, int32_t* table_b, int table_b_width,
                        int32_t* wtable, int padded_stride, deepep_stream_t stream) {
     const bool single = flags & DEEPEP_PLAN_SINGLE, window = flags & DEEPEP_PLAN_WINDOW;
     const int need_width = single ? num_topk : (num_ranks < num_topk ? num_ranks : num_topk);
     if (num_tokens < 0 || padded_stride < 0 || (window && padded_stride > 0) || num_topk < 1 || num_topk > kMaxTopk || num_ranks < 1 || num_ranks > kMaxRanks ||
-        num_experts % num_ranks != 0 || num_tokens > num_max_tokens || blocks_per_chunk < 1 ||
+        num_experts % num_ranks != 0 || rank < 0 || rank >= num_ranks || num_tokens > num_max_tokens || blocks_per_chunk < 1 ||
         num_blocks < (num_tokens + kBlk - 1) / kBlk || table_b_width != need_width ||
         (num_tokens > 0 && (topk_idx == nullptr || table_b == nullptr)) ||
         (!window && num_tokens > 0 && (send_tok == nullptr || (single ? send_pairs == nullptr : dst_slot == nullptr))) ||
@@ -339,7 +375,7 @@ int deepep_plan_source(const int64_t* topk_idx, int num_tokens, int num_topk, in
     if (num_tokens == 0) return DEEPEP_OK;
     hipLaunchKernelGGL(plan_source_kernel, dim3((num_tokens + kBlk - 1) / kBlk), dim3(64), 0,
                        reinterpret_cast<hipStream_t>(stream), topk_idx, num_tokens, num_topk,
-                       num_experts / num_ranks, num_ranks, num_max_tokens, dst_slot, send_tok, send_pairs, num_blocks,
+                       num_experts / num_ranks, num_ranks, rank, num_max_tokens, dst_slot, send_tok, send_pairs, num_blocks,
                        blocks_per_chunk, flags, row_floats, weights_offset, table_b, table_b_width, wtable,
                        padded_stride);
     return launch_status("plan_source");

@@ -31,6 +31,15 @@ def _require_weight_index(plan) -> None:
                            '(num_max_tokens_per_rank * hidden too large for the weight pass-through)')
 
 
+def _splits(plan, ch, me: int):
+    """(send, receive) all-to-all splits of a chunk: with the local bypass the diagonal is 0 (this
+    rank's own rows never enter the collective)."""
+    if not plan.local_bypass:
+        return list(ch.send_counts), list(ch.back_counts)
+    return ([0 if r == me else n for r, n in enumerate(ch.send_counts)],
+            [0 if r == me else n for r, n in enumerate(ch.back_counts)])
+
+
 class ExchangeMixin:
     """EP > 1 exchange paths; uses the host attributes of ElasticBuffer (group, ranks, streams,
     kernels, _mark, _before_epilogue, _all_to_all)."""
@@ -47,8 +56,16 @@ class ExchangeMixin:
         """EP > 1 combine, chunked: phase A (local reduce per received token) -> all-to-all of
         packed rows [bf16 partial | fp32 top-k weights] -> phase B (epilogue + bias).  With more
         than one chunk, phase A of chunk c+1 runs while RCCL moves chunk c and phase B of chunk
-        c runs on a second stream while RCCL moves chunk c+1."""
+        c runs on a second stream while RCCL moves chunk c+1.
+
+        Local bypass: a chunk's rows live in one allocation [send rows | own rows | received rows].
+        Phase A writes the units of the other ranks (the send rows, rank order) and then this rank's
+        own units right behind them; the all-to-all moves the send rows with a zero split for this
+        rank into the received rows; phase B reads [own rows | received rows] -- the own partials
+        where phase A wrote them, with no copy (the reference stores them into its own receive slot,
+        combine.cuh:96-101).  The plan lays the tables out for it (DEEPEP_PLAN_LOCAL_BYPASS)."""
         kern = self.kernels
+        me = self.rank_idx
         # packed rows [bf16 partial | fp32 weights], whole 128-byte lines (handle.packed_row_layout)
         with_w = topk_weights is not None
         row_bytes, w_off, w_pad = packed_row_layout(hidden, K, with_w)
@@ -71,37 +88,39 @@ class ExchangeMixin:
         in_flight = []
         for ch in plan.chunks:
             with (torch.cuda.stream(sa) if sa is not stream else self._null_ctx()):
-                n_send = sum(ch.send_counts)
-                packed = torch.empty((n_send, row_elems), dtype=x.dtype, device=x.device)
-                partial_w = packed.view(torch.float32)[:, w_off // 4:w_off // 4 + K] if with_w else None
+                n_units, n_back, own = sum(ch.send_counts), sum(ch.back_counts), ch.own
+                n_send = n_units - own                    # rows that travel
+                rows = torch.empty((n_units + n_back - own, row_elems), dtype=x.dtype, device=x.device)
+                partial_w = rows.view(torch.float32)[:n_units, w_off // 4:w_off // 4 + K] if with_w else None
                 self._mark(sa)
-                kern.combine_reduce(MODE_LOCAL, x, packed[:, :hidden], n_send, table=ch.table_a, row_weights=row_w,
-                                    wtable=ch.wtable_a, wsrc=wsrc, out_weights=partial_w, weights_pad=w_pad,
-                                    stream=sa)
+                kern.combine_reduce(MODE_LOCAL, x, rows[:n_units, :hidden], n_units, table=ch.table_a,
+                                    row_weights=row_w, wtable=ch.wtable_a, wsrc=wsrc, out_weights=partial_w,
+                                    weights_pad=w_pad, stream=sa)
                 self._mark(sa)
-                recv = torch.empty((sum(ch.back_counts), row_elems), dtype=x.dtype, device=x.device)
+                send_splits, back_splits = _splits(plan, ch, me)
+                send, recv = rows[:n_send], rows[n_units:]
                 if pipelined:
-                    work = self._a2a_async(recv, packed, ch.back_counts, ch.send_counts)
+                    work = self._a2a_async(recv, send, back_splits, send_splits)
                 else:
-                    self._all_to_all(recv, packed, ch.back_counts, ch.send_counts)
+                    self._all_to_all(recv, send, back_splits, send_splits)
                     work = None
-            in_flight.append((ch, recv, packed, work))
+            in_flight.append((ch, rows[n_send:], rows, work))
         if sa is not stream:
             stream.wait_stream(sa)
         self._before_epilogue(previous_event_before_epilogue)
         if pipelined and previous_event_before_epilogue is not None:
             previous_event_before_epilogue.stream_wait(stream_b)
-        for ch, recv, packed, work in in_flight:
+        for ch, src_b, rows, work in in_flight:
             ctx = torch.cuda.stream(stream_b) if pipelined else self._null_ctx()
             with ctx:
                 sb = stream_b if pipelined else stream
                 if work is not None:
                     work.wait()
                 wtable_b = ch.wtable_b if with_w else None
-                recv_wsrc = recv.view(torch.float32).view(-1) if with_w else None
+                recv_wsrc = src_b.view(torch.float32).view(-1) if with_w else None
                 lo, hi = ch.lo, ch.hi
                 self._mark(sb)
-                kern.combine_reduce(MODE_EPILOGUE, recv[:, :hidden], combined_x[lo:hi], hi - lo, table=ch.table_b,
+                kern.combine_reduce(MODE_EPILOGUE, src_b[:, :hidden], combined_x[lo:hi], hi - lo, table=ch.table_b,
                                     bias0=bias_0[lo:hi] if bias_0 is not None else None,
                                     bias1=bias_1[lo:hi] if bias_1 is not None else None,
                                     wtable=wtable_b, wsrc=recv_wsrc,
@@ -109,16 +128,17 @@ class ExchangeMixin:
                 self._mark(sb)
         if pipelined:
             stream.wait_stream(stream_b)
-            for _, recv, packed, _ in in_flight:          # used on stream_b / the RCCL stream
-                recv.record_stream(stream_b)
-                packed.record_stream(stream_b)
+            for _, _, rows, _ in in_flight:               # used on stream_b / the RCCL stream
+                rows.record_stream(stream_b)
 
     def _combine_single_chunks(self, plan, x, row_w, wsrc, hidden, bias_0, bias_1, combined_x, combined_w,
                                previous_event_before_epilogue, stream) -> None:
-        """Single-reduction combine over RCCL, chunked like _combine_chunks: the pack of chunk c+1
-        runs while RCCL moves chunk c, and the one reduction of chunk c (weighted: the legacy fma
-        chain) runs on a second stream while RCCL moves chunk c+1."""
+        """Single-reduction combine over RCCL, chunked like _combine_chunks (and with its local bypass:
+        this rank's own rows are written in place): the pack of chunk c+1 runs while RCCL moves
+        chunk c, and the one reduction of chunk c (weighted: the legacy fma chain) runs on a second
+        stream while RCCL moves chunk c+1."""
         kern = self.kernels
+        me = self.rank_idx
         w_elems = 1 if row_w is not None else 0          # one gating weight per unreduced row
         row_bytes, w_off, w_pad = packed_row_layout(hidden, 1, bool(w_elems), single=True)
         row_elems = row_bytes // 2
@@ -130,33 +150,35 @@ class ExchangeMixin:
             stream_b.wait_stream(stream)
         in_flight = []
         for ch in plan.chunks:
-            n_send = sum(ch.send_counts)
-            send = torch.empty((n_send, row_elems), dtype=x.dtype, device=x.device)
-            send_w = send.view(torch.float32)[:, w_off // 4:w_off // 4 + 1] if w_elems else None
+            n_units, n_back, own = sum(ch.send_counts), sum(ch.back_counts), ch.own
+            n_send = n_units - own
+            rows = torch.empty((n_units + n_back - own, row_elems), dtype=x.dtype, device=x.device)
+            send_w = rows.view(torch.float32)[:n_units, w_off // 4:w_off // 4 + 1] if w_elems else None
             self._mark(stream)
-            kern.combine_reduce(MODE_LOCAL, x, send[:, :hidden], n_send, table=ch.table_a,
+            kern.combine_reduce(MODE_LOCAL, x, rows[:n_units, :hidden], n_units, table=ch.table_a,
                                 wtable=ch.table_a if w_elems else None, wsrc=wsrc if w_elems else None,
                                 out_weights=send_w, weights_pad=w_pad, stream=stream)
             self._mark(stream)
-            recv = torch.empty((sum(ch.back_counts), row_elems), dtype=x.dtype, device=x.device)
+            send_splits, back_splits = _splits(plan, ch, me)
+            send, recv = rows[:n_send], rows[n_units:]
             if pipelined:
-                work = self._a2a_async(recv, send, ch.back_counts, ch.send_counts)
+                work = self._a2a_async(recv, send, back_splits, send_splits)
             else:
-                self._all_to_all(recv, send, ch.back_counts, ch.send_counts)
+                self._all_to_all(recv, send, back_splits, send_splits)
                 work = None
-            in_flight.append((ch, recv, send, work))
+            in_flight.append((ch, rows[n_send:], rows, work))
         self._before_epilogue(previous_event_before_epilogue)
         if pipelined and previous_event_before_epilogue is not None:
             previous_event_before_epilogue.stream_wait(stream_b)
-        for ch, recv, send, work in in_flight:
+        for ch, src_b, rows, work in in_flight:
             with (torch.cuda.stream(stream_b) if pipelined else self._null_ctx()):
                 sb = stream_b if pipelined else stream
                 if work is not None:
                     work.wait()
-                recv_w = recv.view(torch.float32)[:, w_off // 4].contiguous() if w_elems else None
+                recv_w = src_b.view(torch.float32)[:, w_off // 4].contiguous() if w_elems else None
                 lo, hi = ch.lo, ch.hi
                 self._mark(sb)
-                kern.combine_reduce(MODE_EPILOGUE, recv[:, :hidden], combined_x[lo:hi], hi - lo, table=ch.table_b,
+                kern.combine_reduce(MODE_EPILOGUE, src_b[:, :hidden], combined_x[lo:hi], hi - lo, table=ch.table_b,
                                     row_weights=recv_w, bias0=bias_0[lo:hi] if bias_0 is not None else None,
                                     bias1=bias_1[lo:hi] if bias_1 is not None else None,
                                     wtable=ch.table_b if w_elems else None, wsrc=recv_w,
@@ -164,9 +186,8 @@ class ExchangeMixin:
                 self._mark(sb)
         if pipelined:
             stream.wait_stream(stream_b)
-            for _, recv, send, _ in in_flight:
-                recv.record_stream(stream_b)
-                send.record_stream(stream_b)
+            for _, _, rows, _ in in_flight:
+                rows.record_stream(stream_b)
 
     # ------------------------------------------------------------------ EP > 1 over xGMI windows
     def _window(self, row_bytes: int, slots: Optional[int] = None, rows_per_slot: Optional[int] = None):

@@ -26,8 +26,8 @@ from typing import List, Optional
 
 import torch
 
-from ._lib import (PLAN_BLOCK_TOKENS, PLAN_EXPANDED, PLAN_INTERLEAVE, PLAN_RANK_LAYOUT, PLAN_SINGLE,
-                   PLAN_WINDOW)
+from ._lib import (ERROR_RECORD_INTS, PLAN_BLOCK_TOKENS, PLAN_EXPANDED, PLAN_INTERLEAVE, PLAN_LOCAL_BYPASS,
+                   PLAN_RANK_LAYOUT, PLAN_SINGLE, PLAN_WINDOW, describe_error_record)
 from .utils import align, ceil_div
 
 
@@ -58,6 +58,7 @@ class ChunkPlan:
     table_b: torch.Tensor                    # source side: [hi - lo, min(R, K)] (multi) / [hi - lo, K] (single)
     wtable_b: Optional[torch.Tensor] = None  # source side: [hi - lo, K] weight index in the packed rows (multi)
     out_rows: Optional[torch.Tensor] = None  # xGMI transport, expert side: [n] window row address per unit
+    own: int = 0                             # RCCL local bypass: units (= receive rows) of this rank itself
 
 
 @dataclass
@@ -72,7 +73,36 @@ class CombinePlan:
     # EP > 1: the pipeline chunks (one or more)
     chunks: Optional[List[ChunkPlan]] = None
     window_row_bytes: int = 0
+    local_bypass: bool = False                        # RCCL: own units written in place (ChunkPlan.own)
     ready: Optional[tuple] = None                     # (stream, event) the tables were built on
+    # RCCL transport: the plan kernels' error record (a unit rejected because the counts disagree with the
+    # metadata or exceed the padding), copied to pinned host memory behind the build and checked by
+    # poll() at the plan's next use -- no host sync (the xGMI transport uses its window's record)
+    error_record: Optional[torch.Tensor] = None
+    _flag_host: Optional[torch.Tensor] = None
+    _flag_event: Optional[object] = None
+
+    def publish(self, stream) -> None:
+        if self.error_record is None or not self.error_record.is_cuda:
+            return
+        with torch.cuda.stream(stream):
+            self._flag_host = torch.zeros((ERROR_RECORD_INTS,), dtype=torch.int32, pin_memory=True)
+            self._flag_host.copy_(self.error_record, non_blocking=True)
+            self._flag_event = torch.cuda.Event()
+            self._flag_event.record(stream)
+
+    def poll(self) -> None:
+        """Raise (at every later use) once the published record shows a rejected plan entry: that
+        handle's combines are wrong -- the reference has no recovery either (its device asserts trap)."""
+        rec = None
+        if self.error_record is not None and not self.error_record.is_cuda:
+            rec = self.error_record.tolist()
+        elif self._flag_event is not None and self._flag_event.query():
+            rec = self._flag_host.tolist()
+        if rec is not None and rec[0]:
+            raise RuntimeError(f'deepep_amd: combine plan {describe_error_record(rec)}: the routing counts of '
+                               f'this handle disagree with its metadata or exceed the padding of a dispatch '
+                               f'without a CPU sync (a token routed twice to one expert?)')
 
 
 LINE_BYTES = 128      # a memory-side line: packed rows are whole lines (a partial line costs a read-modify-write)
@@ -104,13 +134,15 @@ def _chunk_sums(mat: List[List[int]], bpc: int, n_chunks: int) -> List[List[int]
 
 
 def build_ep_plan(kern, handle: 'EPHandle', *, num_ranks: int, rank: int, single: bool, num_chunks: int,
-                  hidden: int, window=None, stream=None) -> CombinePlan:
+                  hidden: int, window=None, stream=None, local_bypass: bool = True) -> CombinePlan:
     """The EP > 1 combine plan of `handle` on device tensors, with no host synchronisation.
 
     single: every valid expanded row travels unreduced (allow_multiple_reduction=False).
     window: the xGMI transport's SymmetricBuffer (rows go straight into the source ranks' windows)
     or None (RCCL all-to-all of packed rows).  hidden sizes the packed rows the weight tables
-    point into."""
+    point into.  local_bypass (RCCL): this rank's own partials skip the all-to-all (the default; off only
+    to measure what the bypass saves, DEEPEP_LOCAL_BYPASS=0)."""
+    bypass = local_bypass and window is None
     R, T_max = num_ranks, handle.num_max_tokens_per_rank
     T, K = handle.topk_idx.shape
     cnt = handle._counts
@@ -137,8 +169,12 @@ def build_ep_plan(kern, handle: 'EPHandle', *, num_ranks: int, rank: int, single
         units = _chunk_sums(cnt.recv_pairs if single else cnt.recv_tok, bpc, C)   # [c][source rank]
     n_units = [sum(u) for u in units]
     total = sum(n_units)
+    # RCCL: the local bypass -- this rank's own units are written by phase A straight into the receive rows
+    # phase B reads ([send rows | own rows | received rows], exchange._combine_chunks), so the all-to-all
+    # moves no diagonal; xGMI: units round-robin over the peers
     flags = ((PLAN_EXPANDED if expanded else 0) | (PLAN_SINGLE if single else 0) |
-             (PLAN_RANK_LAYOUT if rank_layout and not single else 0) | (PLAN_INTERLEAVE if window is not None else 0))
+             (PLAN_RANK_LAYOUT if rank_layout and not single else 0) |
+             (PLAN_INTERLEAVE if window is not None else 0) | (PLAN_LOCAL_BYPASS if bypass else 0))
     width_a = K if expanded and not single else 1
     # Pre-filled, so a unit the plan kernel does not write (counts that disagree with the metadata) is a
     # skipped slot (-1) and a null window row (0) -- never stale allocator bytes used as an address.
@@ -150,7 +186,8 @@ def build_ep_plan(kern, handle: 'EPHandle', *, num_ranks: int, rank: int, single
         out_rows = torch.full((total,), 1 if padded else 0, dtype=torch.int64, device=dev)
         bases, win_bytes, err = window.data_bases_dev, window.data_bytes, window.error_flag
     else:
-        row_bytes, out_rows, bases, win_bytes, err = 0, None, None, 0, None
+        row_bytes, out_rows, bases, win_bytes = 0, None, None, 0
+        err = torch.zeros((ERROR_RECORD_INTS,), dtype=torch.int32, device=dev)
     kern.plan_expert(handle.recv_src_metadata, K, R, rank, T_max, cnt.dev[2], cnt.dev[3], nb, bpc, flags,
                      table_a, wtable_a, bases, row_bytes, out_rows, window_bytes=win_bytes, error_flag=err,
                      padded_stride=padded, stream=stream)
@@ -171,12 +208,14 @@ def build_ep_plan(kern, handle: 'EPHandle', *, num_ranks: int, rank: int, single
         if max_rows * row_floats + w_off_f + K < 2 ** 31:
             wtable_b = torch.empty((T, K), dtype=torch.int32, device=dev)
     sflags = (PLAN_SINGLE if single else 0) | (PLAN_WINDOW if window is not None else 0) | \
+             (PLAN_LOCAL_BYPASS if bypass else 0) | \
              (PLAN_RANK_LAYOUT if rank_layout and not single else 0)
-    kern.plan_source(handle.topk_idx, handle.num_experts, R, T_max, handle.dst_buffer_slot_idx, cnt.dev[0],
+    kern.plan_source(handle.topk_idx, handle.num_experts, R, rank, T_max, handle.dst_buffer_slot_idx, cnt.dev[0],
                      cnt.dev[1], nb, bpc, sflags, row_floats, w_off_f, table_b, wtable_b,
                      padded_stride=padded if window is None else 0, stream=stream)
     plan = CombinePlan(num_ranks=R, num_tokens=T, num_topk=K, expanded=expanded, chunks=[],
-                       window_row_bytes=row_bytes)
+                       window_row_bytes=row_bytes, error_record=err if window is None else None,
+                       local_bypass=bypass)
     u0 = 0
     for c in range(C):
         lo, hi = min(c * bpc * PLAN_BLOCK_TOKENS, T), min((c + 1) * bpc * PLAN_BLOCK_TOKENS, T)
@@ -186,7 +225,8 @@ def build_ep_plan(kern, handle: 'EPHandle', *, num_ranks: int, rank: int, single
                                      (table_a[u0:u1] if expanded and not single else None),
                                      units[c], back[c], table_b[lo:hi],
                                      wtable_b[lo:hi] if wtable_b is not None else None,
-                                     out_rows[u0:u1] if out_rows is not None else None))
+                                     out_rows[u0:u1] if out_rows is not None else None,
+                                     units[c][rank] if bypass else 0))
         u0 = u1
     return plan
 

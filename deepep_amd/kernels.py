@@ -231,14 +231,14 @@ class HipKernels:
                                          _stream_handle(stream))
         _lib.check(rc, 'plan_expert')
 
-    def plan_source(self, topk_idx, num_experts, num_ranks, num_max_tokens, dst_slot, send_tok, send_pairs,
+    def plan_source(self, topk_idx, num_experts, num_ranks, rank, num_max_tokens, dst_slot, send_tok, send_pairs,
                     num_blocks, blocks_per_chunk, flags, row_floats, weights_offset, table_b, wtable,
                     padded_stride: int = 0, stream=None):
         _require(topk_idx.is_cuda and topk_idx.dtype == torch.int64 and topk_idx.is_contiguous(), 'topk_idx int64')
         _require(table_b.dtype == torch.int32 and table_b.is_contiguous(), 'table_b int32')
         _require(wtable is None or (wtable.dtype == torch.int32 and wtable.is_contiguous()), 'wtable int32')
         T, K = topk_idx.shape
-        rc = self.lib.deepep_plan_source(ptr(topk_idx), T, K, num_experts, num_ranks, num_max_tokens, ptr(dst_slot),
+        rc = self.lib.deepep_plan_source(ptr(topk_idx), T, K, num_experts, num_ranks, rank, num_max_tokens, ptr(dst_slot),
                                          ptr(send_tok), ptr(send_pairs), num_blocks, blocks_per_chunk, flags,
                                          row_floats, weights_offset, ptr(table_b), table_b.shape[1], ptr(wtable),
                                          int(padded_stride), _stream_handle(stream))

@@ -48,7 +48,7 @@ extern "C" {
 
 typedef struct ihipStream_t* deepep_stream_t;   /* == hipStream_t */
 
-#define DEEPEP_AMD_ABI_VERSION 13
+#define DEEPEP_AMD_ABI_VERSION 14
 
 #define DEEPEP_OK               0
 #define DEEPEP_ERR_INVALID_ARG  (-1)
@@ -145,41 +145,17 @@ int deepep_build_local_plan(const int32_t* src_metadata, int num_recv_tokens, in
                             deepep_stream_t stream);
 
 /*
- * Tuning / diagnostics (process-global; 0 or -1 = automatic, the default):
- *   vec_per_lane   16-byte vectors each lane loads per source row and item (1 or 2)
- *   stage_lds      1: stage the slot table / weights per workgroup in LDS; 0: per wave in registers
- *   store_policy   output store cache policy: 0 plain, 1 nt, 2 sc1 (write-through), 3 sc1 nt (the two
- *                  default shapes only: 8 x 8 rows in flight / 4 x 4), 4 per unit (sc1 when the unit
- *                  reduces >= 3 rows, else sc1 nt; phase A only, other modes: sc1).  Automatic: sc1 nt
- *                  for phase A, sc1 for the fused and epilogue reduces.
- *   rows_in_flight source rows each lane loads before accumulating them (2, 4 or 8; LDS staging with
- *                  sc1 or system-scope stores only).  Automatic: at most the slot table's width rounded
- *                  up to 2 / 4 / 8; 2 (with 1 vector per lane, 4-wave workgroups) for the fused reduce
- *                  over top-k >= 5, 8 for the epilogue, 4 for phase A (DEEPEP_MODE_LOCAL) and for every
- *                  launch on a CU-budget stream.
- * The results are identical for every configuration; only the speed changes.
+ * Tuning / diagnostics: vec_per_lane = 16-byte vectors each lane loads per source row and item (1 or 2),
+ * rows_in_flight = source rows each lane loads before accumulating them (2, 4 or 8); 0 = automatic, the
+ * default.  Process-wide, stored as one atomic word that every launch reads once.  Automatic shape: 2 KiB
+ * chunks (1 KiB for rows under 128 vectors); rows in flight at most the slot table's width rounded up to
+ * 2 / 4 / 8, and 2 (with 1 KiB chunks and 4-wave workgroups) for the fused reduce over top-k >= 5, 8 for
+ * the epilogue, 4 for phase A (DEEPEP_MODE_LOCAL) and for every launch on a CU-budget stream.  The store
+ * policy follows the output: sc1 nt for phase A's send rows, system scope for peer windows
+ * (deepep_combine_reduce_scatter), sc1 otherwise.  The results are identical for every configuration;
+ * only the speed changes.
  */
-int deepep_set_launch_config(int vec_per_lane, int stage_lds, int store_policy, int rows_in_flight);
-
-/*
- * Kernel for deepep_combine_reduce / _scatter when the shape is automatic (units_per_block 0, default
- * launch config), the slot table is at most 8 wide and hidden is a whole number of column chunks:
- *   0  the item kernel (one wave per (unit, column chunk));
- *   1  the streaming kernel (one wave per unit, the next chunk's rows loading while the current one
- *      is summed), 2 x 16 B per lane and row when hidden allows;
- *   2  the streaming kernel with 16 B per lane and row (half the registers, more waves per SIMD);
- *   3  the streaming kernel (as 1) on a persistent grid: as many workgroups as the chip holds at
- *      once, units strided over the waves;
- *   4  the item kernel with XCD-contiguous workgroup order (each of the 8 XCDs takes one
- *      contiguous eighth of the items; measured slower, so only when forced);
- *   5  the item kernel on a persistent grid (as many workgroups as the chip or the CU budget holds);
- *   6  the item kernel on its full grid (one workgroup per virtual block) even on a CU-budget stream,
- *      where the default is the persistent grid (the hardware keeps the workgroups on the budget);
- *  -1  (default) the item kernel.  Nothing is timed or synchronised inside a call.
- * All of them produce identical bits.  deepep_last_kernel_choice() says which one the last launch used.
- */
-int deepep_set_kernel_choice(int choice);
-int deepep_last_kernel_choice(void);
+int deepep_set_launch_config(int vec_per_lane, int rows_in_flight);
 
 /* ------------------------------------------------------------------ dispatch
  * Packed token row exchanged between ranks (byte offsets, all 16-byte aligned except as noted):
@@ -313,6 +289,7 @@ int deepep_dispatch_copy(const void* packed, int64_t row_bytes, int x_bytes, int
 #define DEEPEP_PLAN_INTERLEAVE   4    /* phase-A units round-robin over source ranks (xGMI stores)      */
 #define DEEPEP_PLAN_RANK_LAYOUT  8    /* receive slot = expert rank (R <= K), else the master lane        */
 #define DEEPEP_PLAN_WINDOW      16    /* source side: rows are window rows slot * T_max + t               */
+#define DEEPEP_PLAN_LOCAL_BYPASS 32   /* RCCL exchange without the own-rank diagonal (below)              */
 
 /* Sender side of the notify: tok_counts[r][b] = tokens of block b routed to rank r, pair_counts[r][b] =
  * (token, lane) entries of block b routed to r (blocks past num_tokens are zero). */
@@ -338,7 +315,14 @@ int deepep_route_block_counts(const int64_t* topk_idx, int num_tokens, int num_t
  * holds num_ranks * padded_stride unit positions starting at c * num_ranks * padded_stride; unit p of
  * source s sits at s * padded_stride + p (or p * num_ranks + s with DEEPEP_PLAN_INTERLEAVE).  The positions
  * no unit takes keep the caller's fill: -1 slots (a zero partial) and, for out_rows, the value 1, which
- * the scatter skips silently. */
+ * the scatter skips silently.  A unit p >= padded_stride of its source (more (token, lane) pairs on this
+ * rank than the padding allows) is rejected like a unit past its chunk, so it never lands in another
+ * source's positions.
+ * DEEPEP_PLAN_LOCAL_BYPASS (grouped order only): inside every chunk the groups follow the ranks in order
+ * except this rank's, which comes last -- [units of the other sources, rank order | units of `rank`] -- so
+ * the first part is an all-to-all input whose split for `rank` is 0 and the own units can be written
+ * straight into the receive rows deepep_plan_source lays out with the same flag (the reference's own
+ * receive slot is local memory, combine.cuh:96-101). */
 int deepep_plan_expert(const int32_t* src_metadata, int num_recv, int num_topk, int num_ranks, int rank,
                        int num_max_tokens, const int32_t* recv_tok, const int32_t* recv_pairs, int num_blocks,
                        int blocks_per_chunk, int flags, int32_t* table_a, int32_t* wtable_a,
@@ -354,9 +338,13 @@ int deepep_plan_expert(const int32_t* src_metadata, int num_recv, int num_topk, 
  * DEEPEP_PLAN_WINDOW, the window row slot * num_max_tokens + t.  Single reduction: table_b [T][K] = the
  * row of (t, k): receive-buffer order (expert rank, then (token, lane)) or window row k * T_max + t.
  * padded_stride > 0 (not with DEEPEP_PLAN_WINDOW): the receive buffer of a chunk is worst-case padded,
- * expert rank d's rows from d * padded_stride (the plan_expert layout above, after the exchange). */
+ * expert rank d's rows from d * padded_stride (the plan_expert layout above, after the exchange); a row
+ * past d's padded_stride rows (a unit plan_expert rejects) is -1.
+ * DEEPEP_PLAN_LOCAL_BYPASS (not with DEEPEP_PLAN_WINDOW): the chunk's receive rows are [rows from `rank`
+ * (phase A's own units, written in place) | rows received from the other ranks, rank order], i.e. the
+ * rows of `rank` come first. */
 int deepep_plan_source(const int64_t* topk_idx, int num_tokens, int num_topk, int num_experts, int num_ranks,
-                       int num_max_tokens, const int32_t* dst_slot, const int32_t* send_tok,
+                       int rank, int num_max_tokens, const int32_t* dst_slot, const int32_t* send_tok,
                        const int32_t* send_pairs, int num_blocks, int blocks_per_chunk, int flags,
                        int64_t row_floats, int64_t weights_offset, int32_t* table_b, int table_b_width,
                        int32_t* wtable, int padded_stride, deepep_stream_t stream);

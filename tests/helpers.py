@@ -74,6 +74,36 @@ def build_combine_inputs(fx, expert_alignment: int = 1):
     return ranks, per_rank
 
 
+def weighted_multi_expected(fx, rank: int, bias=(None, None)) -> np.ndarray:
+    """Expected bits of this build's gating-weighted combine with multiple reduction
+    (`combine(..., apply_topk_weights=True)` on an expanded handle) for rank `rank` of a fixture: the
+    oracle's restatement (oracle.combine_ep, weighted) -- on every expert rank an fp32 fma chain over the
+    token's local lanes from +0 (internode_ll.cu:704-711), rounded to bf16, then phase B over the
+    partials with the bias in front (combine_reduce_epilogue.cuh:62-125).  The reference has no such
+    two-level weighted recipe, so its bits are this build's definition; `exact_weighted` pins them to
+    the reference's tolerance.  bias: (bias0, bias1) bf16 bit arrays of this rank or None."""
+    from oracle import combine_ep
+    T, H, K, E, R = (int(v) for v in fx['meta'])
+    ranks, per = build_combine_inputs(fx)
+    biases = [(None, None)] * R
+    biases[rank] = bias
+    res = combine_ep([p['x_exp'] for p in per], [p['meta'] for p in per], [r['topk_idx'] for r in ranks], E, T,
+                     expanded=True, topk_weights_per_rank=[p['w_exp'] for p in per], bias_per_rank=biases,
+                     weighted=True)
+    return res[rank][0]
+
+
+def exact_weighted(me) -> np.ndarray:
+    """float64 sum over the valid top-k lanes of weight x expert row, [T, H] -- the reference's weighted
+    check compares combined_x with this exact value (tests/legacy/test_low_latency.py:178-181)."""
+    y = bf16_to_f32(me['y']).astype(np.float64)
+    w = np.where(me['topk_idx'] >= 0, me['topk_weights'], 0).astype(np.float64)
+    return (y * w[..., None]).sum(axis=1)
+
+
+WEIGHTED_TOLERANCE = 1e-5         # calc_diff bound of test_low_latency.py:178-181 (BF16 dispatch)
+
+
 def dispatch_mode_checks(buf, x, topk_idx, topk_weights, num_experts: int, num_max_tokens: int,
                          expert_alignment: int, do_cpu_sync: bool, do_handle_copy: bool) -> List[str]:
     """The dispatch-mode checks of the reference test (tests/elastic/test_ep.py:143-177, 355-466):

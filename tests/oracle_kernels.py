@@ -73,10 +73,10 @@ class OracleKernels:
                              blocks_per_chunk, flags, table_a, wtable_a, window_bases, window_row_bytes, out_rows,
                              padded=padded_stride)
 
-    def plan_source(self, topk_idx, num_experts, num_ranks, num_max_tokens, dst_slot, send_tok, send_pairs,
+    def plan_source(self, topk_idx, num_experts, num_ranks, rank, num_max_tokens, dst_slot, send_tok, send_pairs,
                     num_blocks, blocks_per_chunk, flags, row_floats, weights_offset, table_b, wtable,
                     padded_stride=0, stream=None):
-        plan_ref.plan_source(topk_idx, num_experts, num_ranks, num_max_tokens, dst_slot, send_tok, send_pairs,
+        plan_ref.plan_source(topk_idx, num_experts, num_ranks, rank, num_max_tokens, dst_slot, send_tok, send_pairs,
                              num_blocks, blocks_per_chunk, flags, row_floats, weights_offset, table_b, wtable,
                              padded=padded_stride)
 

@@ -23,7 +23,7 @@ build's, DESIGN.md section 5.
 import torch
 
 BLOCK = 64
-EXPANDED, SINGLE, INTERLEAVE, RANK_LAYOUT, WINDOW = 1, 2, 4, 8, 16
+EXPANDED, SINGLE, INTERLEAVE, RANK_LAYOUT, WINDOW, LOCAL_BYPASS = 1, 2, 4, 8, 16, 32
 
 
 def _rank_of(topk_idx: torch.Tensor, num_experts: int, num_ranks: int) -> torch.Tensor:
@@ -45,10 +45,27 @@ def route_block_counts(topk_idx, num_experts, num_ranks, num_blocks):
     return tok.to(torch.int32), pairs.to(torch.int32)
 
 
-def _positions(unit_src, unit_chunk, counts, R, interleave, padded=0):
+def send_order(l: int, rank: int, R: int, bypass: bool) -> int:
+    """Place of peer l's group in a chunk's send rows: rank order, or with the local bypass rank order
+    without `rank`, whose own units come last (include/deepep_amd.h, DEEPEP_PLAN_LOCAL_BYPASS)."""
+    if not bypass:
+        return l
+    return R - 1 if l == rank else (l - 1 if l > rank else l)
+
+
+def recv_order(l: int, rank: int, bypass: bool) -> int:
+    """Place of peer l's group in a chunk's receive rows: rank order, or with the local bypass `rank`'s
+    own rows first, then the other ranks in order."""
+    if not bypass:
+        return l
+    return 0 if l == rank else (l + 1 if l < rank else l)
+
+
+def _positions(unit_src, unit_chunk, counts, R, interleave, padded=0, rank=0, bypass=False):
     """Unit index of every unit (given in receive order) inside the concatenated chunk tables:
-    chunk base + position inside the chunk (grouped by source rank, or round-robin).  padded > 0:
-    every chunk holds R * padded positions, unit p of source s at s * padded + p (p * R + s)."""
+    chunk base + position inside the chunk (grouped by source rank in send_order, or round-robin).
+    padded > 0: every chunk holds R * padded positions, unit p of source s at send_order(s) * padded + p
+    (p * R + s); a unit p >= padded is rejected (-1: not stored)."""
     n = unit_src.numel()                                       # counts: [chunks, R]
     base = torch.cumsum(counts.sum(dim=1), 0) - counts.sum(dim=1)
     if padded:
@@ -63,12 +80,16 @@ def _positions(unit_src, unit_chunk, counts, R, interleave, padded=0):
     out = torch.empty(n, dtype=torch.int64)
     for i in range(n):
         c, s, pi = int(unit_chunk[i]), int(unit_src[i]), int(p[i])
+        if padded and pi >= padded:
+            out[i] = -1
+            continue
         if padded:
-            pos = pi * R + s if interleave else s * padded + pi
+            pos = pi * R + s if interleave else send_order(s, rank, R, bypass) * padded + pi
         elif interleave:
             pos = sum(min(int(counts[c, l]), pi + (1 if l < s else 0)) for l in range(R))
         else:
-            pos = int(counts[c, :s].sum()) + pi
+            os_ = send_order(s, rank, R, bypass)
+            pos = sum(int(counts[c, l]) for l in range(R) if send_order(l, rank, R, bypass) < os_) + pi
         out[i] = int(base[c]) + pos
     return out
 
@@ -77,6 +98,7 @@ def plan_expert(meta, num_topk, num_ranks, rank, num_max_tokens, recv_tok, recv_
                 blocks_per_chunk, flags, table_a, wtable_a, window_bases, window_row_bytes, out_rows, padded=0):
     K, R, T_max, bpc = num_topk, num_ranks, num_max_tokens, blocks_per_chunk
     single, expanded = bool(flags & SINGLE), bool(flags & EXPANDED)
+    bypass = bool(flags & LOCAL_BYPASS) and not flags & INTERLEAVE
     n_recv = int(recv_tok.sum())
     m = meta[:n_recv].long()
     src = torch.div(m[:, 1], K, rounding_mode='floor')
@@ -87,7 +109,9 @@ def plan_expert(meta, num_topk, num_ranks, rank, num_max_tokens, recv_tok, recv_
     counts = torch.stack([cnt[:, c * bpc:(c + 1) * bpc].sum(dim=1) for c in range(C)])    # [C, R]
     if single:
         ii, kk = (m[:, 2:] >= 0).nonzero(as_tuple=True)         # (row, lane) order
-        u = _positions(src[ii], chunk[ii], counts, R, bool(flags & INTERLEAVE), padded)
+        u = _positions(src[ii], chunk[ii], counts, R, bool(flags & INTERLEAVE), padded, rank, bypass)
+        keep = u >= 0
+        u, ii, kk = u[keep], ii[keep], kk[keep]
         table_a[u, 0] = m[ii, 2 + kk].to(torch.int32)
         if out_rows is not None:
             bases = window_bases.long().cpu()
@@ -95,7 +119,7 @@ def plan_expert(meta, num_topk, num_ranks, rank, num_max_tokens, recv_tok, recv_
             addr = bases[src[ii].clamp(0, R - 1)] + (kk * T_max + st[ii]) * window_row_bytes
             out_rows[u] = torch.where(ok, addr, torch.zeros_like(addr)).to(out_rows.dtype)
         return
-    u = _positions(src, chunk, counts, R, bool(flags & INTERLEAVE), padded)
+    u = _positions(src, chunk, counts, R, bool(flags & INTERLEAVE), padded, rank, bypass)
     rows = torch.arange(n_recv)
     if expanded:
         table_a[u] = m[:, 2:2 + K].to(torch.int32)
@@ -111,12 +135,20 @@ def plan_expert(meta, num_topk, num_ranks, rank, num_max_tokens, recv_tok, recv_
         out_rows[u] = torch.where(ok, addr, torch.zeros_like(addr)).to(out_rows.dtype)
 
 
-def plan_source(topk_idx, num_experts, num_ranks, num_max_tokens, dst_slot, send_tok, send_pairs, num_blocks,
+def plan_source(topk_idx, num_experts, num_ranks, rank, num_max_tokens, dst_slot, send_tok, send_pairs, num_blocks,
                 blocks_per_chunk, flags, row_floats, weights_offset, table_b, wtable, padded=0):
     """Per owned token, from the routing alone (running counters, not dst_slot)."""
     T, K = topk_idx.shape
     R, T_max, bpc = num_ranks, num_max_tokens, blocks_per_chunk
     single, window, rank_layout = bool(flags & SINGLE), bool(flags & WINDOW), bool(flags & RANK_LAYOUT)
+    bypass = bool(flags & LOCAL_BYPASS) and not window
+
+    def base(c, d):
+        """First row of expert rank d's group in chunk c's receive rows (recv_order)."""
+        o = recv_order(d, rank, bypass)
+        if padded:
+            return o * padded
+        return sum(int(counts[c, l]) for l in range(R) if recv_order(l, rank, bypass) < o)
     rank_of = _rank_of(topk_idx.long().cpu(), num_experts, R)
     C = (num_blocks + bpc - 1) // bpc
     cnt = (send_pairs if single else send_tok).long().cpu()
@@ -135,7 +167,8 @@ def plan_source(topk_idx, num_experts, num_ranks, num_max_tokens, dst_slot, send
                 if window:
                     tb[t, k] = k * T_max + t
                 else:
-                    tb[t, k] = (d * padded if padded else int(counts[c, :d].sum())) + int(running[c, d])
+                    ok = not padded or int(running[c, d]) < padded     # past d's padded rows: rejected
+                    tb[t, k] = base(c, d) + int(running[c, d]) if ok else -1
                     running[c, d] += 1
             continue
         master = {d: k for k, d in enumerate(ranks) if d >= 0}            # highest lane wins
@@ -144,7 +177,7 @@ def plan_source(topk_idx, num_experts, num_ranks, num_max_tokens, dst_slot, send
             if window:
                 row[d] = (d if rank_layout else mk) * T_max + t
             else:
-                row[d] = (d * padded if padded else int(counts[c, :d].sum())) + int(running[c, d])
+                row[d] = base(c, d) + int(running[c, d])
                 running[c, d] += 1
         for j, d in enumerate(sorted(master, key=lambda d: master[d])[:width]):
             tb[t, j] = row[d]

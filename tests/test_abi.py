@@ -33,7 +33,7 @@ def test_exports_every_declared_symbol(lib):
 
 
 def test_abi_version(lib):
-    assert lib.deepep_amd_abi_version() == 13
+    assert lib.deepep_amd_abi_version() == 14
 
 
 def test_build_id_matches_sources(lib):
@@ -69,16 +69,12 @@ def test_invalid_arguments_are_rejected_without_a_gpu(lib):
     # zero units: nothing to do, success without a launch
     assert lib.deepep_combine_reduce(1, 0, 16, 1, 8, None, 0, 1, None, None, None, 48, 8, 0, 8,
                                      None, 0, None, None, 0, 0, 0, 0, None, None) == 0
-    # kernel choice: -1 (default: the item kernel), 0-6; anything else is rejected with a message
-    assert lib.deepep_set_kernel_choice(7) == -1 and b'kernel choice' in lib.deepep_amd_last_error()
-    assert lib.deepep_set_kernel_choice(-2) == -1
-    for c in (0, 1, 2, 3, 4, 5, 6, -1):
-        assert lib.deepep_set_kernel_choice(c) == 0
-    assert lib.deepep_last_kernel_choice() in (0, 1, 2, 3, 4, 5, 6)
-    # launch configuration knobs out of range
-    assert lib.deepep_set_launch_config(3, -1, -1, 0) == -1
-    assert lib.deepep_set_launch_config(0, -1, -1, 3) == -1
-    assert lib.deepep_set_launch_config(0, -1, -1, 0) == 0
+    # launch configuration knobs out of range (vectors per lane 0-2, rows in flight 0 / 2 / 4 / 8)
+    assert lib.deepep_set_launch_config(3, 0) == -1 and b'launch configuration' in lib.deepep_amd_last_error()
+    assert lib.deepep_set_launch_config(0, 3) == -1
+    assert lib.deepep_set_launch_config(-1, 0) == -1
+    assert lib.deepep_set_launch_config(2, 8) == 0
+    assert lib.deepep_set_launch_config(0, 0) == 0
     # EP > 1 plan builders: rank out of range, too few blocks, wrong table width, single w/o expanded
     assert lib.deepep_plan_expert(16, 4, 8, 8, 8, 64, 16, 16, 1, 1, 1, 16, None, None, 0, 0, None, None,
                                   0, None) == -1
@@ -97,10 +93,12 @@ def test_invalid_arguments_are_rejected_without_a_gpu(lib):
     assert lib.deepep_combine_reduce_scatter(0, 16, 4, 64, None, 0, 1, None, 32, 4, 64, None, 0, None, 0, 0, 0,
                                              48, 1, 64, None, None) == -1
     # dispatch pack: negative destination rows
-    assert lib.deepep_plan_source(16, 200, 8, 64, 8, 256, 16, 16, 16, 1, 1, 0, 0, 0, 16, 8, None, 0, None) == -1
-    assert lib.deepep_plan_source(16, 64, 8, 64, 8, 256, 16, 16, 16, 1, 1, 0, 0, 0, 16, 7, None, 0, None) == -1
+    assert lib.deepep_plan_source(16, 200, 8, 64, 8, 0, 256, 16, 16, 16, 1, 1, 0, 0, 0, 16, 8, None, 0, None) == -1
+    assert lib.deepep_plan_source(16, 64, 8, 64, 8, 0, 256, 16, 16, 16, 1, 1, 0, 0, 0, 16, 7, None, 0, None) == -1
+    # rank outside [0, num_ranks)
+    assert lib.deepep_plan_source(16, 64, 8, 64, 8, 8, 256, 16, 16, 16, 1, 1, 0, 0, 0, 16, 8, None, 0, None) == -1
     # a padded stride with window rows (the window layout is never padded)
-    assert lib.deepep_plan_source(16, 64, 8, 64, 8, 256, 16, 16, 16, 4, 1, 16, 0, 0, 16, 8, None, 64, None) == -1
+    assert lib.deepep_plan_source(16, 64, 8, 64, 8, 0, 256, 16, 16, 16, 4, 1, 16, 0, 0, 16, 8, None, 64, None) == -1
     assert lib.deepep_dispatch_pack(16, 64, 64, None, 0, 0, 32, None, 4, 2, 0, 48, 64, 2, 80, None, 128, -1,
                                     64, 64, 96, 112, None, None) == -1
     assert lib.deepep_route_block_counts(16, 200, 8, 64, 8, 1, 16, 16, None) == -1

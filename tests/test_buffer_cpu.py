@@ -18,7 +18,8 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from tests.helpers import load, ordered_accumulate, ranks_of
+from tests.helpers import (WEIGHTED_TOLERANCE, exact_weighted, load, ordered_accumulate, ranks_of,
+                           weighted_multi_expected)
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -125,6 +126,19 @@ def _worker(rank, world, port, fixture, queue, env=None):
                         failures.append(f'expanded combine b{nb}')
                     if not torch.equal(out_w, topk_w):
                         failures.append(f'expanded weights b{nb}')
+                    # gating-weighted with multiple reduction (the N > 1 bench recipe): bitwise vs the oracle's
+                    # restatement, and within the reference's weighted tolerance of the exact sum
+                    out, out_w, _ = buf.combine(x_exp, ex_handle, topk_weights=ex_w, bias=bias,
+                                                apply_topk_weights=True)
+                    bias_u16 = (None, None) if nb == 0 else (me['bias0'], me['bias1'] if nb == 2 else None)
+                    if not np.array_equal(_bf16_to_u16(out), weighted_multi_expected(fx, rank, bias_u16)):
+                        failures.append(f'weighted multi-reduction combine b{nb}')
+                    if not torch.equal(out_w, topk_w):
+                        failures.append(f'weighted multi-reduction weights b{nb}')
+                    if nb == 0:
+                        d = oracle.calc_diff(oracle.bf16_to_f32(_bf16_to_u16(out)), exact_weighted(me))
+                        if not d < WEIGHTED_TOLERANCE:
+                            failures.append(f'weighted multi-reduction calc_diff {d} >= {WEIGHTED_TOLERANCE}')
                 else:
                     out, out_w, _ = buf.combine(x_exp, ex_handle, bias=bias)
                     if not np.array_equal(_bf16_to_u16(out), me[f'combined_single_b{nb}']):

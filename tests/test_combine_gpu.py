@@ -18,7 +18,8 @@ import pytest
 import torch
 
 import oracle
-from tests.helpers import load, ordered_accumulate, ranks_of
+from tests.helpers import (WEIGHTED_TOLERANCE, exact_weighted, load, ordered_accumulate, ranks_of,
+                           weighted_multi_expected)
 from tests.oracle_kernels import OracleKernels
 
 pytestmark = pytest.mark.gpu
@@ -123,13 +124,11 @@ def test_kernel_units_per_block(kern, upb):
     _run(kern, MODE_LOCAL, True, 53, 8, 7168, 0, seed=upb + 1, upb=upb, wt=False)
 
 
-@pytest.mark.parametrize('cfg', [(1, 0, 0, 0), (1, 1, 1, 0), (2, 0, 1, 0), (2, 1, 0, 0), (2, 0, 2, 0), (0, -1, -1, 0),
-                                 (0, -1, -1, 2), (0, -1, -1, 4), (1, 1, 2, 2), (2, 1, 3, 4), (0, -1, 4, 0),
-                                 (2, 1, 2, 8)])
+@pytest.mark.parametrize('cfg', [(1, 0), (2, 0), (0, 2), (0, 4), (0, 8), (1, 2), (1, 8), (2, 2), (2, 4)])
 @pytest.mark.parametrize('upb', [0, 4, 8])
 def test_kernel_launch_configs_identical(kern, cfg, upb):
-    """Every deepep_set_launch_config variant (vector width, LDS staging, store policy, rows in
-    flight) and workgroup shape gives the same bits (the tuning knobs of tools/kbench.py)."""
+    """Every deepep_set_launch_config variant (vectors per lane, rows in flight) and workgroup shape
+    gives the same bits (the tuning knobs of tools/kshapes.py)."""
     assert kern.lib.deepep_set_launch_config(*cfg) == 0
     try:
         for mode in (MODE_LOCAL, MODE_EPILOGUE, MODE_FUSED):
@@ -139,7 +138,7 @@ def test_kernel_launch_configs_identical(kern, cfg, upb):
             _run(kern, mode, True, 29, 17, 520, 0 if mode == MODE_LOCAL else 2, seed=sum(cfg) + 10 + 5 * mode,
                  upb=upb)                                                       # > 8 valid rows
     finally:
-        kern.lib.deepep_set_launch_config(0, -1, -1, 0)
+        kern.lib.deepep_set_launch_config(0, 0)
 
 
 @pytest.mark.parametrize('weighted,hidden', [(False, 7168), (True, 520), (False, 64)])
@@ -182,8 +181,8 @@ def test_kernel_poisoned_by_timed_out_barrier(kern):
     rng = np.random.default_rng(3)
     src = _bf16(_random_rows(rng, 64, 1024))
     table = torch.randint(0, 64, (16, 8), dtype=torch.int32, device='cuda')
-    for flag, choice in ((2, 0), (3, 1), (2, 3)):
-        assert kern.lib.deepep_set_kernel_choice(choice) == 0
+    for flag, cfg in ((2, (0, 0)), (3, (1, 2)), (2, (2, 8))):
+        assert kern.lib.deepep_set_launch_config(*cfg) == 0
         try:
             err = torch.zeros((8,), dtype=torch.int32, device='cuda')
             err[0] = flag
@@ -197,7 +196,7 @@ def test_kernel_poisoned_by_timed_out_barrier(kern):
             assert bool(torch.isnan(out.float()).all()), flag
             assert int(win.count_nonzero()) == 0, flag
         finally:
-            kern.lib.deepep_set_kernel_choice(-1)
+            kern.lib.deepep_set_launch_config(0, 0)
     err = torch.ones((1,), dtype=torch.int32, device='cuda')
     out = torch.zeros((16, 1024), dtype=torch.bfloat16, device='cuda')
     kern.combine_reduce(MODE_FUSED, src, out, 16, table=table, error_flag=err)
@@ -207,24 +206,24 @@ def test_kernel_poisoned_by_timed_out_barrier(kern):
     assert torch.equal(out, ref)
 
 
-@pytest.mark.parametrize('choice', [0, 1, 5])
-def test_kernel_weights_pad_fills_the_tail_line(kern, choice):
+@pytest.mark.parametrize('cfg', [(0, 0), (1, 2), (2, 8)])
+def test_kernel_weights_pad_fills_the_tail_line(kern, cfg):
     """weights_pad: each unit's weight row is written as weights_pad floats (the weights, then zeros) --
     a packed row's whole 128-byte tail line -- and nothing past it."""
-    rng = np.random.default_rng(choice)
+    rng = np.random.default_rng(sum(cfg))
     units, K, H = 23, 8, 1024
     src = _bf16(_random_rows(rng, units * K, H))
     table = torch.from_numpy(rng.integers(0, units * K, size=(units, K)).astype(np.int32)).cuda()
     wsrc = torch.rand(units * K, device='cuda')
     packed = torch.full((units, H + 128), 7.0, dtype=torch.bfloat16, device='cuda')
     ow = packed.view(torch.float32)[:, H // 2:H // 2 + K]
-    assert kern.lib.deepep_set_kernel_choice(choice) == 0
+    assert kern.lib.deepep_set_launch_config(*cfg) == 0
     try:
         kern.combine_reduce(MODE_LOCAL, src, packed[:, :H], units, table=table, wtable=table, wsrc=wsrc,
                             out_weights=ow, weights_pad=32)
         torch.cuda.synchronize()
     finally:
-        kern.lib.deepep_set_kernel_choice(-1)
+        kern.lib.deepep_set_launch_config(0, 0)
     tail = packed.view(torch.float32)[:, H // 2:]
     assert torch.equal(tail[:, :K], wsrc[table.long()])
     assert bool((tail[:, K:32] == 0).all())
@@ -323,6 +322,20 @@ def _buffer_case(rank, world, fixture, comm, results):
                     failures.append(f'{tag} b{nb}')
                 if not torch.equal(out_w.cpu(), torch.from_numpy(me['topk_weights'])):
                     failures.append(f'{tag} weights b{nb}')
+            # gating-weighted with multiple reduction (the N > 1 bench recipe): bitwise vs the oracle's
+            # restatement, and within the reference's weighted tolerance (calc_diff < 1e-5,
+            # test_low_latency.py:178-181) of the exact float64 sum
+            out, out_w, _ = buf.combine(x_exp, ex_handle, topk_weights=ex_w, bias=bias, apply_topk_weights=True)
+            torch.cuda.synchronize()
+            bias_u16 = (None, None) if nb == 0 else (me['bias0'], me['bias1'] if nb == 2 else None)
+            if not np.array_equal(_u16(out), weighted_multi_expected(fx, rank, bias_u16)):
+                failures.append(f'weighted multi-reduction b{nb}')
+            if not torch.equal(out_w.cpu(), torch.from_numpy(me['topk_weights'])):
+                failures.append(f'weighted multi-reduction weights b{nb}')
+            if nb == 0:
+                d = oracle.calc_diff(oracle.bf16_to_f32(_u16(out)), exact_weighted(me))
+                if not d < WEIGHTED_TOLERANCE:
+                    failures.append(f'weighted multi-reduction calc_diff {d} >= {WEIGHTED_TOLERANCE}')
         # allow_multiple_reduction=False: every expanded row travels unreduced, one reduction at the
         # source rank -- plain (refs.combine single-level fixtures) and gating-weighted (legacy
         # low-latency fma chain, bias in front)
@@ -408,17 +421,15 @@ def test_config2_full_size_bitwise(weighted, T, skew):
     ref, _ = oracle.phase_b(recv, None, idx.cpu().numpy(), E, 1, True, True)
     lib = buf.kernels.lib
     try:
-        # the item kernel, the streaming kernel (2 and 1 vectors per lane, persistent), XCD order, persistent,
-        # full grid, default
-        for choice in (0, 1, 2, 3, 4, 5, 6, -1):
-            assert lib.deepep_set_kernel_choice(choice) == 0
+        # the automatic shape (last) and the other launch shapes (vectors per lane, rows in flight)
+        for cfg in ((1, 2), (1, 8), (2, 4), (2, 8), (0, 0)):
+            assert lib.deepep_set_launch_config(*cfg) == 0
             out, out_w, _ = buf.combine(y, handle, topk_weights=ex_w, apply_topk_weights=weighted)
             torch.cuda.synchronize()
-            assert lib.deepep_last_kernel_choice() == (choice if choice >= 0 else 0)
-            assert np.array_equal(_u16(out), ref), f'kernel choice {choice}'
+            assert np.array_equal(_u16(out), ref), f'launch config {cfg}'
             assert torch.equal(out_w, w)
     finally:
-        lib.deepep_set_kernel_choice(-1)
+        lib.deepep_set_launch_config(0, 0)
     if weighted:
         # and within the reference's weighted tolerance of the exact sum (test_low_latency.py:178-181)
         yd = y.double()

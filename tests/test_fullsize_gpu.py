@@ -3,7 +3,9 @@
 dispatch and the pipelined (4-chunk) combine.
 
   C3  8 x 8192 tokens, hidden 7168, top-8, 256 experts, uniform routing: plain + bias, and the
-      gating-weighted combine (apply_topk_weights)
+      gating-weighted combine (apply_topk_weights: bitwise vs the oracle AND calc_diff < 1e-5 against the
+      exact float64 sum on every rank, the reference's weighted tolerance); and both again with 10 %
+      masked top-k slots and ragged batches (8192 - rank tokens)
   C4  the same with the FP8 dispatch (per-128 e4m3 + fp32 scales) chained into the BF16 combine:
       every expanded FP8 row is checked against its source token, the dequantised rows are the
       expert outputs the combine reduces
@@ -31,12 +33,20 @@ def _u16(t: torch.Tensor) -> np.ndarray:
     return t.detach().cpu().contiguous().view(torch.int16).numpy().view(np.uint16)
 
 
-def _rank(rank, world, T, H, K, E, skew, fp8, weighted, comm, shared, results):
+def _calc_diff(a: torch.Tensor, b: torch.Tensor) -> float:
+    """deep_ep/utils/math.py:5-9, in float64 on the GPU."""
+    a, b = a.double() + 1, b.double() + 1
+    return float(1 - 2 * (a * b).sum() / (a * a + b * b).sum())
+
+
+def _rank(rank, world, T_max, H, K, E, skew, fp8, weighted, masked, ragged, comm, shared, results):
     try:
         torch.cuda.set_device(0)
         from deepep_amd import ElasticBuffer
         from workloads import get_unbalanced_scores, per_token_cast_back, per_token_cast_to_fp8
         g = torch.Generator(device='cuda').manual_seed(4242 + rank)
+        # ragged: rank r holds T_max - r tokens (the reference's test, tests/elastic/test_ep.py:62)
+        T = T_max - rank if ragged else T_max
         if skew != 1.0:
             with comm.lock:                                   # the bisection uses torch's global generator
                 torch.manual_seed(4242 + rank)
@@ -45,10 +55,14 @@ def _rank(rank, world, T, H, K, E, skew, fp8, weighted, comm, shared, results):
             scores = torch.rand((T, E), device='cuda', generator=g)
         w, idx = torch.topk(scores, K, dim=-1, sorted=False)
         idx = idx.to(torch.int64).contiguous()
+        if masked:
+            # --masked-ratio (tests/elastic/test_ep.py:78-81): a share of the top-k slots -1, their weights 0
+            idx.masked_fill_(torch.rand(idx.shape, device='cuda', generator=g) < masked, -1)
+            w = w.masked_fill(idx < 0, 0)
         w = w.contiguous()
         x = torch.randn((T, H), device='cuda', generator=g).to(torch.bfloat16)
         bias = torch.randn((T, H), device='cuda', generator=g).to(torch.bfloat16)
-        buf = ElasticBuffer(FakeGroup(rank, world, comm), num_max_tokens_per_rank=T, hidden=H, num_topk=K)
+        buf = ElasticBuffer(FakeGroup(rank, world, comm), num_max_tokens_per_rank=T_max, hidden=H, num_topk=K)
         comm.install(buf, rank)
         failures = []
         if fp8:
@@ -87,9 +101,10 @@ def _rank(rank, world, T, H, K, E, skew, fp8, weighted, comm, shared, results):
         S = np.arange(T)
         pos = np.arange(T, dtype=np.int64)
         x_sub, m_sub, w_sub = [], [], []
+        exact = torch.zeros((T, H), dtype=torch.float64, device='cuda') if weighted else None
         for r in range(world):
             m = shared[r]['meta']
-            sel = (m[:, 0] // T == rank) & (pos[m[:, 0] % T] >= 0)
+            sel = m[:, 0] // T_max == rank
             mr = m[sel].copy()
             slots = mr[:, 2:]
             valid = slots >= 0
@@ -99,8 +114,14 @@ def _rank(rank, world, T, H, K, E, skew, fp8, weighted, comm, shared, results):
             new = np.full(slots.shape, -1, np.int32)
             new[valid] = np.arange(int(valid.sum()), dtype=np.int32)
             mr[:, 2:] = new
-            mr[:, 0] = rank * n_s + pos[mr[:, 0] % T]
+            mr[:, 0] = rank * n_s + pos[mr[:, 0] % T_max]
             m_sub.append(mr)
+            if weighted:
+                # the exact float64 gating-weighted sum of every token over all its expert ranks' rows
+                tok = np.broadcast_to((m[sel, 0] % T_max)[:, None], slots.shape)[valid]
+                if src_rows.numel():
+                    exact.index_add_(0, torch.from_numpy(tok.astype(np.int64)).cuda(),
+                                     shared[r]['y'][src_rows].double() * shared[r]['ex_w'][src_rows].double()[:, None])
         bias_sub = (_u16(b[torch.from_numpy(S).cuda()]) if b is not None else None, None)
         exp, exp_w = oracle.combine_ep_one(rank, x_sub, m_sub, shared[rank]['idx'][S], E, n_s, expanded=True,
                                            topk_weights_per_rank=w_sub, bias=bias_sub, weighted=weighted,
@@ -112,6 +133,16 @@ def _rank(rank, world, T, H, K, E, skew, fp8, weighted, comm, shared, results):
         shared[('full_checked', rank)] = got.shape[0]
         if not np.array_equal(exp_w, w.cpu().numpy()[S]):
             failures.append('oracle weights of the sample')
+        if weighted:
+            # the reference's weighted tolerance (tests/legacy/test_low_latency.py:178-181): calc_diff < 1e-5
+            # against the exact sum, on every rank's whole output
+            d = _calc_diff(out.double(), exact)
+            shared[('calc_diff', rank)] = d
+            if not d < 1e-5:
+                failures.append(f'calc_diff {d:.3g} >= 1e-5 vs the exact float64 weighted sum')
+            del exact
+            if bool(torch.isnan(out.float()).any()):
+                failures.append('NaN in combined_x')
         comm.bar.wait()
         results[rank] = failures
     except Exception:
@@ -120,7 +151,7 @@ def _rank(rank, world, T, H, K, E, skew, fp8, weighted, comm, shared, results):
         comm.bar.abort()
 
 
-def _run(T, skew=1.0, fp8=False, weighted=False):
+def _run(T, skew=1.0, fp8=False, weighted=False, masked=0.0, ragged=False):
     import threading
     world, H, K, E = 8, 7168, 8, 256
     torch.cuda.init()                                   # not lazily from 8 threads at once
@@ -128,19 +159,32 @@ def _run(T, skew=1.0, fp8=False, weighted=False):
     comm = ThreadComm(world)
     comm.lock = threading.Lock()
     shared = {}
-    results = run_threads(world, _rank, (world, T, H, K, E, skew, fp8, weighted, comm, shared), timeout=600)
+    results = run_threads(world, _rank, (world, T, H, K, E, skew, fp8, weighted, masked, ragged, comm, shared),
+                          timeout=600)
     full = [shared.get(('full_checked', r)) for r in range(world)]
+    diffs = [shared.get(('calc_diff', r)) for r in range(world)]
     del shared
     torch.cuda.empty_cache()
     assert len(results) == world, results
     bad = {r: f for r, f in results.items() if f}
     assert not bad, bad
-    assert full == [T] * world, f'tokens checked per rank {full}, expected {T} each'
+    want = [T - r if ragged else T for r in range(world)]
+    assert full == want, f'tokens checked per rank {full}, expected {want}'
+    if weighted:
+        assert all(d is not None and d < 1e-5 for d in diffs), diffs
+        print(f'calc_diff per rank vs the exact weighted sum: {["%.2e" % d for d in diffs]}')
 
 
 @pytest.mark.parametrize('weighted', [False, True], ids=['plain_bias', 'gating_weighted'])
 def test_config3_ep8_8192_tokens(weighted):
     _run(8192, weighted=weighted)
+
+
+@pytest.mark.parametrize('weighted', [False, True], ids=['plain_bias', 'gating_weighted'])
+def test_config3_ep8_masked_ragged(weighted):
+    """Config 3 with 10 % of the top-k slots masked (-1, weight 0; the reference's --masked-ratio) and
+    ragged batches (rank r holds 8192 - r tokens of T_max = 8192, the reference's num_tokens)."""
+    _run(8192, weighted=weighted, masked=0.1, ragged=True)
 
 
 def test_config4_ep8_fp8_dispatch_bf16_combine():

@@ -36,17 +36,15 @@ def _case(seed: int):
     return rng, T, H, K, E, masked
 
 
-@pytest.fixture(params=[0, 1, 2, 3, 4, 5], ids=['item', 'stream', 'stream_vpt1', 'stream_persistent', 'item_xcd',
-                                                'item_persistent'])
+@pytest.fixture(params=[(0, 0), (1, 8), (2, 2)], ids=['auto', 'vpt1_rows8', 'vpt2_rows2'])
 def kernel_choice(request):
-    """Every combine kernel (deepep_set_kernel_choice): the item kernel and the streaming kernel at 2 and 1
-    vectors per lane and on a persistent grid, and the item kernel in XCD-contiguous order and on a
-    persistent grid."""
+    """The automatic launch shape and two forced ones (deepep_set_launch_config: vectors per lane, rows in
+    flight): every shape gives the same bits."""
     from deepep_amd import _lib
     lib = _lib.load()
-    assert lib.deepep_set_kernel_choice(request.param) == 0
+    assert lib.deepep_set_launch_config(*request.param) == 0
     yield request.param
-    lib.deepep_set_kernel_choice(-1)
+    lib.deepep_set_launch_config(0, 0)
 
 
 @pytest.fixture(scope='module')

@@ -87,57 +87,65 @@ def test_plan_kernels_match_reference(kern, world, K, T, chunks):
         tok_all.append(rt)
         pairs_all.append(rp)
     bases = torch.tensor([(1 << 40) * (s + 1) for s in range(world)], dtype=torch.int64)
+    epr = E // world
+    C = (nb + bpc - 1) // bpc
     for r in range(world):
         meta = torch.from_numpy(disp[r]['src_metadata']).cuda()
         recv_tok = torch.stack([tok_all[s][r] for s in range(world)])        # [source, block]
         recv_pairs = torch.stack([pairs_all[s][r] for s in range(world)])
         for single in (False, True):
             for expanded in ((True,) if single else (True, False)):
-                for window in (False, True):
-                    flags = ((_lib.PLAN_EXPANDED if expanded else 0) | (_lib.PLAN_SINGLE if single else 0) |
-                             (_lib.PLAN_RANK_LAYOUT if world <= K and not single else 0) |
-                             (_lib.PLAN_INTERLEAVE if window else 0))
-                    total = int((recv_pairs if single else recv_tok).sum())
-                    width = K if expanded and not single else 1
-                    outs = []
-                    for dev in ('cuda', 'cpu'):
-                        ta = torch.full((total, width), -7, dtype=torch.int32, device=dev)
-                        wa = torch.full((total, K), -7, dtype=torch.int32, device=dev) if not expanded else None
-                        orow = torch.full((total,), -7, dtype=torch.int64, device=dev) if window else None
-                        args = (K, world, r, T, recv_tok.to(dev), recv_pairs.to(dev), nb, bpc, flags, ta, wa,
-                                bases.to(dev) if window else None, 14400 if window else 0, orow)
-                        if dev == 'cuda':
-                            kern.plan_expert(meta, *args, window_bytes=K * T * 14400 if window else 0)
-                        else:
-                            plan_ref.plan_expert(meta.cpu(), *args)
-                        outs.append([t.cpu() if t is not None else None for t in (ta, wa, orow)])
-                    for g, c, name in zip(outs[0], outs[1], ('table_a', 'wtable_a', 'out_rows')):
-                        assert (g is None) == (c is None)
-                        assert g is None or torch.equal(g, c), (r, single, expanded, window, name)
+                # (transport, padded): RCCL with and without the local bypass, xGMI windows; exact counts and
+                # the worst-case padding of a dispatch without a CPU sync
+                for window, bypass in ((False, False), (False, True), (True, False)):
+                    for padded in (0, bpc * 64 * (min(K, epr) if single else 1)):
+                        flags = ((_lib.PLAN_EXPANDED if expanded else 0) | (_lib.PLAN_SINGLE if single else 0) |
+                                 (_lib.PLAN_RANK_LAYOUT if world <= K and not single else 0) |
+                                 (_lib.PLAN_INTERLEAVE if window else 0) | (_lib.PLAN_LOCAL_BYPASS if bypass else 0))
+                        total = C * world * padded if padded else int((recv_pairs if single else recv_tok).sum())
+                        width = K if expanded and not single else 1
+                        outs = []
+                        for dev in ('cuda', 'cpu'):
+                            ta = torch.full((total, width), -7, dtype=torch.int32, device=dev)
+                            wa = torch.full((total, K), -7, dtype=torch.int32, device=dev) if not expanded else None
+                            orow = torch.full((total,), -7, dtype=torch.int64, device=dev) if window else None
+                            args = (K, world, r, T, recv_tok.to(dev), recv_pairs.to(dev), nb, bpc, flags, ta, wa,
+                                    bases.to(dev) if window else None, 14400 if window else 0, orow)
+                            if dev == 'cuda':
+                                kern.plan_expert(meta, *args, window_bytes=K * T * 14400 if window else 0,
+                                                 padded_stride=padded)
+                            else:
+                                plan_ref.plan_expert(meta.cpu(), *args, padded=padded)
+                            outs.append([t.cpu() if t is not None else None for t in (ta, wa, orow)])
+                        for g, c, name in zip(outs[0], outs[1], ('table_a', 'wtable_a', 'out_rows')):
+                            assert (g is None) == (c is None)
+                            assert g is None or torch.equal(g, c), (r, single, expanded, window, bypass, padded, name)
         # source side (this rank's own tokens)
         idx = torch.from_numpy(idx_all[r]).cuda()
         dst = torch.empty((T, world), dtype=torch.int32, device='cuda')
         send_counts = torch.empty((world,), dtype=torch.int32, device='cuda')
         kern.dispatch_route(idx, E, world, dst, send_counts)
         for single in (False, True):
-            for window in (False, True):
-                flags = ((_lib.PLAN_SINGLE if single else 0) | (_lib.PLAN_WINDOW if window else 0) |
-                         (_lib.PLAN_RANK_LAYOUT if world <= K and not single else 0))
-                width = K if single else min(world, K)
-                outs = []
-                for dev in ('cuda', 'cpu'):
-                    tb = torch.full((T, width), -7, dtype=torch.int32, device=dev)
-                    wt = None if single else torch.full((T, K), -7, dtype=torch.int32, device=dev)
-                    args = (E, world, T, dst.to(dev), tok_all[r].to(dev), pairs_all[r].to(dev), nb, bpc, flags,
-                            0 if single else 3600, 0 if single else 3584, tb, wt)
-                    if dev == 'cuda':
-                        kern.plan_source(idx, *args)
-                    else:
-                        plan_ref.plan_source(idx.cpu(), *args)
-                    outs.append((tb.cpu(), wt.cpu() if wt is not None else None))
-                assert torch.equal(outs[0][0], outs[1][0]), (r, single, window, 'table_b')
-                assert (outs[0][1] is None and outs[1][1] is None) or torch.equal(outs[0][1], outs[1][1]), \
-                    (r, single, window, 'wtable')
+            for window, bypass in ((False, False), (False, True), (True, False)):
+                for padded in ((0,) if window else (0, bpc * 64 * (min(K, epr) if single else 1))):
+                    flags = ((_lib.PLAN_SINGLE if single else 0) | (_lib.PLAN_WINDOW if window else 0) |
+                             (_lib.PLAN_RANK_LAYOUT if world <= K and not single else 0) |
+                             (_lib.PLAN_LOCAL_BYPASS if bypass else 0))
+                    width = K if single else min(world, K)
+                    outs = []
+                    for dev in ('cuda', 'cpu'):
+                        tb = torch.full((T, width), -7, dtype=torch.int32, device=dev)
+                        wt = None if single else torch.full((T, K), -7, dtype=torch.int32, device=dev)
+                        args = (E, world, r, T, dst.to(dev), tok_all[r].to(dev), pairs_all[r].to(dev), nb, bpc, flags,
+                                0 if single else 3600, 0 if single else 3584, tb, wt)
+                        if dev == 'cuda':
+                            kern.plan_source(idx, *args, padded_stride=padded)
+                        else:
+                            plan_ref.plan_source(idx.cpu(), *args, padded=padded)
+                        outs.append((tb.cpu(), wt.cpu() if wt is not None else None))
+                    assert torch.equal(outs[0][0], outs[1][0]), (r, single, window, bypass, padded, 'table_b')
+                    assert (outs[0][1] is None and outs[1][1] is None) or torch.equal(outs[0][1], outs[1][1]), \
+                        (r, single, window, bypass, padded, 'wtable')
 
 
 # ----------------------------------------------------------------------------- sync-free first combine

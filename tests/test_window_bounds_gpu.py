@@ -41,8 +41,8 @@ def _addr(rec) -> int:
     return (int(rec[5]) & 0xffffffff) << 32 | (int(rec[4]) & 0xffffffff)
 
 
-@pytest.mark.parametrize('choice', [-1, 1, 3, 5])
-def test_scatter_never_stores_outside_its_windows(kern, choice):
+@pytest.mark.parametrize('cfg', [(0, 0), (1, 2), (2, 8)])
+def test_scatter_never_stores_outside_its_windows(kern, cfg):
     """Units whose row address is in a canary region, straddles a window's end, is misaligned or is
     null are skipped; every other unit lands exactly; the first bad unit is recorded."""
     rng = np.random.default_rng(7)
@@ -64,7 +64,7 @@ def test_scatter_never_stores_outside_its_windows(kern, choice):
            10: 0}                                    # a unit plan_expert rejected
     addr = good + [bad[u] for u in range(6, 11)] + [base + 2 * W + 3 * row_bytes]
     err = torch.zeros((8,), dtype=torch.int32, device='cuda')
-    assert kern.lib.deepep_set_kernel_choice(choice) == 0
+    assert kern.lib.deepep_set_launch_config(*cfg) == 0
     try:
         kern.combine_reduce_scatter(_bf16(src), units, torch.tensor(addr, dtype=torch.int64, device='cuda'),
                                     table=torch.from_numpy(table).cuda(), wtable=torch.from_numpy(table).cuda(),
@@ -72,7 +72,7 @@ def test_scatter_never_stores_outside_its_windows(kern, choice):
                                     error_flag=err, windows=(wins, W))
         torch.cuda.synchronize()
     finally:
-        kern.lib.deepep_set_kernel_choice(-1)
+        kern.lib.deepep_set_launch_config(0, 0)
     host = buf.cpu()
     assert int(host[W:2 * W].count_nonzero()) == 0, 'a store escaped into canary 1'
     assert int(host[3 * W:].count_nonzero()) == 0, 'a store escaped into canary 2'
@@ -211,3 +211,93 @@ def test_sym_put_never_stores_past_the_window(kern):
         assert torch.equal(big[d, window - 256:window].view(torch.int32), src[d])
         assert int(big[d, window:].count_nonzero()) == 0
         assert int(big[d, :window - 256].count_nonzero()) == 0
+
+
+def test_padded_plan_never_overwrites_another_source(kern):
+    """A dispatch without a CPU sync pads the single reduction's plan per source to min(K, experts per
+    rank) lanes per token (buffer.hpp:1067-1069's bound).  A token routed twice to one expert breaks that
+    bound: its excess units must be rejected and recorded -- never written into the next source's
+    positions -- and the source side must not point past its destination's padded rows."""
+    from deepep_amd import _lib
+    from tests import plan_ref
+    R, K, E, T = 2, 4, 4, 64                               # 2 experts per rank < K
+    idx0 = np.tile(np.array([[0, 0, 1, 1]], dtype=np.int64), (T, 1))     # 4 lanes on rank 0: duplicates
+    idx1 = np.tile(np.array([[0, 1, 2, 3]], dtype=np.int64), (T, 1))     # 2 lanes on rank 0
+    disp = oracle.simulate_dispatch([idx0, idx1], E, T)
+    meta = torch.from_numpy(disp[0]['src_metadata']).cuda()
+    recv_tok = torch.tensor([[T], [T]], dtype=torch.int32, device='cuda')
+    recv_pairs = torch.tensor([[4 * T], [2 * T]], dtype=torch.int32, device='cuda')
+    padded = T * min(K, E // R)                            # 128 positions per source
+    for bypass in (False, True):
+        flags = _lib.PLAN_EXPANDED | _lib.PLAN_SINGLE | (_lib.PLAN_LOCAL_BYPASS if bypass else 0)
+        table = torch.full((R * padded, 1), -1, dtype=torch.int32, device='cuda')
+        err = torch.zeros((8,), dtype=torch.int32, device='cuda')
+        kern.plan_expert(meta, K, R, 0, T, recv_tok, recv_pairs, 1, 1, flags, table, None, None, 0, None,
+                         error_flag=err, padded_stride=padded)
+        torch.cuda.synchronize()
+        rec = err.tolist()
+        assert rec[0] == FLAG_BAD_SLOT and rec[1] == FAULT_PLAN_UNIT and rec[3] == 0, rec
+        ref = torch.full((R * padded, 1), -1, dtype=torch.int32)
+        plan_ref.plan_expert(meta.cpu(), K, R, 0, T, recv_tok.cpu(), recv_pairs.cpu(), 1, 1, flags, ref, None, None,
+                             0, None, padded=padded)
+        assert torch.equal(table.cpu(), ref), bypass
+        # source 1's 128 units are all there, in its own positions (send order: 1 first with the bypass)
+        own1 = slice(0, padded) if bypass else slice(padded, 2 * padded)
+        assert bool((table.cpu()[own1] >= 0).all()), bypass
+        rows1 = meta.cpu()[meta.cpu()[:, 1] // K == 1][:, 2:]
+        assert sorted(table.cpu()[own1].view(-1).tolist()) == sorted(rows1[rows1 >= 0].tolist())
+    # the source side of rank 0's tokens: destination 0's rows stop at its padded rows (-1 past them)
+    dst = torch.empty((T, R), dtype=torch.int32, device='cuda')
+    kern.dispatch_route(torch.from_numpy(idx0).cuda(), E, R, dst, torch.empty((R,), dtype=torch.int32, device='cuda'))
+    tok, pairs = plan_ref.route_block_counts(torch.from_numpy(idx0), E, R, 1)
+    for bypass in (False, True):
+        flags = _lib.PLAN_SINGLE | (_lib.PLAN_LOCAL_BYPASS if bypass else 0)
+        tb = torch.full((T, K), -7, dtype=torch.int32, device='cuda')
+        kern.plan_source(torch.from_numpy(idx0).cuda(), E, R, 0, T, dst, tok.cuda(), pairs.cuda(), 1, 1, flags, 0, 0,
+                         tb, None, padded_stride=padded)
+        ref = torch.full((T, K), -7, dtype=torch.int32)
+        plan_ref.plan_source(torch.from_numpy(idx0), E, R, 0, T, dst.cpu(), tok, pairs, 1, 1, flags, 0, 0, ref, None,
+                             padded=padded)
+        got = tb.cpu()
+        assert torch.equal(got, ref), bypass
+        assert int((got >= 0).sum()) == padded and int(got.max()) < (1 if bypass else 0) * padded + padded
+
+
+def test_rccl_plan_fault_raises_at_the_next_call():
+    """Over the RCCL transport the plan kernels' fault record (here: duplicate experts in a sync-free
+    dispatch's handle, more lanes per rank than its padding) is published behind the plan build and
+    raises RuntimeError at the handle's next combine -- no silently wrong repeats."""
+    from deepep_amd import ElasticBuffer
+    from tests.sim import FakeGroup, ThreadComm, run_threads
+    R, K, E, T, H = 2, 4, 4, 64, 256
+    comm = ThreadComm(R)
+
+    def rank_fn(rank, results):
+        try:
+            torch.cuda.set_device(0)
+            buf = ElasticBuffer(FakeGroup(rank, R, comm), num_max_tokens_per_rank=T, hidden=H, num_topk=K,
+                                allow_multiple_reduction=False)
+            comm.install(buf, rank)
+            row = [0, 0, 1, 1] if rank == 0 else [0, 1, 2, 3]
+            idx = torch.tensor([row] * T, dtype=torch.int64, device='cuda')
+            w = torch.rand((T, K), device='cuda')
+            x = torch.randn((T, H), device='cuda').to(torch.bfloat16)
+            ex_x, _, _, handle, _ = buf.dispatch(x, topk_idx=idx, topk_weights=w, num_experts=E, do_expand=True,
+                                                 do_cpu_sync=False)
+            buf.combine(ex_x, handle)
+            torch.cuda.synchronize()
+            comm.bar.wait()
+            try:
+                buf.combine(ex_x, handle)
+                results[rank] = 'no error' if rank == 1 else 'rank 0 (expert side of the duplicates) did not raise'
+            except RuntimeError as e:
+                results[rank] = 'raised' if 'combine plan' in str(e) else f'wrong error: {e}'
+                comm.bar.abort()                  # the peer waits in the call's exchange: release it
+        except Exception:
+            import traceback
+            results[rank] = traceback.format_exc()
+            comm.bar.abort()
+
+    results = run_threads(R, rank_fn, (), timeout=120)
+    # rank 0 receives rank 0's duplicate lanes: its expert-side plan rejects them
+    assert results.get(0) == 'raised', results

@@ -3,9 +3,12 @@ simulated by threads on the one GPU (tests/sim.py: the exchange with NCCL stream
 with bench.py's inputs (seed = rank, uniform routing, 8192 x 7168 x top-8, 256 experts, gating-weighted,
 expanded layout), the real library path (HIP dispatch, device-built plan), ONE chunk per rank so each
 rank's phase A is one launch over its whole share.  A 512 MB flush precedes every combine.
-Writes gpurun_out/pmc_ep{N}_meta.json: the algorithmic bytes of every rank's phase-A and phase-B launch
-(the definitions bench.py uses for its N > 1 roofline), in launch order.
-usage: rocprofv3 --pmc FETCH_SIZE -d OUT -o pmc --output-format csv -- python3 tools/pmc_ep.py N"""
+Writes gpurun_out/pmc_ep{N}[_nobypass]_meta.json: the algorithmic bytes of every rank's phase-A and phase-B
+launch (the definitions bench.py uses for its N > 1 roofline), in launch order, and every rank's rows of
+itself (the all-to-all diagonal the local bypass removes) with the packed row size -- `summarize_prof.py
+step` sums every kernel of the whole step (phase A + the exchange's copies + phase B) from the same passes.
+usage: rocprofv3 --pmc FETCH_SIZE -d OUT -o pmc --output-format csv -- python3 tools/pmc_ep.py N [reps]
+       (DEEPEP_LOCAL_BYPASS=0 in the environment: the all-to-all carries the diagonal, for the A/B)"""
 import json
 import os
 import sys
@@ -30,7 +33,8 @@ def main():
     comm = ThreadComm(world)
     flush = torch.empty((512 << 20) // 4, dtype=torch.int32, device='cuda')
     lock = threading.Lock()
-    meta = {'a_bytes': [None] * world, 'b_bytes': [None] * world}
+    meta = {'a_bytes': [None] * world, 'b_bytes': [None] * world, 'own_rows': [None] * world,
+            'sent_rows': [None] * world}
     errors = []
 
     def rank_fn(rank):
@@ -62,6 +66,9 @@ def main():
                 comm.bar.wait()
                 buf.combine(y, handle, topk_weights=ex_w, apply_topk_weights=True)
                 torch.cuda.synchronize()
+            plan = next(p for k, p in handle._combine_plans.items() if k[0] == 'multi')
+            meta['own_rows'][rank] = sum(ch.send_counts[rank] for ch in plan.chunks)
+            meta['sent_rows'][rank] = sum(sum(ch.send_counts) for ch in plan.chunks)
         except Exception:
             import traceback
             errors.append(traceback.format_exc())
@@ -76,8 +83,12 @@ def main():
         print(errors[0], file=sys.stderr)
         sys.exit(1)
     os.makedirs(os.path.join(ROOT, 'gpurun_out'), exist_ok=True)
-    meta.update(world=world, reps=reps, tokens=T, hidden=H, topk=K, experts=E)
-    with open(os.path.join(ROOT, 'gpurun_out', f'pmc_ep{world}_meta.json'), 'w') as f:
+    from deepep_amd.handle import packed_row_layout
+    bypass = os.environ.get('DEEPEP_LOCAL_BYPASS', '1') != '0'
+    meta.update(world=world, reps=reps, tokens=T, hidden=H, topk=K, experts=E, local_bypass=bypass,
+                packed_row_bytes=packed_row_layout(H, K, True)[0])
+    tag = '' if bypass else '_nobypass'
+    with open(os.path.join(ROOT, 'gpurun_out', f'pmc_ep{world}{tag}_meta.json'), 'w') as f:
         json.dump(meta, f)
     print(json.dumps(meta))
 

@@ -163,6 +163,51 @@ def pmc_ep(out, meta_json, *paths):
     print(json.dumps({key: entry}, indent=1))
 
 
+def step(out, meta_json, *paths):
+    """The whole EP = N combine step of tools/pmc_ep.py (every rank, ranks simulated on one GPU): HBM bytes
+    of every kernel but the 512 MB flush fill, grouped as phase A (combine_rows_kernel<0), phase B (<1) and
+    the exchange (the simulated all-to-all's copies), per step (the passes' totals / reps), 2 x FETCH_SIZE +
+    WRITE_SIZE (KiB).  `diagonal_bytes` = what the own-rank rows cost when they travel (read + write of every
+    rank's rows of itself); with the local bypass they do not."""
+    meta = json.load(open(meta_json))
+    tot = defaultdict(lambda: defaultdict(float))
+    launches = defaultdict(int)
+
+    def kind(name):
+        if 'combine_rows_kernel<0' in name:
+            return 'phase_a'
+        if 'combine_rows_kernel<1' in name:
+            return 'phase_b'
+        if 'fill' in name.lower():
+            return None                      # the flush before every step
+        return 'exchange'
+    for p in paths:
+        for r in csv.DictReader(open(p)):
+            k = kind(r.get('Kernel_Name', '').replace('(anonymous namespace)::', ''))
+            if k is None:
+                continue
+            tot[k][r['Counter_Name']] += float(r['Counter_Value'])
+            if r['Counter_Name'] == 'WRITE_SIZE':
+                launches[k] += 1
+    reps = meta['reps']
+    res = {}
+    for k, cs in tot.items():
+        e = {}
+        if 'FETCH_SIZE' in cs:
+            e['read_bytes_per_step'] = 2 * cs['FETCH_SIZE'] * 1024 / reps
+        if 'WRITE_SIZE' in cs:
+            e['write_bytes_per_step'] = cs['WRITE_SIZE'] * 1024 / reps
+        e['launches'] = launches.get(k, 0)
+        res[k] = e
+    total = sum(e.get('read_bytes_per_step', 0) + e.get('write_bytes_per_step', 0) for e in res.values())
+    diag = 2 * sum(meta['own_rows']) * meta['packed_row_bytes']
+    summary = dict(meta=meta, kernels=res, step_bytes=total, diagonal_bytes=diag,
+                   exchanged_rows=sum(meta['sent_rows']) - (sum(meta['own_rows']) if meta['local_bypass'] else 0),
+                   build_id=_build_id())
+    json.dump(summary, open(out, 'w'), indent=1, sort_keys=True)
+    print(json.dumps(summary, indent=1))
+
+
 def policy(out, meta_json, *paths):
     """Phase A under its store policies (tools/pmc_policy.py): the mean counter values and durations of each
     policy's launches (told apart by the store-policy template argument in the kernel name)."""
@@ -190,7 +235,9 @@ def policy(out, meta_json, *paths):
 
 
 if __name__ == '__main__':
-    if sys.argv[1] == 'policy':
+    if sys.argv[1] == 'step':
+        step(sys.argv[2], sys.argv[3], *sys.argv[4:])
+    elif sys.argv[1] == 'policy':
         policy(sys.argv[2], sys.argv[3], *sys.argv[4:])
     elif sys.argv[1] == 'ep':
         pmc_ep(sys.argv[2], sys.argv[3], *sys.argv[4:])

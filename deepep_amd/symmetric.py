@@ -142,8 +142,10 @@ class SymmetricBuffer:
             raise RuntimeError(f'deepep_amd: notify record of {n} ints x {self.num_ranks} ranks does not fit the '
                                f'{HEADER_BYTES - NOTIFY_OFFSET}-byte notify area in 16-byte units')
         handle = stream.cuda_stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        # dest_extent = the header: the C-ABI bound then covers the region this put may write (the notify
+        # area), not the whole window whose data region holds received rows
         _lib.check(self.lib.deepep_sym_put(records.data_ptr(), n * 4, self.bases_dev.data_ptr(), self.num_ranks,
-                                           NOTIFY_OFFSET + self.rank * n * 4, HEADER_BYTES + self.data_bytes,
+                                           NOTIFY_OFFSET + self.rank * n * 4, HEADER_BYTES,
                                            self.error_flag.data_ptr(), handle),
                    'sym_put')
 

@@ -16,9 +16,9 @@ def value_or(value, default):
 def check_torch_deterministic() -> None:
     """deep_ep/utils/envs.py:183-189: deterministic algorithms together with fill_uninitialized_memory make
     torch.empty launch a fill kernel that may overlap the communication streams; the reference refuses the
-    combination in dispatch and combine (elastic.py:924, :1083), and so does this build -- with a RuntimeError
-    (the reference's EP_HOST_ASSERT surfaces as one), which `python -O` does not strip."""
+    combination in dispatch and combine (elastic.py:924, :1083) with a plain `assert`, so this build raises
+    the same exception type, AssertionError -- explicitly, so that `python -O` does not strip it."""
     import torch
     if torch.are_deterministic_algorithms_enabled() and torch.utils.deterministic.fill_uninitialized_memory:
-        raise RuntimeError('Assertion failed: deterministic algorithms with fill_uninitialized_memory would launch '
-                           'fill kernels that overlap the communication streams; disable one of them')
+        raise AssertionError('deterministic algorithms with fill_uninitialized_memory would launch fill kernels '
+                             'that overlap the communication streams; disable one of them')

@@ -1,6 +1,7 @@
 """The reference refuses deterministic algorithms together with fill_uninitialized_memory in dispatch and
 combine (deep_ep/utils/envs.py:183-189, called at elastic.py:924 and :1083): torch.empty then launches a
-fill kernel that may overlap the communication streams.  This build keeps the same guard."""
+fill kernel that may overlap the communication streams.  This build keeps the same guard and
+the same exception type (the reference's plain `assert`: AssertionError)."""
 import pytest
 import torch
 
@@ -25,10 +26,10 @@ def test_guard_passes_by_default():
 
 
 def test_dispatch_and_combine_refuse_deterministic_fill(deterministic_fill):
-    with pytest.raises(RuntimeError):
+    with pytest.raises(AssertionError):
         check_torch_deterministic()
     # the guard is the first thing either call does (nothing about the buffer is touched before it)
-    with pytest.raises(RuntimeError):
+    with pytest.raises(AssertionError):
         ElasticBuffer.combine(object(), None, None)
-    with pytest.raises(RuntimeError):
+    with pytest.raises(AssertionError):
         ElasticBuffer.dispatch(object(), None)

@@ -527,14 +527,15 @@ def _bench_sync_free(buf, x, topk_idx, topk_w, E, weighted, dev, n_iter: int = 8
         torch.cuda.synchronize()
         el = (time.perf_counter() - t0) / n_iter
         plan = next((p for k, p in h._combine_plans.items() if k[0] == 'multi'), None)
-        comb_rows = sum(sum(ch.send_counts) for ch in plan.chunks) if plan is not None else None
+        # rows the all-to-all moves (the local bypass keeps a rank's own rows out of it)
+        comb_rows = sum(sum(ch.send_counts) - ch.own for ch in plan.chunks) if plan is not None else None
         return vmax(el * 1e3), comb_rows
 
     try:
         ms_sync, rows_sync = run(True)
         ms_free, rows_free = run(False)
-        n_sent = int(sum(c for c in buf.dispatch(x, topk_idx=topk_idx, topk_weights=topk_w, num_experts=E,
-                                                 do_expand=True)[3]._send_counts))
+        h_sync = buf.dispatch(x, topk_idx=topk_idx, topk_weights=topk_w, num_experts=E, do_expand=True)[3]
+        n_sent = int(sum(c for d, c in enumerate(h_sync._send_counts) if not (h_sync._bypass and d == buf.rank_idx)))
         moved = torch.tensor([n_sent * disp_row, R * T_max * disp_row, (rows_sync or 0) * comb_row,
                               (rows_free or 0) * comb_row], dtype=torch.float64, device=dev)
         dist.all_reduce(moved)
@@ -548,7 +549,8 @@ def _bench_sync_free(buf, x, topk_idx, topk_w, E, weighted, dev, n_iter: int = 8
                     note='fresh dispatch(do_expand=True, do_cpu_sync=False) + the handle\'s first combine (plan '
                          'built on the device), per iteration, RCCL transport, max over ranks; synced_* = the same '
                          'pair with the host-synced dispatch; *_exchange_bytes = all ranks\' all-to-all bytes '
-                         '(sync-free: worst-case padded, incl. rows a rank keeps); fp8 input: dispatch only')
+                         '(sync-free: worst-case padded, incl. rows a rank keeps; synced: the local bypass keeps '
+                         'them out); fp8 input: dispatch only')
     except Exception as e:          # noqa: BLE001 -- reported in the JSON line
         return dict(error=f'{type(e).__name__}: {e}'[:300])
 

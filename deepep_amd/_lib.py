@@ -96,12 +96,12 @@ SIGNATURES = {
     'deepep_dispatch_route': (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P]),
     'deepep_dispatch_notify': (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _I64, _P]),
     'deepep_dispatch_notify_workspace': (_I64, [_I, _I, _I]),
-    'deepep_dispatch_receive': (_I, [_P, _I64, _I, _I, _I, _I, _I, _I, _P, _I, _I, _P, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P,
-                                     _P]),
+    'deepep_dispatch_receive': (_I, [_P, _I64, _I, _I, _I, _I, _I, _I, _P, _I, _I, _P, _I, _I, _P, _P, _P, _P, _I, _I, _P,
+                                     _P, _P, _P]),
     'deepep_dispatch_expert_counts': (_I, [_P, _I, _I, _I, _P, _P]),
     'deepep_dispatch_pack': (_I, [_P, _I64, _I, _P, _I64, _I, _P, _P, _I, _I, _I, _P, _P, _I,
                                   _P, _P, _I64, _I64, _I, _I, _I, _I, _P, _P]),
-    'deepep_dispatch_count': (_I, [_P, _I64, _I, _I, _I, _I, _I, _I, _P, _I, _I, _P, _I, _P, _P, _P, _P, _P]),
+    'deepep_dispatch_count': (_I, [_P, _I64, _I, _I, _I, _I, _I, _I, _P, _I, _I, _P, _I, _I, _P, _P, _P, _P, _P]),
     'deepep_dispatch_scan': (_I, [_P, _I, _I, _I, _I, _P, _P, _P]),
     'deepep_dispatch_slots': (_I, [_P, _I64, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P]),
     'deepep_dispatch_copy': (_I, [_P, _I64, _I, _I, _I, _I, _I, _I, _P, _I, _P, _I64, _P, _I64, _I,

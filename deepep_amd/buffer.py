@@ -608,6 +608,7 @@ class ElasticBuffer(ExchangeMixin):
             padded = (sync_free or worst_handle) and R > 1 and not use_xgmi
             pad_rows = num_max_tokens_per_rank if padded else 0
             row_map = None
+            own_first = False
             if use_xgmi:
                 kern.dispatch_pack(x_bytes, sf_bytes, idx64, w, r * num_max_tokens_per_rank, dst_slot,
                                    peer_offsets, None, layout, dest_bases=sym.data_bases_dev,
@@ -626,6 +627,28 @@ class ElasticBuffer(ExchangeMixin):
                 recv_packed = torch.empty_like(packed)
                 self._a2a(recv_packed, packed)
                 row_map = torch.empty((N,), dtype=torch.int32, device=dev)
+            elif R > 1 and (cached._bypass if cached is not None else self.local_bypass):
+                # Local bypass (the combine's, exchange.py): one allocation [send rows | own rows | received
+                # rows]; the pack writes the other destinations' rows in rank order and this rank's own rows
+                # right behind them, the all-to-all moves the send rows with a zero split for this rank, and
+                # the receive side reads [own rows | received rows] through a row map (own_first) -- the own
+                # rows are never copied by the collective.
+                own = send_counts_l[r]
+                n_send = sum(send_counts_l)
+                if cached is None:
+                    off, acc = [0] * R, 0
+                    for d in [d for d in range(R) if d != r] + [r]:
+                        off[d], acc = acc, acc + send_counts_l[d]
+                    send_offsets = torch.tensor(off, dtype=torch.int32, device=dev)
+                    row_map = torch.empty((N,), dtype=torch.int32, device=dev)
+                rows_all = torch.empty((n_send + N - own, layout.row_bytes), dtype=torch.uint8, device=dev)
+                kern.dispatch_pack(x_bytes, sf_bytes, idx64, w, r * num_max_tokens_per_rank, dst_slot, send_offsets,
+                                   rows_all, layout, stream=stream)
+                self._a2a(rows_all[n_send:], rows_all[:n_send - own],
+                          [0 if d == r else c for d, c in enumerate(recv_counts_l)],
+                          [0 if d == r else c for d, c in enumerate(send_counts_l)])
+                recv_packed = rows_all[n_send - own:]
+                own_first = True
             else:
                 n_send = T if sync_free else sum(send_counts_l)
                 packed = torch.empty((n_send, layout.row_bytes), dtype=torch.uint8, device=dev)
@@ -667,7 +690,7 @@ class ElasticBuffer(ExchangeMixin):
                 # count -> scan -> slots (expanded; else metadata slot columns -1), back to back
                 kern.dispatch_receive(recv_packed, layout, N, r, epr, recv_counts_t, psum_rank, meta, out_idx,
                                       block_counts, expert_alignment, do_expand, expert_counts, psum_expert, inv=inv,
-                                      pad_rows=pad_rows, row_map=row_map, stream=stream)
+                                      pad_rows=pad_rows, row_map=row_map, own_first=own_first, stream=stream)
                 # known since the notify; [] without a CPU sync (as the reference's handle)
                 aligned_l = [] if sync_free or host_notify is not None else \
                     [align(c, expert_alignment) for c in expert_counts_l]
@@ -757,6 +780,7 @@ class ElasticBuffer(ExchangeMixin):
             handle._copy_tables = (inv, block_offsets)      # reused by cached dispatches
             handle._copy_meta = (copy_meta, copy_rows) if copy_rows != N else None
             handle._row_map = row_map
+            handle._bypass = own_first
             handle._sync_free = sync_free
         out_x = (out_x, out_sf) if out_sf is not None else out_x
         return out_x, out_idx, out_w, handle, EventOverlap(event)

@@ -366,7 +366,7 @@ __device__ __forceinline__ int local_expert(int64_t e, int rank, int epr) {
 __global__ void __launch_bounds__(kBlockRows)
 count_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int idx_off, int src_off, int N, int K,
              int rank, int epr, const int32_t* __restrict__ recv_counts, int counts_stride, int32_t* __restrict__ psum_out,
-             int R, int pad_rows, int32_t* __restrict__ row_map,
+             int R, int pad_rows, int own_first, int32_t* __restrict__ row_map,
              int32_t* __restrict__ meta, int64_t* __restrict__ recv_topk_idx, int32_t* __restrict__ block_counts,
              int fill_slots) {
     extern __shared__ int32_t s_hist[];                 // [epr]
@@ -393,10 +393,13 @@ count_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int idx_off,
     if (i < received) {
         int src_rank = 0;
         while (src_rank < R - 1 && i >= rank_psum[src_rank]) ++src_rank;
-        // padded receive buffer (a worst-case-sized exchange): source s's rows start at s * pad_rows
-        const int64_t prow = pad_rows > 0 ? static_cast<int64_t>(src_rank) * pad_rows + i -
-                                                (src_rank > 0 ? rank_psum[src_rank - 1] : 0)
-                                          : i;
+        // padded receive buffer (a worst-case-sized exchange): source s's rows start at s * pad_rows;
+        // own rows first (the local bypass): [rows from this rank | rows from the others, rank order]
+        const int start = src_rank > 0 ? rank_psum[src_rank - 1] : 0;
+        const int own_start = rank > 0 ? rank_psum[rank - 1] : 0, own_rows = rank_psum[rank] - own_start;
+        int64_t prow = i;
+        if (pad_rows > 0) prow = static_cast<int64_t>(src_rank) * pad_rows + i - start;
+        else if (own_first) prow = src_rank == rank ? i - own_start : (src_rank < rank ? i + own_rows : i);
         if (row_map != nullptr) row_map[i] = static_cast<int32_t>(prow);
         const uint8_t* row = packed + prow * row_bytes;
         const int64_t* idx = reinterpret_cast<const int64_t*>(row + idx_off);
@@ -815,36 +818,37 @@ int deepep_dispatch_pack(const void* x, int64_t x_row_stride_bytes, int x_bytes,
 
 int deepep_dispatch_count(const void* packed, int64_t row_bytes, int idx_off, int src_off, int num_recv, int num_topk,
                           int rank, int num_local_experts, const int32_t* recv_rank_psum, int num_ranks,
-                          int recv_counts_stride, int32_t* psum_out, int pad_rows, int32_t* row_map,
+                          int recv_counts_stride, int32_t* psum_out, int pad_rows, int own_first, int32_t* row_map,
                           int32_t* src_metadata, int64_t* recv_topk_idx, int32_t* block_counts,
                           deepep_stream_t stream) {
     // a rank that receives nothing: no rows, but one workgroup still forms psum_out
     if (num_recv == 0 && (psum_out == nullptr || recv_counts_stride == 0)) return DEEPEP_OK;
     if (num_recv < 0 || num_topk < 1 || num_topk > 32 || num_local_experts < 1 || num_local_experts > 1024 ||
-        num_ranks < 1 || num_ranks > 64 || recv_counts_stride < 0 ||
+        num_ranks < 1 || num_ranks > 64 || recv_counts_stride < 0 || rank < 0 || rank >= num_ranks ||
         (num_recv > 0 && (src_metadata == nullptr || block_counts == nullptr || packed == nullptr)) ||
-        recv_rank_psum == nullptr || pad_rows < 0 || (num_recv > 0 && pad_rows > 0 && row_map == nullptr) ||
-        static_cast<int64_t>(pad_rows) * num_ranks >= (int64_t(1) << 31))
+        recv_rank_psum == nullptr || pad_rows < 0 || (num_recv > 0 && (pad_rows > 0 || own_first) && row_map == nullptr) ||
+        (pad_rows > 0 && own_first) || static_cast<int64_t>(pad_rows) * num_ranks >= (int64_t(1) << 31))
         return deepep_amd_set_error(DEEPEP_ERR_INVALID_ARG, "dispatch_count: invalid arguments");
     const int nblocks = std::max(1, (num_recv + kBlockRows - 1) / kBlockRows);
     hipLaunchKernelGGL(count_kernel, dim3(nblocks), dim3(kBlockRows), num_local_experts * 4,
                        reinterpret_cast<hipStream_t>(stream), static_cast<const uint8_t*>(packed), row_bytes,
                        idx_off, src_off, num_recv, num_topk, rank, num_local_experts, recv_rank_psum,
-                       recv_counts_stride, psum_out, num_ranks, pad_rows, row_map, src_metadata, recv_topk_idx,
-                       block_counts, 0);
+                       recv_counts_stride, psum_out, num_ranks, pad_rows, own_first ? 1 : 0, row_map, src_metadata,
+                       recv_topk_idx, block_counts, 0);
     return launch_status("dispatch_count");
 }
 
 int deepep_dispatch_receive(const void* packed, int64_t row_bytes, int idx_off, int src_off, int num_recv,
                             int num_topk, int rank, int num_local_experts, const int32_t* recv_counts,
-                            int num_ranks, int recv_counts_stride, int32_t* psum_out, int pad_rows, int32_t* row_map,
-                            int32_t* src_metadata, int64_t* recv_topk_idx, int32_t* block_counts,
+                            int num_ranks, int recv_counts_stride, int32_t* psum_out, int pad_rows, int own_first,
+                            int32_t* row_map, int32_t* src_metadata, int64_t* recv_topk_idx, int32_t* block_counts,
                             int expert_alignment, int expanded, int32_t* expert_counts, int32_t* psum_expert,
                             int32_t* inv, deepep_stream_t stream) {
     if (num_recv < 0 || num_topk < 1 || num_topk > 32 || num_local_experts < 1 || num_local_experts > 1024 ||
         num_ranks < 1 || num_ranks > 64 || recv_counts_stride < 1 || recv_counts == nullptr || psum_out == nullptr ||
+        rank < 0 || rank >= num_ranks ||
         (num_recv > 0 && (src_metadata == nullptr || block_counts == nullptr || packed == nullptr)) ||
-        pad_rows < 0 || (num_recv > 0 && pad_rows > 0 && row_map == nullptr) ||
+        pad_rows < 0 || (num_recv > 0 && (pad_rows > 0 || own_first) && row_map == nullptr) || (pad_rows > 0 && own_first) ||
         static_cast<int64_t>(pad_rows) * num_ranks >= (int64_t(1) << 31) || expert_alignment < 1 ||
         expert_counts == nullptr || psum_expert == nullptr ||
         static_cast<int64_t>(num_recv) * num_topk >= (int64_t(1) << 31))
@@ -853,8 +857,8 @@ int deepep_dispatch_receive(const void* packed, int64_t row_bytes, int idx_off, 
     const int nblocks = (num_recv + kBlockRows - 1) / kBlockRows;
     hipLaunchKernelGGL(count_kernel, dim3(std::max(nblocks, 1)), dim3(kBlockRows), num_local_experts * 4, s,
                        static_cast<const uint8_t*>(packed), row_bytes, idx_off, src_off, num_recv, num_topk, rank,
-                       num_local_experts, recv_counts, recv_counts_stride, psum_out, num_ranks, pad_rows, row_map,
-                       src_metadata, recv_topk_idx, block_counts, expanded ? 0 : 1);
+                       num_local_experts, recv_counts, recv_counts_stride, psum_out, num_ranks, pad_rows,
+                       own_first ? 1 : 0, row_map, src_metadata, recv_topk_idx, block_counts, expanded ? 0 : 1);
     hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, s, block_counts, nblocks, num_local_experts,
                        expert_alignment, expanded, expert_counts, psum_expert);
     if (expanded && nblocks > 0)

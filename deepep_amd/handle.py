@@ -274,6 +274,7 @@ class EPHandle:
         self._send_offsets: Optional[torch.Tensor] = None
         self._recv_topk_idx: Optional[torch.Tensor] = None    # non-expanded recv_topk_idx (int64, N rows)
         self._counts: Optional[BlockCounts] = None            # per-block routing counts (EP > 1 plans)
+        self._bypass = False                                  # rows laid out for the dispatch's local bypass
         self._combine_plans = {}
 
     def deterministic_sort(self, *args, **kwargs) -> None:

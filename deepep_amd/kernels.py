@@ -269,12 +269,14 @@ class HipKernels:
 
     def dispatch_count(self, packed, layout: RowLayout, num_recv, rank, num_local_experts, rank_psum, meta,
                        recv_topk_idx, block_counts, pad_rows: int = 0, row_map=None, rank_counts=None,
-                       psum_out=None, stream=None):
+                       psum_out=None, own_first: bool = False, stream=None):
         """rank_psum: inclusive prefix of rows per source rank (int32 [R]); or, with rank_psum None,
         rank_counts: rows per source rank (an int32 [R] view of any stride, e.g. the notify records'
         first column), whose prefix the kernel forms and writes to psum_out (int32 [R]).
         pad_rows > 0: `packed` is a worst-case-sized receive buffer, source s's rows at s * pad_rows;
-        row_map (int32 [num_recv]) receives each received row's packed row (for slots / copy)."""
+        row_map (int32 [num_recv]) receives each received row's packed row (for slots / copy).
+        own_first: `packed` = [rows from this rank | rows from the others, rank order] (the local bypass);
+        row_map is written the same way."""
         src = rank_psum if rank_psum is not None else rank_counts
         _require(src is not None and src.dim() == 1 and src.dtype == torch.int32 and src.stride(0) >= 1,
                  'dispatch_count needs rank_psum or rank_counts (int32 [num_ranks])')
@@ -285,15 +287,18 @@ class HipKernels:
         _require(pad_rows == 0 or (row_map is not None and row_map.dtype == torch.int32 and
                                    row_map.numel() >= num_recv and packed.shape[0] >= pad_rows * R),
                  'padded receive rows need a row map and R * pad_rows packed rows')
+        _require(not own_first or (row_map is not None and row_map.dtype == torch.int32 and
+                                   row_map.numel() >= num_recv and packed.shape[0] >= num_recv),
+                 'own-first receive rows need a row map')
         rc = self.lib.deepep_dispatch_count(
             ptr(packed), layout.row_bytes, layout.idx_off, layout.src_off, num_recv, layout.num_topk, rank,
-            num_local_experts, ptr(src), R, stride, ptr(psum_out), pad_rows, ptr(row_map), ptr(meta),
+            num_local_experts, ptr(src), R, stride, ptr(psum_out), pad_rows, int(own_first), ptr(row_map), ptr(meta),
             ptr(recv_topk_idx), ptr(block_counts), _stream_handle(stream))
         _lib.check(rc, 'dispatch_count')
 
     def dispatch_receive(self, packed, layout: RowLayout, num_recv, rank, num_local_experts, rank_counts, psum_out,
                          meta, recv_topk_idx, block_counts, expert_alignment, expanded, expert_counts, psum_expert,
-                         inv=None, pad_rows: int = 0, row_map=None, stream=None):
+                         inv=None, pad_rows: int = 0, row_map=None, own_first: bool = False, stream=None):
         """count (counts mode) -> scan -> slots (expanded) in one call: the receive side's launches back to
         back.  Non-expanded: meta columns 2.. become -1."""
         _require(rank_counts.dim() == 1 and rank_counts.dtype == torch.int32 and rank_counts.stride(0) >= 1,
@@ -304,10 +309,13 @@ class HipKernels:
         _require(pad_rows == 0 or (row_map is not None and row_map.dtype == torch.int32 and
                                    row_map.numel() >= num_recv and packed.shape[0] >= pad_rows * R),
                  'padded receive rows need a row map and R * pad_rows packed rows')
+        _require(not own_first or (row_map is not None and row_map.dtype == torch.int32 and
+                                   row_map.numel() >= num_recv), 'own-first receive rows need a row map')
         _require(inv is None or (inv.dtype == torch.int32 and inv.is_contiguous()), 'inv int32')
         rc = self.lib.deepep_dispatch_receive(
             ptr(packed), layout.row_bytes, layout.idx_off, layout.src_off, num_recv, layout.num_topk, rank,
-            num_local_experts, ptr(rank_counts), R, rank_counts.stride(0), ptr(psum_out), pad_rows, ptr(row_map),
+            num_local_experts, ptr(rank_counts), R, rank_counts.stride(0), ptr(psum_out), pad_rows, int(own_first),
+            ptr(row_map),
             ptr(meta), ptr(recv_topk_idx), ptr(block_counts), expert_alignment, int(expanded), ptr(expert_counts),
             ptr(psum_expert), ptr(inv), _stream_handle(stream))
         _lib.check(rc, 'dispatch_receive')

@@ -140,7 +140,8 @@ class OracleKernels:
         return torch.where(inr, idx - rank * epr, torch.full_like(idx, -1))
 
     def dispatch_count(self, packed, layout, num_recv, rank, num_local_experts, rank_psum, meta, recv_topk_idx,
-                       block_counts, pad_rows=0, row_map=None, rank_counts=None, psum_out=None, stream=None):
+                       block_counts, pad_rows=0, row_map=None, rank_counts=None, psum_out=None, own_first=False,
+                       stream=None):
         K, epr = layout.num_topk, num_local_experts
         if rank_psum is None:
             rank_psum = torch.cumsum(rank_counts, 0).to(torch.int32)
@@ -153,10 +154,18 @@ class OracleKernels:
         if recv_topk_idx is not None:
             recv_topk_idx[N:num_recv] = -1
         src_rank = torch.searchsorted(rank_psum.to(torch.int64), torch.arange(N), right=True).clamp(max=rank_psum.numel() - 1)
+        start = torch.cat([torch.zeros(1, dtype=torch.int64), rank_psum.to(torch.int64)])[src_rank]
         if pad_rows:
-            start = torch.cat([torch.zeros(1, dtype=torch.int64), rank_psum.to(torch.int64)])[src_rank]
             row_map[:N] = (src_rank * pad_rows + torch.arange(N) - start).to(torch.int32)
-        rm = row_map if pad_rows else None
+        elif own_first:
+            # [rows from this rank | the other sources' rows in rank order] (the local bypass)
+            psum = rank_psum.to(torch.int64)
+            own_start = int(psum[rank - 1]) if rank > 0 else 0
+            own_rows = int(psum[rank]) - own_start
+            i = torch.arange(N)
+            row_map[:N] = torch.where(src_rank == rank, i - own_start,
+                                      torch.where(src_rank < rank, i + own_rows, i)).to(torch.int32)
+        rm = row_map if pad_rows or own_first else None
         le = self._local(packed, layout, N, rank, epr, rm)
         src = self._rows(packed, N, rm)[:, layout.src_off:layout.src_off + 4].contiguous().view(torch.int32).view(N)
         master = torch.where(le >= 0, torch.arange(K).view(1, K), torch.full_like(le, -1)).amax(dim=1)
@@ -173,9 +182,10 @@ class OracleKernels:
 
     def dispatch_receive(self, packed, layout, num_recv, rank, num_local_experts, rank_counts, psum_out, meta,
                          recv_topk_idx, block_counts, expert_alignment, expanded, expert_counts, psum_expert,
-                         inv=None, pad_rows=0, row_map=None, stream=None):
+                         inv=None, pad_rows=0, row_map=None, own_first=False, stream=None):
         self.dispatch_count(packed, layout, num_recv, rank, num_local_experts, None, meta, recv_topk_idx, block_counts,
-                            pad_rows=pad_rows, row_map=row_map, rank_counts=rank_counts, psum_out=psum_out)
+                            pad_rows=pad_rows, row_map=row_map, rank_counts=rank_counts, psum_out=psum_out,
+                            own_first=own_first)
         self.dispatch_scan(block_counts, num_local_experts, expert_alignment, expanded, expert_counts, psum_expert)
         if expanded:
             self.dispatch_slots(packed, layout, num_recv, rank, num_local_experts, block_counts, meta, inv=inv,

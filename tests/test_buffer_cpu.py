@@ -246,21 +246,39 @@ def _random_worker(rank, world, port, seed, queue, env=None):
         expect = oracle.combine_ep(x_exp_all, [d['src_metadata'] for d in disp], idx_all, E, T, expanded=True,
                                    topk_weights_per_rank=w_exp_all,
                                    bias_per_rank=[(b, None) for b in b_all])
-        buf = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=T, hidden=H, num_topk=K)
-        buf._kernels = OracleKernels()
-        x = torch.zeros((T, H), dtype=torch.bfloat16)
-        _, _, ex_w, handle, _ = buf.dispatch(x, topk_idx=torch.from_numpy(idx_all[rank]),
-                                             topk_weights=torch.from_numpy(w_all[rank]),
-                                             num_experts=E, do_expand=True)
         failures = []
-        if not np.array_equal(handle.recv_src_metadata.numpy(), disp[rank]['src_metadata']):
-            failures.append('recv_src_metadata differs from the oracle dispatch')
-        out, out_w, _ = buf.combine(_u16_to_bf16(x_exp_all[rank]), handle, topk_weights=ex_w,
-                                    bias=_u16_to_bf16(b_all[rank]))
-        if not np.array_equal(_bf16_to_u16(out), expect[rank][0]):
-            failures.append('combined_x')
-        if not np.array_equal(out_w.numpy(), expect[rank][1]):
-            failures.append('combined_topk_weights')
+        x = torch.zeros((T, H), dtype=torch.bfloat16)
+        diagonals = {}
+        for bypass in (True, False):
+            buf = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=T, hidden=H, num_topk=K)
+            buf._kernels = OracleKernels()
+            buf.local_bypass = bypass
+            # every row all-to-all of this buffer (dispatch rows, combine partials): this rank's own split
+            splits = []
+            a2a = buf._a2a
+
+            def spy(out, inp, out_splits=None, in_splits=None, _a2a=a2a, _splits=splits):
+                if in_splits is not None:
+                    _splits.append((in_splits[rank], out_splits[rank]))
+                return _a2a(out, inp, out_splits, in_splits)
+            buf._a2a = spy
+            _, _, ex_w, handle, _ = buf.dispatch(x, topk_idx=torch.from_numpy(idx_all[rank]),
+                                                 topk_weights=torch.from_numpy(w_all[rank]),
+                                                 num_experts=E, do_expand=True)
+            if not np.array_equal(handle.recv_src_metadata.numpy(), disp[rank]['src_metadata']):
+                failures.append(f'recv_src_metadata differs from the oracle dispatch (bypass {bypass})')
+            out, out_w, _ = buf.combine(_u16_to_bf16(x_exp_all[rank]), handle, topk_weights=ex_w,
+                                        bias=_u16_to_bf16(b_all[rank]))
+            if not np.array_equal(_bf16_to_u16(out), expect[rank][0]):
+                failures.append(f'combined_x (bypass {bypass})')
+            if not np.array_equal(out_w.numpy(), expect[rank][1]):
+                failures.append(f'combined_topk_weights (bypass {bypass})')
+            diagonals[bypass] = splits
+        # the local bypass: no row exchange carries this rank's own rows; without it they travel
+        if not diagonals[True] or any(a or b for a, b in diagonals[True]):
+            failures.append(f'own rows in the all-to-all with the local bypass: {diagonals[True]}')
+        if not any(a for a, _ in diagonals[False]):
+            failures.append(f'no own rows without the bypass (test routing too sparse?): {diagonals[False]}')
         queue.put((rank, failures))
         dist.barrier()
         dist.destroy_process_group()

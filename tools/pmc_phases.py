@@ -1,7 +1,7 @@
 """Launch each HBM-bound kernel of the path three times, a 512 MB flush before every launch, for
 rocprofv3 --pmc passes (one counter set per run):
   fused    EP = 1 combine, BASELINE config 2 (weighted)
-  local    EP = 8 phase A, one rank's share of config 3 (tools/kphase.py's shapes)
+  local    EP = 8 phase A, one rank's share of config 3 (round 4's kphase tool, in git history)
   epilogue EP = 8 phase B, same rank
   copy     EP = 1 dispatch copy (expanded), config 2
 Writes the algorithmic bytes per launch of each to gpurun_out/pmc_phases_meta.json.
@@ -59,7 +59,7 @@ def main():
                            num_max_tokens=T, inv=inv, block_offsets=block_offsets,
                            expert_end=handle.psum_num_recv_tokens_per_expert)
     meta_out['copy'] = T * H * 2 + ex_x.shape[0] * H * 2
-    # ---- EP = 8, rank 0's phases (tools/kphase.py)
+    # ---- EP = 8, rank 0's phases (as round 4's kphase tool)
     epr = E // R
     idx8 = torch.stack([torch.topk(torch.rand((T, E), device='cuda', generator=g), K, dim=-1)[1] for _ in range(R)])
     local = (idx8 >= 0) & (idx8 < epr)

@@ -191,5 +191,6 @@ def test_config4_ep8_fp8_dispatch_bf16_combine():
     _run(8192, fp8=True)
 
 
-def test_config5_ep8_16384_tokens_skewed():
-    _run(16384, skew=4.0)
+@pytest.mark.parametrize('weighted', [False, True], ids=['plain_bias', 'gating_weighted'])
+def test_config5_ep8_16384_tokens_skewed(weighted):
+    _run(16384, skew=4.0, weighted=weighted)

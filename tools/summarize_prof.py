@@ -165,8 +165,9 @@ def pmc_ep(out, meta_json, *paths):
 
 def step(out, meta_json, *paths):
     """The whole EP = N combine step of tools/pmc_ep.py (every rank, ranks simulated on one GPU): HBM bytes
-    of every kernel but the 512 MB flush fill, grouped as phase A (combine_rows_kernel<0), phase B (<1) and
-    the exchange (the simulated all-to-all's copies), per step (the passes' totals / reps), 2 x FETCH_SIZE +
+    of every kernel after the first 512 MB flush fill (the set-up -- inputs, dispatch -- runs before it) but
+    the flushes, grouped as phase A (combine_rows_kernel<0), phase B (<1) and the exchange (the simulated
+    all-to-all's copies), per step (the passes' totals / reps), 2 x FETCH_SIZE +
     WRITE_SIZE (KiB).  `diagonal_bytes` = what the own-rank rows cost when they travel (read + write of every
     rank's rows of itself); with the local bypass they do not."""
     meta = json.load(open(meta_json))
@@ -182,7 +183,10 @@ def step(out, meta_json, *paths):
             return None                      # the flush before every step
         return 'exchange'
     for p in paths:
-        for r in csv.DictReader(open(p)):
+        rows = sorted(csv.DictReader(open(p)), key=lambda r: int(r['Dispatch_Id']))
+        # the set-up (inputs, dispatch) runs before the first flush; every combine step follows a flush
+        first = next((i for i, r in enumerate(rows) if kind(r.get('Kernel_Name', '')) is None), len(rows))
+        for r in rows[first:]:
             k = kind(r.get('Kernel_Name', '').replace('(anonymous namespace)::', ''))
             if k is None:
                 continue

@@ -29,6 +29,8 @@ for step in "$@"; do
     case $step in
         tests)  run pytest_gpu 1100 python -u -m pytest tests -m gpu -x -q --timeout 170 --timeout-method thread ;;
         smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+        fullweighted) # item 1: the full-size gating-weighted cases with their per-rank calc_diff printed
+                run fullweighted 600 python -u -m pytest tests/test_fullsize_gpu.py -k gating_weighted -s -q --timeout 170 --timeout-method thread ;;
         bench)  run bench 600 python bench.py ;;
         benchjson) run bench 600 python bench.py && grep '^{' $OUT/bench.log | tail -1 > $OUT/bench.json ;;
         profdefault) # the driver's exact command under rocprofv3; per-loop averages from the kernel trace

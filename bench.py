@@ -536,7 +536,9 @@ def _bench_sync_free(buf, x, topk_idx, topk_w, E, weighted, dev, n_iter: int = 8
         ms_free, rows_free = run(False)
         h_sync = buf.dispatch(x, topk_idx=topk_idx, topk_weights=topk_w, num_experts=E, do_expand=True)[3]
         n_sent = int(sum(c for d, c in enumerate(h_sync._send_counts) if not (h_sync._bypass and d == buf.rank_idx)))
-        moved = torch.tensor([n_sent * disp_row, R * T_max * disp_row, (rows_sync or 0) * comb_row,
+        # the padded exchange moves T_max rows to every rank but itself (the local bypass keeps its own block)
+        moved = torch.tensor([n_sent * disp_row, (R - (1 if buf.local_bypass else 0)) * T_max * disp_row,
+                              (rows_sync or 0) * comb_row,
                               (rows_free or 0) * comb_row], dtype=torch.float64, device=dev)
         dist.all_reduce(moved)
         moved = [float(v) for v in moved.tolist()]
@@ -549,8 +551,8 @@ def _bench_sync_free(buf, x, topk_idx, topk_w, E, weighted, dev, n_iter: int = 8
                     note='fresh dispatch(do_expand=True, do_cpu_sync=False) + the handle\'s first combine (plan '
                          'built on the device), per iteration, RCCL transport, max over ranks; synced_* = the same '
                          'pair with the host-synced dispatch; *_exchange_bytes = all ranks\' all-to-all bytes '
-                         '(sync-free: worst-case padded, incl. rows a rank keeps; synced: the local bypass keeps '
-                         'them out); fp8 input: dispatch only')
+                         '(worst-case padded without a CPU sync; the local bypass keeps a rank\'s own rows / '
+                         'padded block out of both); fp8 input: dispatch only')
     except Exception as e:          # noqa: BLE001 -- reported in the JSON line
         return dict(error=f'{type(e).__name__}: {e}'[:300])
 

@@ -619,13 +619,27 @@ class ElasticBuffer(ExchangeMixin):
                     sym.publish(stream)
                 recv_packed = sym.data[:N * layout.row_bytes].view(N, layout.row_bytes)
             elif padded:
-                # worst-case-padded all-to-all: T_max rows per destination (rank d's rows at d * T_max)
-                packed = torch.empty((R * num_max_tokens_per_rank, layout.row_bytes), dtype=torch.uint8, device=dev)
-                pad_offsets = torch.arange(R, dtype=torch.int32, device=dev) * num_max_tokens_per_rank
-                kern.dispatch_pack(x_bytes, sf_bytes, idx64, w, r * num_max_tokens_per_rank, dst_slot, pad_offsets,
-                                   packed, layout, stream=stream)
-                recv_packed = torch.empty_like(packed)
-                self._a2a(recv_packed, packed)
+                # worst-case-padded all-to-all: T_max rows per destination (rank d's rows at d * T_max); with the
+                # local bypass this rank's own T_max rows are packed behind the others' and stay out of the
+                # collective: [send rows | own rows | received rows], slots in send / receive order (no host
+                # sync: the splits are T_max)
+                T_max = num_max_tokens_per_rank
+                own_first = cached._bypass if cached is not None else self.local_bypass
+                ar = torch.arange(R, dtype=torch.int32, device=dev)
+                if own_first:
+                    pad_offsets = torch.where(ar == r, R - 1, torch.where(ar > r, ar - 1, ar)) * T_max
+                    rows_all = torch.empty(((2 * R - 1) * T_max, layout.row_bytes), dtype=torch.uint8, device=dev)
+                    kern.dispatch_pack(x_bytes, sf_bytes, idx64, w, r * T_max, dst_slot, pad_offsets, rows_all, layout,
+                                       stream=stream)
+                    splits = [0 if d == r else T_max for d in range(R)]
+                    self._a2a(rows_all[R * T_max:], rows_all[:(R - 1) * T_max], splits, splits)
+                    recv_packed = rows_all[(R - 1) * T_max:]
+                else:
+                    packed = torch.empty((R * T_max, layout.row_bytes), dtype=torch.uint8, device=dev)
+                    kern.dispatch_pack(x_bytes, sf_bytes, idx64, w, r * T_max, dst_slot, ar * T_max, packed, layout,
+                                       stream=stream)
+                    recv_packed = torch.empty_like(packed)
+                    self._a2a(recv_packed, packed)
                 row_map = torch.empty((N,), dtype=torch.int32, device=dev)
             elif R > 1 and (cached._bypass if cached is not None else self.local_bypass):
                 # Local bypass (the combine's, exchange.py): one allocation [send rows | own rows | received

@@ -398,8 +398,13 @@ count_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int idx_off,
         const int start = src_rank > 0 ? rank_psum[src_rank - 1] : 0;
         const int own_start = rank > 0 ? rank_psum[rank - 1] : 0, own_rows = rank_psum[rank] - own_start;
         int64_t prow = i;
-        if (pad_rows > 0) prow = static_cast<int64_t>(src_rank) * pad_rows + i - start;
-        else if (own_first) prow = src_rank == rank ? i - own_start : (src_rank < rank ? i + own_rows : i);
+        if (pad_rows > 0) {
+            // own first: the slots in receive order [rank, 0, .., rank - 1, rank + 1, ..]
+            const int slot = !own_first ? src_rank : (src_rank == rank ? 0 : (src_rank < rank ? src_rank + 1 : src_rank));
+            prow = static_cast<int64_t>(slot) * pad_rows + i - start;
+        } else if (own_first) {
+            prow = src_rank == rank ? i - own_start : (src_rank < rank ? i + own_rows : i);
+        }
         if (row_map != nullptr) row_map[i] = static_cast<int32_t>(prow);
         const uint8_t* row = packed + prow * row_bytes;
         const int64_t* idx = reinterpret_cast<const int64_t*>(row + idx_off);
@@ -827,7 +832,7 @@ int deepep_dispatch_count(const void* packed, int64_t row_bytes, int idx_off, in
         num_ranks < 1 || num_ranks > 64 || recv_counts_stride < 0 || rank < 0 || rank >= num_ranks ||
         (num_recv > 0 && (src_metadata == nullptr || block_counts == nullptr || packed == nullptr)) ||
         recv_rank_psum == nullptr || pad_rows < 0 || (num_recv > 0 && (pad_rows > 0 || own_first) && row_map == nullptr) ||
-        (pad_rows > 0 && own_first) || static_cast<int64_t>(pad_rows) * num_ranks >= (int64_t(1) << 31))
+        static_cast<int64_t>(pad_rows) * num_ranks >= (int64_t(1) << 31))
         return deepep_amd_set_error(DEEPEP_ERR_INVALID_ARG, "dispatch_count: invalid arguments");
     const int nblocks = std::max(1, (num_recv + kBlockRows - 1) / kBlockRows);
     hipLaunchKernelGGL(count_kernel, dim3(nblocks), dim3(kBlockRows), num_local_experts * 4,
@@ -848,7 +853,7 @@ int deepep_dispatch_receive(const void* packed, int64_t row_bytes, int idx_off, 
         num_ranks < 1 || num_ranks > 64 || recv_counts_stride < 1 || recv_counts == nullptr || psum_out == nullptr ||
         rank < 0 || rank >= num_ranks ||
         (num_recv > 0 && (src_metadata == nullptr || block_counts == nullptr || packed == nullptr)) ||
-        pad_rows < 0 || (num_recv > 0 && (pad_rows > 0 || own_first) && row_map == nullptr) || (pad_rows > 0 && own_first) ||
+        pad_rows < 0 || (num_recv > 0 && (pad_rows > 0 || own_first) && row_map == nullptr) ||
         static_cast<int64_t>(pad_rows) * num_ranks >= (int64_t(1) << 31) || expert_alignment < 1 ||
         expert_counts == nullptr || psum_expert == nullptr ||
         static_cast<int64_t>(num_recv) * num_topk >= (int64_t(1) << 31))

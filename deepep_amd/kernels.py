@@ -288,8 +288,7 @@ class HipKernels:
                                    row_map.numel() >= num_recv and packed.shape[0] >= pad_rows * R),
                  'padded receive rows need a row map and R * pad_rows packed rows')
         _require(not own_first or (row_map is not None and row_map.dtype == torch.int32 and
-                                   row_map.numel() >= num_recv and packed.shape[0] >= num_recv),
-                 'own-first receive rows need a row map')
+                                   row_map.numel() >= num_recv), 'own-first receive rows need a row map')
         rc = self.lib.deepep_dispatch_count(
             ptr(packed), layout.row_bytes, layout.idx_off, layout.src_off, num_recv, layout.num_topk, rank,
             num_local_experts, ptr(src), R, stride, ptr(psum_out), pad_rows, int(own_first), ptr(row_map), ptr(meta),

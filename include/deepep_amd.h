@@ -223,10 +223,11 @@ int deepep_dispatch_pack(const void* x, int64_t x_row_stride_bytes, int x_bytes,
  * columns 0-1 = -1 and recv_topk_idx -1; passes 3 and 4 skip them.
  * pad_rows > 0: the packed rows come from a worst-case-sized exchange, source s's rows at s * pad_rows
  * (not contiguous); row_map (int32 [num_recv]) then receives the packed row of every received row i,
- * which passes 3 and 4 take as their row_map.  own_first (the local bypass of an exact all-to-all, not
- * with pad_rows): packed = [rows from `rank` itself | rows from the other sources in rank order] -- the
- * sender packed its own rows straight behind its send rows, so they never enter the all-to-all -- and
- * row_map is written the same way.  Neither: packed row i is row i (row_map may be NULL). */
+ * which passes 3 and 4 take as their row_map.  own_first (the local bypass): packed = [rows from `rank`
+ * itself | rows from the other sources in rank order] -- the sender packed its own rows straight behind
+ * its send rows, so they never enter the all-to-all -- and row_map is written the same way; with pad_rows
+ * the padded slots are in that order too (`rank`'s at 0, source s < rank at (s + 1) * pad_rows, s > rank at
+ * s * pad_rows).  Neither: packed row i is row i (row_map may be NULL). */
 int deepep_dispatch_count(const void* packed, int64_t row_bytes, int idx_off, int src_off, int num_recv, int num_topk,
                           int rank, int num_local_experts, const int32_t* recv_rank_psum, int num_ranks,
                           int recv_counts_stride, int32_t* psum_out, int pad_rows, int own_first, int32_t* row_map,

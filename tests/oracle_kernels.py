@@ -156,7 +156,11 @@ class OracleKernels:
         src_rank = torch.searchsorted(rank_psum.to(torch.int64), torch.arange(N), right=True).clamp(max=rank_psum.numel() - 1)
         start = torch.cat([torch.zeros(1, dtype=torch.int64), rank_psum.to(torch.int64)])[src_rank]
         if pad_rows:
-            row_map[:N] = (src_rank * pad_rows + torch.arange(N) - start).to(torch.int32)
+            slot = src_rank
+            if own_first:                                # receive order [rank, 0, .., rank - 1, rank + 1, ..]
+                slot = torch.where(src_rank == rank, torch.zeros_like(src_rank),
+                                   torch.where(src_rank < rank, src_rank + 1, src_rank))
+            row_map[:N] = (slot * pad_rows + torch.arange(N) - start).to(torch.int32)
         elif own_first:
             # [rows from this rank | the other sources' rows in rank order] (the local bypass)
             psum = rank_psum.to(torch.int64)

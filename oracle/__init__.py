@@ -299,8 +299,15 @@ def combine_ep_one(rank: int, recv_x_per_rank: Sequence[np.ndarray], src_metadat
             m = np.ascontiguousarray(meta[mine])
             x = np.asarray(recv_x_per_rank[r], dtype=np.uint16)
             w = topk_weights_per_rank[r] if with_w else None
-            parts = list(pool.map(lambda lh: phase_a(x, m[lh[0]:lh[1]], K, expanded, w, weighted=weighted),
-                                  _split_rows(m.shape[0], threads)))
+            if expanded:                  # slots index the whole expanded x / weight arrays
+                parts = list(pool.map(lambda lh: phase_a(x, m[lh[0]:lh[1]], K, True, w, weighted=weighted),
+                                      _split_rows(m.shape[0], threads)))
+            else:                         # received row i is x row i: select and slice the rows with the metadata
+                xs = np.ascontiguousarray(x[mine])
+                ws = np.ascontiguousarray(np.asarray(w, np.float32).reshape(-1, K)[mine]) if w is not None else None
+                parts = list(pool.map(lambda lh: phase_a(xs[lh[0]:lh[1]], m[lh[0]:lh[1]], K, False,
+                                                         ws[lh[0]:lh[1]] if ws is not None else None),
+                                      _split_rows(m.shape[0], threads)))
             partial = np.concatenate([p[0] for p in parts])
             tok = m[:, 0] % num_max_tokens
             slot = np.full(m.shape[0], r) if rank_layout else m[:, 1] % K

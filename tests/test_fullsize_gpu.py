@@ -39,7 +39,7 @@ def _calc_diff(a: torch.Tensor, b: torch.Tensor) -> float:
     return float(1 - 2 * (a * b).sum() / (a * a + b * b).sum())
 
 
-def _rank(rank, world, T_max, H, K, E, skew, fp8, weighted, masked, ragged, comm, shared, results):
+def _rank(rank, world, T_max, H, K, E, skew, fp8, weighted, masked, ragged, expanded, comm, shared, results):
     try:
         torch.cuda.set_device(0)
         from deepep_amd import ElasticBuffer
@@ -83,9 +83,14 @@ def _rank(rank, world, T_max, H, K, E, skew, fp8, weighted, masked, ragged, comm
                         not torch.equal(ex_sf[rows[ok].long()], sf_all[src[ok]]):
                     failures.append(f'fp8 dispatch rows of lane {k}')
             y = per_token_cast_back(ex_q, ex_sf)                  # the expert outputs
-        else:
+        elif expanded:
             _, _, ex_w, handle, _ = buf.dispatch(x, topk_idx=idx, topk_weights=w, num_experts=E, do_expand=True)
             y = torch.randn((handle.num_expanded_tokens, H), device='cuda', generator=g).to(torch.bfloat16)
+        else:
+            # the received-token layout: one row per received token, which the caller has pre-reduced over its
+            # local lanes (test_ep.py:187-195), and its K weights
+            _, _, ex_w, handle, _ = buf.dispatch(x, topk_idx=idx, topk_weights=w, num_experts=E)
+            y = torch.randn((handle.num_recv_tokens, H), device='cuda', generator=g).to(torch.bfloat16)
         b = None if weighted or fp8 else bias
         out, out_w, _ = buf.combine(y, handle, topk_weights=ex_w, bias=b, apply_topk_weights=weighted)
         torch.cuda.synchronize()
@@ -108,12 +113,15 @@ def _rank(rank, world, T_max, H, K, E, skew, fp8, weighted, masked, ragged, comm
             mr = m[sel].copy()
             slots = mr[:, 2:]
             valid = slots >= 0
-            src_rows = torch.from_numpy(slots[valid].astype(np.int64)).cuda()
+            if expanded:
+                src_rows = torch.from_numpy(slots[valid].astype(np.int64)).cuda()
+                new = np.full(slots.shape, -1, np.int32)
+                new[valid] = np.arange(int(valid.sum()), dtype=np.int32)
+                mr[:, 2:] = new
+            else:                                             # row i of the received tokens is x row i
+                src_rows = torch.from_numpy(np.nonzero(sel)[0].astype(np.int64)).cuda()
             x_sub.append(_u16(shared[r]['y'][src_rows]) if src_rows.numel() else np.zeros((0, H), np.uint16))
             w_sub.append(shared[r]['ex_w'][src_rows].cpu().numpy())
-            new = np.full(slots.shape, -1, np.int32)
-            new[valid] = np.arange(int(valid.sum()), dtype=np.int32)
-            mr[:, 2:] = new
             mr[:, 0] = rank * n_s + pos[mr[:, 0] % T_max]
             m_sub.append(mr)
             if weighted:
@@ -123,7 +131,7 @@ def _rank(rank, world, T_max, H, K, E, skew, fp8, weighted, masked, ragged, comm
                     exact.index_add_(0, torch.from_numpy(tok.astype(np.int64)).cuda(),
                                      shared[r]['y'][src_rows].double() * shared[r]['ex_w'][src_rows].double()[:, None])
         bias_sub = (_u16(b[torch.from_numpy(S).cuda()]) if b is not None else None, None)
-        exp, exp_w = oracle.combine_ep_one(rank, x_sub, m_sub, shared[rank]['idx'][S], E, n_s, expanded=True,
+        exp, exp_w = oracle.combine_ep_one(rank, x_sub, m_sub, shared[rank]['idx'][S], E, n_s, expanded=expanded,
                                            topk_weights_per_rank=w_sub, bias=bias_sub, weighted=weighted,
                                            threads=2)
         got = _u16(out[torch.from_numpy(S).cuda()])
@@ -151,7 +159,7 @@ def _rank(rank, world, T_max, H, K, E, skew, fp8, weighted, masked, ragged, comm
         comm.bar.abort()
 
 
-def _run(T, skew=1.0, fp8=False, weighted=False, masked=0.0, ragged=False):
+def _run(T, skew=1.0, fp8=False, weighted=False, masked=0.0, ragged=False, expanded=True):
     import threading
     world, H, K, E = 8, 7168, 8, 256
     torch.cuda.init()                                   # not lazily from 8 threads at once
@@ -159,8 +167,8 @@ def _run(T, skew=1.0, fp8=False, weighted=False, masked=0.0, ragged=False):
     comm = ThreadComm(world)
     comm.lock = threading.Lock()
     shared = {}
-    results = run_threads(world, _rank, (world, T, H, K, E, skew, fp8, weighted, masked, ragged, comm, shared),
-                          timeout=600)
+    results = run_threads(world, _rank, (world, T, H, K, E, skew, fp8, weighted, masked, ragged, expanded, comm,
+                                         shared), timeout=600)
     full = [shared.get(('full_checked', r)) for r in range(world)]
     diffs = [shared.get(('calc_diff', r)) for r in range(world)]
     del shared
@@ -185,6 +193,12 @@ def test_config3_ep8_masked_ragged(weighted):
     """Config 3 with 10 % of the top-k slots masked (-1, weight 0; the reference's --masked-ratio) and
     ragged batches (rank r holds 8192 - r tokens of T_max = 8192, the reference's num_tokens)."""
     _run(8192, weighted=weighted, masked=0.1, ragged=True)
+
+
+def test_config3_ep8_received_token_layout():
+    """Config 3 in the received-token (non-expanded) layout with bias: one pre-reduced row per received token
+    and its K weights (the reference's combine of a `do_expand=False` handle, test_ep.py:187-217)."""
+    _run(8192, expanded=False)
 
 
 def test_config4_ep8_fp8_dispatch_bf16_combine():

@@ -769,6 +769,14 @@ class ElasticBuffer(ExchangeMixin):
                 out_x = out_x[:n_rows]
                 out_sf = out_sf[:n_rows] if out_sf is not None else None
                 out_w = out_w[:n_rows] if out_w is not None else None
+            if out_sf is not None and use_tma_aligned_col_major_sf:
+                # the reference's TMA-aligned column-major scale factors for the next GEMM (buffer.hpp:1090-1096):
+                # packs of consecutive rows adjacent, each pack column starting on 16 bytes
+                n_sf, packs = out_sf.shape
+                col_major = torch.empty_strided((n_sf, packs), (1, align(max(n_sf, 1), max(1, 16 // out_sf.element_size()))),
+                                                dtype=out_sf.dtype, device=dev)
+                col_major.copy_(out_sf)
+                out_sf = col_major
             recv_idx64 = out_idx
             if out_idx is not None and topk_idx.dtype != torch.int64:
                 out_idx = out_idx.to(topk_idx.dtype)

@@ -481,3 +481,62 @@ def test_notify_layout_matches_brute_force():
             assert [s[2] for s in sp] == list(range(R)) and sp[0][0] == 0
             assert all(a[1] == b[0] for a, b in zip(sp, sp[1:]))
             assert sp[-1][1] == int(rec[:, d, 0].sum())
+
+
+def _sf_worker(rank, world, port, queue):
+    import sys
+    sys.path.insert(0, ROOT)
+    try:
+        os.environ['MASTER_ADDR'] = '127.0.0.1'
+        os.environ['MASTER_PORT'] = str(port)
+        dist.init_process_group('gloo', rank=rank, world_size=world)
+        from deepep_amd import ElasticBuffer
+        from tests.oracle_kernels import OracleKernels
+        T, H, K, E = 37, 256, 4, 8 * world
+        g = torch.Generator().manual_seed(rank)
+        idx = torch.stack([torch.randperm(E, generator=g)[:K] for _ in range(T)])
+        w = torch.rand((T, K), generator=g)
+        xq = torch.randn((T, H), generator=g).to(torch.float8_e4m3fn)
+        sf = torch.rand((T, H // 128), generator=g)
+        buf = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=T, hidden=H, num_topk=K)
+        buf._kernels = OracleKernels()
+        failures = []
+        (rq, rsf), _, _, h, _ = buf.dispatch((xq, sf), topk_idx=idx, topk_weights=w, num_experts=E, do_expand=True)
+        for hh in (None, h):
+            args = dict(topk_weights=w, do_expand=True, use_tma_aligned_col_major_sf=True)
+            args.update(handle=hh) if hh is not None else args.update(topk_idx=idx, num_experts=E)
+            (cq, csf), _, _, _, _ = buf.dispatch((xq, sf), **args)
+            n = csf.shape[0]
+            if csf.stride() != (1, (n + 3) // 4 * 4):
+                failures.append(f'scale-factor strides {csf.stride()} (cached {hh is not None})')
+            if not (torch.equal(csf, rsf) and torch.equal(cq.view(torch.uint8), rq.view(torch.uint8))):
+                failures.append(f'column-major dispatch differs (cached {hh is not None})')
+        queue.put((rank, failures))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:
+        queue.put((rank, [traceback.format_exc()]))
+
+
+@pytest.mark.parametrize('world', [1, 2])
+def test_tma_aligned_col_major_scale_factors(world):
+    """dispatch(..., use_tma_aligned_col_major_sf=True) (the reference's layout for the next GEMM,
+    buffer.hpp:1090-1096): the received scale factors are column-major with each pack column 16-byte
+    aligned, and hold the same values as the row-major ones, fresh and cached."""
+    ctx = mp.get_context('spawn')
+    queue = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sf_worker, args=(r, world, port, queue)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = {}
+    try:
+        for _ in range(world):
+            rank, failures = queue.get(timeout=240)
+            results[rank] = failures
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    assert len(results) == world and not any(results.values()), results

@@ -529,6 +529,15 @@ def test_fp8_dispatch_then_bf16_combine():
         ok = rows >= 0
         assert torch.equal(ex_q[rows[ok].long()].view(torch.uint8), xq[0][tok[ok]].view(torch.uint8))
         assert torch.equal(ex_sf[rows[ok].long()], xq[1][tok[ok]])
+    # the reference's TMA-aligned column-major scale factors (its expanded test dispatches with them,
+    # tests/elastic/test_ep.py:157, 174): the same values, packs of consecutive rows adjacent, fresh and cached
+    for h in (None, handle):
+        args = dict(topk_weights=w, do_expand=True, use_tma_aligned_col_major_sf=True)
+        args.update(handle=h) if h is not None else args.update(topk_idx=idx, num_experts=E)
+        (cq, csf), _, _, _, _ = buf.dispatch(xq, **args)
+        n = csf.shape[0]
+        assert csf.stride() == (1, (n + 3) // 4 * 4), csf.stride()
+        assert torch.equal(csf, ex_sf) and torch.equal(cq.view(torch.uint8), ex_q.view(torch.uint8))
     y = per_token_cast_back(ex_q, ex_sf)                     # "expert output" = dequantised input
     out, out_w, _ = buf.combine(y, handle, topk_weights=ex_w)
     torch.cuda.synchronize()

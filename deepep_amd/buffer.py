@@ -437,6 +437,34 @@ class ElasticBuffer(ExchangeMixin):
         (`handle=...`) needs no sync.
         The notify also carries per-64-token-block counts, so the handle's combines never sync."""
         check_torch_deterministic()
+        args = (x, topk_idx, topk_weights, cumulative_local_expert_recv_stats, num_experts, num_max_tokens_per_rank,
+                expert_alignment, num_sms, num_qps, previous_event, previous_event_before_epilogue,
+                async_with_compute_stream, allocate_on_comm_stream, handle, do_handle_copy, do_cpu_sync, do_expand,
+                do_zero_padding, use_tma_aligned_col_major_sf)
+        # An explicit num_sms below the CU count: the dispatch's kernels run on a stream restricted to that many
+        # CUs (the reference sizes its dispatch grids with num_sms), the rest stay free for compute -- as the
+        # combine (combine() below); that stream plays the comm stream, so the call takes the async-capable path.
+        budget = self._cu_budget_stream(num_sms)
+        if budget is not None and self.use_cuda and torch.cuda.current_stream() == budget:
+            budget = None
+        if budget is None:
+            return self._dispatch(*args)
+        capturing = torch.cuda.is_current_stream_capturing()
+        saved, self.comm_stream = self.comm_stream, budget
+        if not capturing:
+            budget.wait_stream(saved)
+        try:
+            return self._dispatch(*args, force_comm_stream=True)
+        finally:
+            self.comm_stream = saved
+            if not capturing:
+                saved.wait_stream(budget)
+
+    def _dispatch(self, x, topk_idx, topk_weights, cumulative_local_expert_recv_stats, num_experts,
+                  num_max_tokens_per_rank, expert_alignment, num_sms, num_qps, previous_event,
+                  previous_event_before_epilogue, async_with_compute_stream, allocate_on_comm_stream, handle,
+                  do_handle_copy, do_cpu_sync, do_expand, do_zero_padding, use_tma_aligned_col_major_sf,
+                  force_comm_stream: bool = False):
         num_topk = (handle.topk_idx if topk_idx is None else topk_idx).shape[1]
         num_sms = self.get_theoretical_num_sms(num_experts or handle.num_experts, num_topk) if num_sms == 0 else num_sms
         num_qps = self.get_theoretical_num_qps(num_sms) if num_qps == 0 else num_qps
@@ -474,7 +502,7 @@ class ElasticBuffer(ExchangeMixin):
         # a call that neither overlaps nor waits on events runs on the caller's stream (as the combine:
         # the same ordering without the two cross-stream hops)
         sync_mode = self._sync_mode(previous_event, previous_event_before_epilogue, async_with_compute_stream,
-                                    allocate_on_comm_stream)
+                                    allocate_on_comm_stream) and not force_comm_stream
         compute_stream = None if sync_mode else self._prologue(previous_event, allocate_on_comm_stream)
         kern = self.kernels
         with (self._null_ctx() if sync_mode else self._stream_ctx()):

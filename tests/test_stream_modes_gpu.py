@@ -167,7 +167,7 @@ def test_cu_budget_is_honoured_and_bitwise(num_sms, expect_cus):
     """An explicit num_sms is rounded up to whole CUs per XCD (a CU mask without bits on an XCD would
     leave that XCD unrestricted): the budget stream's workgroups run on exactly that many CUs, spread
     over all 8 XCDs; the combine on it -- from the default stream, and issued from the budget stream
-    itself (no stream hops) -- is bitwise the whole-chip combine."""
+    itself (no stream hops) -- is bitwise the whole-chip combine; so is a dispatch with that num_sms."""
     import ctypes
     import torch.distributed as dist
     from deepep_amd import ElasticBuffer
@@ -193,6 +193,16 @@ def test_cu_budget_is_honoured_and_bitwise(num_sms, expect_cus):
     torch.cuda.synchronize()
     assert torch.equal(out, ref) and torch.equal(out_w, ref_w)
     assert torch.equal(out2, ref) and torch.equal(out2_w, ref_w)
+    # the dispatch honours an explicit num_sms the same way (the reference sizes its dispatch grids with it):
+    # fresh and cached, bitwise the whole-chip dispatch
+    x = torch.randn((T, H), device='cuda', generator=g).to(torch.bfloat16)
+    args = dict(topk_idx=idx.to(torch.int64), topk_weights=w, num_experts=E, do_expand=True)
+    rx, _, rw, rh, _ = buf.dispatch(x, **args)
+    bx, _, bw, bh, _ = buf.dispatch(x, num_sms=num_sms, **args)
+    cx, _, cw, _, _ = buf.dispatch(x, topk_weights=w, do_expand=True, handle=rh, num_sms=num_sms)
+    torch.cuda.synchronize()
+    assert torch.equal(bx, rx) and torch.equal(bw, rw) and torch.equal(bh.recv_src_metadata, rh.recv_src_metadata)
+    assert torch.equal(cx, rx) and torch.equal(cw, rw)
 
 
 @pytest.mark.parametrize('world', [1, 4])

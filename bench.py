@@ -228,6 +228,9 @@ SOFT_BUDGET_S = float(os.environ.get('DEEPEP_BENCH_SOFT_S', 300))
 HARD_DEADLINE_S = float(os.environ.get('DEEPEP_BENCH_HARD_S', 480))
 
 
+_LINE = [None]          # rank 0's line once the headline is measured (emitted if a later leg raises)
+
+
 class _Line:
     """Rank 0's result line, filled leg by leg; `emit()` prints it once (normally at the end, or from the
     watchdog at the hard deadline with `incomplete` naming the leg that was running)."""
@@ -781,6 +784,7 @@ def main():
     ms_per_step = elapsed * 1e3 / args.steps
 
     line = _Line(rank)
+    _LINE[0] = line
     res = dict(roofline=None, cpu_baseline=None, cpu_torch=None, loopback=None, phases=None, su_bandwidth=None,
                rccl=None, xgmi=None, single_reduction=None, fastest_leg=None, dispatch=None)
 
@@ -1190,5 +1194,17 @@ def main():
     dist.destroy_process_group()
 
 
+def _entry() -> None:
+    """main(); an exception after the headline was measured still prints rank 0's line (with `incomplete`
+    naming the leg), then propagates."""
+    try:
+        main()
+    except Exception as e:                  # noqa: BLE001 -- the measured fields still reach the driver
+        if _LINE[0] is not None:
+            _LINE[0].emit(incomplete=f'leg "{_LINE[0].leg}" raised {type(e).__name__}: {e}; the fields '
+                                     f'present were measured before it')
+        raise
+
+
 if __name__ == '__main__':
-    main()
+    _entry()

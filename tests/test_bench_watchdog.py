@@ -1,7 +1,8 @@
 """The N > 1 bench's safety net (bench.py `_Line`): a secondary leg that hangs on a real node must not cost
 the line.  At the hard deadline the watchdog prints the line built so far -- with `incomplete` naming the
 leg that was running and `skipped_legs` -- and ends the rank with status 0; the line is printed once even if
-the run then finishes normally.  CPU only (no GPU is touched)."""
+the run then finishes normally.  A leg that raises still prints the line (then the error propagates).
+CPU only (no GPU is touched)."""
 import json
 import os
 import subprocess
@@ -49,3 +50,29 @@ def test_line_is_printed_once_when_the_run_finishes_first():
     assert r.returncode == 0, r.stderr
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith('{')]
     assert len(lines) == 1 and 'incomplete' not in json.loads(lines[0]) and 'normal end' in r.stdout
+
+
+_RAISE = r'''
+import sys
+sys.path.insert(0, {root!r})
+import bench
+
+def fake_main():
+    line = bench._Line(0)
+    bench._LINE[0] = line
+    line.fields = {{'metric': 'm', 'value': 2.0, 'launch': {{}}}}
+    line.leg = 'dispatch'
+    raise RuntimeError('boom')
+
+bench.main = fake_main
+bench._entry()
+'''
+
+
+def test_a_leg_that_raises_still_prints_the_line():
+    r = subprocess.run([sys.executable, '-c', _RAISE.format(root=ROOT)], capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and 'RuntimeError: boom' in r.stderr, r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith('{')]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d['value'] == 2.0 and 'dispatch' in d['incomplete'] and 'boom' in d['incomplete'], d

@@ -37,7 +37,7 @@ def _case(seed: int):
 
 
 @pytest.fixture(params=[(0, 0), (1, 8), (2, 2)], ids=['auto', 'vpt1_rows8', 'vpt2_rows2'])
-def kernel_choice(request):
+def launch_shape(request):
     """The automatic launch shape and two forced ones (deepep_set_launch_config: vectors per lane, rows in
     flight): every shape gives the same bits."""
     from deepep_amd import _lib
@@ -58,7 +58,7 @@ def group():
 
 
 @pytest.mark.parametrize('seed', range(32))
-def test_random_shapes_ep1(group, seed, kernel_choice):
+def test_random_shapes_ep1(group, seed, launch_shape):
     from deepep_amd import ElasticBuffer
     rng, T, H, K, E, masked = _case(seed)
     idx = np.array([rng.permutation(E)[:K] for _ in range(T)], dtype=np.int64).reshape(T, K)
@@ -202,7 +202,7 @@ def _ep_thread(rank, world, seed, comm, results):
 
 
 @pytest.mark.parametrize('case', range(16))
-def test_random_shapes_ep_sim(case, monkeypatch, kernel_choice):
+def test_random_shapes_ep_sim(case, monkeypatch, launch_shape):
     """Random EP = 2..8 cases (ragged per-rank batches incl. empty ranks, top-k 1..8, R > K and
     R <= K layouts, chunked and one-shot exchange), all ranks simulated by threads on the GPU."""
     import threading

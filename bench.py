@@ -841,7 +841,7 @@ def main():
         # the reference's protocol (deep_ep/utils/testing.py:12-21, bench_kineto): a 256 MB+ cache flush
         # before every launch, each launch timed alone (here: 512 MB written, HIP events around the kernel)
         # The write flush leaves up to the caches' size of dirty lines that this launch then writes
-        # back (tools/kflush.py: +11 us on one box, and no change after a 200 us idle); a read flush
+        # back (round-4 probe, CHANGELOG.md: +11 us on one box, and no change after a 200 us idle); a read flush
         # (a reduction over the same 512 MB) evicts as much without dirtying, so it isolates the kernel.
         flush = torch.empty((512 << 20) // 4, dtype=torch.int32, device=dev)
         sink = torch.empty((), dtype=torch.int64, device=dev)
@@ -874,7 +874,7 @@ def main():
         torch.cuda.synchronize()
         copy_gbps = 2 * y.numel() * 2 * 5 / (c0.elapsed_time(c1) * 1e-3) / 1e9
         del dst
-        # same-run layout reference (tools/klayout.py): the same kernel over the same rows with each token's
+        # same-run layout reference (round-4 probe, CHANGELOG.md): the same kernel over the same rows with each token's
         # K rows adjacent ([T, K] placement) instead of grouped by expert -- what the kernel reaches when
         # the rows a workgroup reads at once are one contiguous run; output checked bit for bit
         token_major = None

@@ -112,7 +112,7 @@ def packed_row_layout(hidden: int, num_topk: int, with_weights: bool = True, sin
     """(row_bytes, weights_offset, weights_pad_floats) of a packed exchange row [bf16 row | fp32
     weights]: the bf16 part and the weight tail each a whole number of 128-byte lines, so every row
     starts on a line and the tail is written as full lines (zeros past the weights).  Measured on
-    EP = 8's phase A (tools/kphase.py): 32-byte aligned rows with a 32-byte weight tail 303 us,
+    EP = 8's phase A (round 2, CHANGELOG.md): 32-byte aligned rows with a 32-byte weight tail 303 us,
     line-aligned rows with a partial tail line 281 us, line-aligned rows without a tail 257 us.
     single: one weight per row (the single reduction), else num_topk."""
     w_off = align(hidden * 2, LINE_BYTES)

@@ -128,7 +128,7 @@ def test_kernel_units_per_block(kern, upb):
 @pytest.mark.parametrize('upb', [0, 4, 8])
 def test_kernel_launch_configs_identical(kern, cfg, upb):
     """Every deepep_set_launch_config variant (vectors per lane, rows in flight) and workgroup shape
-    gives the same bits (the tuning knobs of tools/kshapes.py)."""
+    gives the same bits (deepep_set_launch_config, the diagnostic launch-shape knob)."""
     assert kern.lib.deepep_set_launch_config(*cfg) == 0
     try:
         for mode in (MODE_LOCAL, MODE_EPILOGUE, MODE_FUSED):

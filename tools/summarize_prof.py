@@ -212,37 +212,9 @@ def step(out, meta_json, *paths):
     print(json.dumps(summary, indent=1))
 
 
-def policy(out, meta_json, *paths):
-    """Phase A under its store policies (tools/pmc_policy.py): the mean counter values and durations of each
-    policy's launches (told apart by the store-policy template argument in the kernel name)."""
-    meta = json.load(open(meta_json))
-    names = {', 16, ': 'sc1', ', 18, ': 'sc1 nt', ', 1003, ': 'per unit'}
-    res = defaultdict(lambda: defaultdict(list))
-    for path in paths:
-        for r in csv.DictReader(open(path)):
-            if 'combine_rows_kernel<0' not in r['Kernel_Name']:
-                continue
-            pol = next((v for k, v in names.items() if k in r['Kernel_Name']), None)
-            if pol is None:
-                continue
-            res[pol][r['Counter_Name']].append(float(r['Counter_Value']))
-            res[pol]['duration_us'].append((int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3)
-    summary = {pol: {c: sum(v) / len(v) for c, v in cs.items()} for pol, cs in res.items()}
-    for pol, cs in summary.items():
-        if 'FETCH_SIZE' in cs and 'WRITE_SIZE' in cs:
-            cs['hbm_bytes'] = 2 * cs['FETCH_SIZE'] * 1024 + cs['WRITE_SIZE'] * 1024
-            cs['traffic_over_algorithmic'] = cs['hbm_bytes'] / meta['bytes']
-        if 'TCC_HIT_sum' in cs and 'TCC_MISS_sum' in cs:
-            cs['l2_hit_rate'] = cs['TCC_HIT_sum'] / max(1.0, cs['TCC_HIT_sum'] + cs['TCC_MISS_sum'])
-    json.dump(dict(meta=meta, policies=summary), open(out, 'w'), indent=1)
-    print(json.dumps(dict(meta=meta, policies=summary), indent=1))
-
-
 if __name__ == '__main__':
     if sys.argv[1] == 'step':
         step(sys.argv[2], sys.argv[3], *sys.argv[4:])
-    elif sys.argv[1] == 'policy':
-        policy(sys.argv[2], sys.argv[3], *sys.argv[4:])
     elif sys.argv[1] == 'ep':
         pmc_ep(sys.argv[2], sys.argv[3], *sys.argv[4:])
     elif sys.argv[1] == 'phases':

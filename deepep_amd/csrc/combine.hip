@@ -368,7 +368,7 @@ combine_rows_kernel(const Params p) {
 // CU-budget streams created by deepep_stream_create_cu_budget (symmetric.hip) and their CU counts: a
 // launch on one keeps its full grid (the CU mask alone holds it to the budget) with at most 4 rows in
 // flight per lane -- 64 VGPRs, 8 waves per SIMD, more bytes in flight per budgeted CU than 8 rows at 5
-// waves (config 2: 128 CUs 208 vs 235 us, 32 CUs 603 vs 661 us, profiles/r02n_kcu2.jsonl).
+// waves (config 2: 128 CUs 208 vs 235 us, 32 CUs 603 vs 661 us, profiles/archive/r02n_kcu2.jsonl).
 std::mutex g_budget_mutex;
 std::map<hipStream_t, int> g_budget_cus;
 
@@ -617,7 +617,7 @@ namespace {
 int launch_combine(int mode, int weighted, const Params& p, deepep_stream_t stream) {
     // Launch shape: one wave per (unit, 64 x vpt x 16-byte column chunk) item, `waves` items per
     // workgroup, `group` source rows loaded per lane before any is accumulated.  Measured per shape
-    // class (tools/kshapes.py, tools/kphase_a.py, tools/kphase_b.py):
+    // class (launch-shape sweeps of rounds 2-4: DESIGN.md section 3, CHANGELOG.md):
     //   fused reduce over top-k >= 5, rows >= 256 vectors: 1 KiB chunks, 2 rows, 4 waves -- few registers,
     //     many waves (config 2: -0.9 to -1.6 % against 2 KiB / 8 rows / 8 waves on three boxes);
     //   fused over top-k >= 5, rows of 128-255 vectors: 2 KiB chunks, 4 rows, 8 waves;

@@ -618,7 +618,7 @@ copy_kernel(const uint8_t* __restrict__ packed, int64_t row_bytes, int x_bytes, 
 // and reads their sources through inv.  The block's source rows (1.8 MB) are read once from HBM and
 // re-read -- once per local expert of each row -- from the L2 of the one XCD that owns the block
 // (workgroups w = x (mod 8) run on XCD x and take blocks x, x + 8, ...).  Stores are streaming
-// write-through (sc1 nt).  Measured at BASELINE config 2 (tools/probe_copy.py, two boxes): 151.4 vs
+// write-through (sc1 nt).  Measured at BASELINE config 2 (round-3 probe, CHANGELOG.md; two boxes): 151.4 vs
 // 163.5 us and 182.0 vs 213.6 us for the source-major copy (one load, up to K scattered stores).
 constexpr int kCopyAux = 18;                          // sc1 | nt
 

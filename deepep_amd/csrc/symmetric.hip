@@ -258,7 +258,7 @@ int deepep_stream_create_cu_budget(int num_cus, deepep_stream_t* stream) {
     hipStream_t s = nullptr;
     e = hipExtStreamCreateWithCUMask(&s, static_cast<uint32_t>(words), mask);
     if (e != hipSuccess) return hip_fail(e, "hipExtStreamCreateWithCUMask");
-    deepep_amd_register_budget(s, num_cus);          // combine launches on it size a persistent grid to it
+    deepep_amd_register_budget(s, num_cus);          // combine launches on it cap rows in flight at 4
     *stream = reinterpret_cast<deepep_stream_t>(s);
     return DEEPEP_OK;
 }

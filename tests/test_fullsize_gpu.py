@@ -10,6 +10,8 @@ dispatch and the pipelined (4-chunk) combine.
       every expanded FP8 row is checked against its source token, the dequantised rows are the
       expert outputs the combine reduces
   C5  8 x 16384 tokens, skewed routing (get_unbalanced_scores, rank 0's experts ~4x the tokens)
+  the reference test's default: 8 x 4096 ragged tokens, top-6 (fewer top-k lanes than ranks: the top-k
+      receive layout), 0 or 2 biases, both layouts
 
 The reference's own test checks every rank's whole output bitwise at 4096 tokens x 7168 x top-6
 across 8 ranks (tests/elastic/test_ep.py:502-511, 577-580).  Here too: EVERY rank's whole combined_x
@@ -39,7 +41,7 @@ def _calc_diff(a: torch.Tensor, b: torch.Tensor) -> float:
     return float(1 - 2 * (a * b).sum() / (a * a + b * b).sum())
 
 
-def _rank(rank, world, T_max, H, K, E, skew, fp8, weighted, masked, ragged, expanded, comm, shared, results):
+def _rank(rank, world, T_max, H, K, E, skew, fp8, weighted, masked, ragged, expanded, num_bias, comm, shared, results):
     try:
         torch.cuda.set_device(0)
         from deepep_amd import ElasticBuffer
@@ -61,7 +63,7 @@ def _rank(rank, world, T_max, H, K, E, skew, fp8, weighted, masked, ragged, expa
             w = w.masked_fill(idx < 0, 0)
         w = w.contiguous()
         x = torch.randn((T, H), device='cuda', generator=g).to(torch.bfloat16)
-        bias = torch.randn((T, H), device='cuda', generator=g).to(torch.bfloat16)
+        biases = [torch.randn((T, H), device='cuda', generator=g).to(torch.bfloat16) for _ in range(num_bias)]
         buf = ElasticBuffer(FakeGroup(rank, world, comm), num_max_tokens_per_rank=T_max, hidden=H, num_topk=K)
         comm.install(buf, rank)
         failures = []
@@ -91,7 +93,7 @@ def _rank(rank, world, T_max, H, K, E, skew, fp8, weighted, masked, ragged, expa
             # local lanes (test_ep.py:187-195), and its K weights
             _, _, ex_w, handle, _ = buf.dispatch(x, topk_idx=idx, topk_weights=w, num_experts=E)
             y = torch.randn((handle.num_recv_tokens, H), device='cuda', generator=g).to(torch.bfloat16)
-        b = None if weighted or fp8 else bias
+        b = None if weighted or fp8 or not biases else (biases[0] if len(biases) == 1 else tuple(biases))
         out, out_w, _ = buf.combine(y, handle, topk_weights=ex_w, bias=b, apply_topk_weights=weighted)
         torch.cuda.synchronize()
         if getattr(buf, '_stream_b', None) is None:          # made by the pipelined schedule only
@@ -130,7 +132,8 @@ def _rank(rank, world, T_max, H, K, E, skew, fp8, weighted, masked, ragged, expa
                 if src_rows.numel():
                     exact.index_add_(0, torch.from_numpy(tok.astype(np.int64)).cuda(),
                                      shared[r]['y'][src_rows].double() * shared[r]['ex_w'][src_rows].double()[:, None])
-        bias_sub = (_u16(b[torch.from_numpy(S).cuda()]) if b is not None else None, None)
+        bl = [] if b is None else ([b] if isinstance(b, torch.Tensor) else list(b))
+        bias_sub = tuple(_u16(t[torch.from_numpy(S).cuda()]) for t in bl) + (None,) * (2 - len(bl))
         exp, exp_w = oracle.combine_ep_one(rank, x_sub, m_sub, shared[rank]['idx'][S], E, n_s, expanded=expanded,
                                            topk_weights_per_rank=w_sub, bias=bias_sub, weighted=weighted,
                                            threads=2)
@@ -159,16 +162,16 @@ def _rank(rank, world, T_max, H, K, E, skew, fp8, weighted, masked, ragged, expa
         comm.bar.abort()
 
 
-def _run(T, skew=1.0, fp8=False, weighted=False, masked=0.0, ragged=False, expanded=True):
+def _run(T, skew=1.0, fp8=False, weighted=False, masked=0.0, ragged=False, expanded=True, K=8, num_bias=1):
     import threading
-    world, H, K, E = 8, 7168, 8, 256
+    world, H, E = 8, 7168, 256
     torch.cuda.init()                                   # not lazily from 8 threads at once
     torch.cuda.get_device_properties(0)
     comm = ThreadComm(world)
     comm.lock = threading.Lock()
     shared = {}
-    results = run_threads(world, _rank, (world, T, H, K, E, skew, fp8, weighted, masked, ragged, expanded, comm,
-                                         shared), timeout=600)
+    results = run_threads(world, _rank, (world, T, H, K, E, skew, fp8, weighted, masked, ragged, expanded, num_bias,
+                                         comm, shared), timeout=600)
     full = [shared.get(('full_checked', r)) for r in range(world)]
     diffs = [shared.get(('calc_diff', r)) for r in range(world)]
     del shared
@@ -199,6 +202,16 @@ def test_config3_ep8_received_token_layout():
     """Config 3 in the received-token (non-expanded) layout with bias: one pre-reduced row per received token
     and its K weights (the reference's combine of a `do_expand=False` handle, test_ep.py:187-217)."""
     _run(8192, expanded=False)
+
+
+@pytest.mark.parametrize('expanded,num_bias', [(True, 0), (True, 2), (False, 2)],
+                         ids=['expanded_no_bias', 'expanded_two_biases', 'received_token_two_biases'])
+def test_reference_default_ep8_4096_top6(expanded, num_bias):
+    """The reference's own test at its default size (tests/elastic/test_ep.py:577-580: 4096 tokens x 7168 x
+    top-6 over 256 experts, 8 ranks, rank r holding max(1, 4096 - r) tokens, :62) with 0 or 2 biases (:96-98):
+    top-6 < 8 ranks, so the receive slots are per top-k lane (use_rank_layout false, combine_utils.cuh:8-18)
+    -- the top-k layout at full size."""
+    _run(4096, ragged=True, expanded=expanded, K=6, num_bias=num_bias)
 
 
 def test_config4_ep8_fp8_dispatch_bf16_combine():

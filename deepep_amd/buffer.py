@@ -260,13 +260,37 @@ class ElasticBuffer(ExchangeMixin):
         return BUFFER_ALIGNMENT
 
     def barrier(self, use_comm_stream: bool = True, with_cpu_sync: bool = False, sequential: bool = True) -> None:
+        """A GPU-level barrier across all ranks (elastic.py:497-508, buffer.hpp:181-208), ordered on the comm
+        stream -- which first waits for the current stream, and which the current stream then waits for -- or
+        on the current stream.  The host blocks only with `with_cpu_sync` (a device synchronize before and
+        after).  The device barrier is the xGMI windows' (deepep_sym_barrier: device-counted epochs, the
+        window's timeout and error record) once this buffer has a window, else a one-element RCCL all-reduce
+        on that stream; a host-side group (gloo) gets a host barrier.  `sequential` (scale-out vs scale-up
+        order) has no meaning on one node's single fabric."""
+        self._note_capture()
         if with_cpu_sync and self.use_cuda:
             torch.cuda.synchronize()
-        if self.use_cuda and use_comm_stream:
-            with torch.cuda.stream(self.comm_stream):
-                dist.barrier(group=self.group)
-        else:
+        rccl = isinstance(self.group, dist.ProcessGroup) and dist.get_backend(self.group) == 'nccl'
+        if self.use_cuda and (self._sym is not None or rccl):
+            compute = torch.cuda.current_stream()
+            stream = self.comm_stream if use_comm_stream else compute
+            if stream != compute:
+                stream.wait_stream(compute)
+            if self._sym is not None:
+                if not self._capturing:
+                    self._sym.poll()                  # an earlier barrier timed out: raise now
+                self._sym.barrier(stream)
+                if not self._capturing:
+                    self._sym.publish(stream)
+            else:
+                with torch.cuda.stream(stream):
+                    dist.all_reduce(torch.zeros(1, dtype=torch.int32, device=self.device), group=self.group)
+            if stream != compute:
+                compute.wait_stream(stream)
+        elif isinstance(self.group, dist.ProcessGroup):
             dist.barrier(group=self.group)
+        else:
+            self.group.barrier()
         if with_cpu_sync and self.use_cuda:
             torch.cuda.synchronize()
 

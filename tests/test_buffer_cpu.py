@@ -540,3 +540,45 @@ def test_tma_aligned_col_major_scale_factors(world):
             if p.is_alive():
                 p.kill()
     assert len(results) == world and not any(results.values()), results
+
+
+def _barrier_worker(rank, world, port, queue):
+    import sys
+    import time
+    sys.path.insert(0, ROOT)
+    try:
+        os.environ['MASTER_ADDR'] = '127.0.0.1'
+        os.environ['MASTER_PORT'] = str(port)
+        dist.init_process_group('gloo', rank=rank, world_size=world)
+        from deepep_amd import ElasticBuffer
+        buf = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=16, hidden=64, num_topk=2)
+        waited = []
+        for kw in (dict(), dict(use_comm_stream=False), dict(with_cpu_sync=True), dict(sequential=False)):
+            dist.barrier()
+            if rank == 0:
+                time.sleep(0.4)                            # the last rank to arrive
+            t0 = time.perf_counter()
+            buf.barrier(**kw)
+            waited.append(time.perf_counter() - t0)
+        queue.put((rank, waited))
+        dist.destroy_process_group()
+    except Exception:
+        queue.put((rank, traceback.format_exc()))
+
+
+def test_barrier_waits_for_every_rank():
+    """ElasticBuffer.barrier (elastic.py:497-508) on a host-side group: every argument form returns on a rank
+    only once the last rank has arrived."""
+    world = 3
+    ctx = mp.get_context('spawn')
+    queue = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_barrier_worker, args=(r, world, port, queue)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(queue.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=30)
+    assert all(isinstance(v, list) for v in res.values()), res
+    for r in range(1, world):
+        assert all(t > 0.3 for t in res[r]), (r, res[r])

@@ -24,6 +24,10 @@ def get_logical_domain_size(group=None, allow_hybrid_mode: bool = True):
     return 1, n
 
 
-__version__ = '0.1.0'
+# The API level implemented: the reference's deep_ep.__version__ (deep_ep/__init__.py:97), so caller
+# code that gates on it sees the library it was written against.  This build's own version is
+# __build_version__; the library's source hash is deepep_amd._lib.source_build_id().
+__version__ = '2.1.0'
+__build_version__ = '0.6.0'
 __all__ = ['ElasticBuffer', 'EPHandle', 'EventOverlap', 'EventHandle', 'topk_idx_t',
            'calculate_buffer_size', 'get_physical_domain_size', 'get_logical_domain_size']

@@ -143,3 +143,14 @@ def test_header_is_plain_c():
     r = subprocess.run(['gcc', '-std=c11', '-Wall', '-Wextra', '-Werror', '-D__HIP_PLATFORM_AMD__',
                         '-I/opt/rocm/include', '-fsyntax-only', g.C_CONSUMER + '.c'], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
+
+
+def test_reference_version_and_alias():
+    """`import deep_ep` reports the reference's API level (deep_ep/__init__.py:97) and its classes are
+    this build's; the build's own version stays available beside it."""
+    import deep_ep
+    import deepep_amd
+    assert deep_ep.__version__ == '2.1.0'
+    assert deep_ep.ElasticBuffer is deepep_amd.ElasticBuffer
+    assert deep_ep.EPHandle is deepep_amd.EPHandle
+    assert deepep_amd.__build_version__ != deep_ep.__version__

@@ -4,9 +4,15 @@ the last rank's stream arrives.
 
   rccl   one rank over a real RCCL group: the barrier is queued behind the caller's work and returns to the
          host at once; with_cpu_sync makes the host wait
-  xgmi   2 processes sharing the GPU over HIP-IPC windows: rank 0's stream is held by a long device sleep
+  xgmi   2 processes sharing the GPU over HIP-IPC windows: rank 0's stream is held by a long device spin
          before its barrier; rank 1's barrier returns to the host at once, but its stream passes the barrier
-         only after rank 0's sleep (the windows' device barrier, deepep_sym_barrier)
+         only after rank 0's spin (the windows' device barrier, deepep_sym_barrier)
+
+Ordering is proven on the device: kernels of tests/probe/libstamp.so store the GPU's constant 100 MHz clock
+(wall_clock64, one counter for every process on the GPU) when a stream reaches them -- at the end of the
+pre-barrier spin and right after the barrier -- so "rank 1 passed the barrier after rank 0's work ended" is a
+comparison of two device timestamps, not of host wall-clock ratios.  The spin is in that clock too, so its
+length does not depend on the shader clock.  The host-returned-early checks stay host-timed.
 """
 import os
 import socket
@@ -21,8 +27,8 @@ import torch.multiprocessing as mp
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SLEEP_S = 0.3
-MIN_S = 0.05                   # the device sleep must be long enough to time on the host
+SPIN_S = 0.3                   # the pre-barrier device spin (wall-clock time)
+STAMP_LIB = os.path.join(ROOT, 'tests', 'probe', 'libstamp.so')
 
 
 def _free_port() -> int:
@@ -31,27 +37,50 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _sleep_cycles(seconds: float) -> int:
-    """torch.cuda._sleep cycles for about `seconds` on this device (measured)."""
-    n = 1_000_000
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    torch.cuda._sleep(n)                                   # warm-up
-    e0.record()
-    torch.cuda._sleep(n)
-    e1.record()
-    torch.cuda.synchronize()
-    return max(1, int(n * seconds * 1e3 / max(e0.elapsed_time(e1), 1e-3)))
+class _Clock:
+    """Device clock probes: stamp(i, stream) stores the GPU clock into slot i when `stream` reaches it;
+    spin(seconds, i, stream) holds the stream for that long in wall-clock time, then stamps slot i."""
+
+    def __init__(self, n: int = 16):
+        import ctypes
+        self.lib = ctypes.CDLL(STAMP_LIB)
+        self.lib.stamp_clock.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        self.lib.spin_ticks.argtypes = [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
+        self.hz = self.lib.clock_rate_khz() * 1000
+        assert self.hz > 0
+        self.slots = torch.zeros(n, dtype=torch.int64, device='cuda')
+
+    def _ptr(self, i):
+        return self.slots.data_ptr() + 8 * i
+
+    def stamp(self, i, stream=None):
+        stream = stream or torch.cuda.current_stream()
+        assert self.lib.stamp_clock(self._ptr(i), stream.cuda_stream) == 0
+
+    def spin(self, seconds, i, stream=None):
+        stream = stream or torch.cuda.current_stream()
+        assert self.lib.spin_ticks(int(seconds * self.hz), self._ptr(i), stream.cuda_stream) == 0
+
+    def seconds(self):
+        """All slots as seconds of the device clock."""
+        return [v / self.hz for v in self.slots.cpu().tolist()]
 
 
-def _timed_barrier(buf, cycles, **kw):
-    """(host seconds until barrier() returned, seconds until the device passed it), with `cycles` of device
-    sleep queued before it on the current stream (0: none)."""
+def _timed_barrier(buf, clock, spin: bool, base: int, **kw):
+    """Slots base+0: end of the pre-barrier spin (or a stamp with no spin), base+1: the current stream right
+    after the barrier, base+2: the comm stream right after it.  Returns (host seconds until barrier()
+    returned, host seconds until the device had passed it)."""
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    if cycles:
-        torch.cuda._sleep(cycles)
+    if spin:
+        clock.spin(SPIN_S, base)
+    else:
+        clock.stamp(base)
     buf.barrier(**kw)
     t_call = time.perf_counter() - t0
+    clock.stamp(base + 1)
+    if kw.get('use_comm_stream', True):
+        clock.stamp(base + 2, buf.comm_stream)
     torch.cuda.synchronize()
     return t_call, time.perf_counter() - t0
 
@@ -68,10 +97,11 @@ def _rccl_worker(port, queue):
         buf = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=16, hidden=64, num_topk=2)
         buf.barrier()                                      # the communicator's first use
         torch.cuda.synchronize()
-        cycles = _sleep_cycles(SLEEP_S)
-        res = {name: _timed_barrier(buf, cycles, **kw) for name, kw in
-               (('comm_stream', {}), ('current_stream', dict(use_comm_stream=False)),
-                ('cpu_sync', dict(with_cpu_sync=True)))}
+        clock = _Clock()
+        res = {name: _timed_barrier(buf, clock, True, 3 * i, **kw) for i, (name, kw) in
+               enumerate((('comm_stream', {}), ('current_stream', dict(use_comm_stream=False)),
+                          ('cpu_sync', dict(with_cpu_sync=True))))}
+        res['stamps'] = clock.seconds()
         queue.put(res)
         dist.destroy_process_group()
     except Exception:
@@ -90,12 +120,19 @@ def test_rccl_barrier_is_stream_ordered():
         if p.is_alive():
             p.kill()
     assert isinstance(res, dict), res
-    # relative to each run's own device time (the sleep counts shader clocks, which vary with the clock)
-    for name in ('comm_stream', 'current_stream'):
+    st = res['stamps']
+    for i, name in enumerate(('comm_stream', 'current_stream', 'cpu_sync')):
+        spin_end, after_cur, after_comm = st[3 * i:3 * i + 3]
+        # device order: the stream passed the barrier after the caller's pre-barrier work had ended
+        assert after_cur >= spin_end, (name, st)
+        if name != 'current_stream':
+            assert after_comm >= spin_end, (name, st)      # the comm stream waited for the caller's stream
         t_call, t_done = res[name]
-        assert t_done > MIN_S and t_call < 0.5 * t_done, (name, res)           # queued, not waited for
-    t_call, t_done = res['cpu_sync']
-    assert t_done > MIN_S and t_call > 0.9 * t_done, res                        # with_cpu_sync: the host waits
+        assert t_done > 0.9 * SPIN_S, (name, res)
+        if name == 'cpu_sync':
+            assert t_call > 0.9 * SPIN_S, res              # with_cpu_sync: the host waits
+        else:
+            assert t_call < 0.5 * SPIN_S, (name, res)      # queued, not waited for
 
 
 def _xgmi_worker(rank, world, port, queue):
@@ -117,12 +154,13 @@ def _xgmi_worker(rank, world, port, queue):
         ex_x, _, _, handle, _ = buf.dispatch(x, topk_idx=idx, num_experts=E, do_expand=True)
         buf.combine(ex_x, handle)                          # the window exists from here on
         assert buf._sym is not None
-        cycles = _sleep_cycles(SLEEP_S)
+        clock = _Clock()
         res = {}
-        for name, kw in (('comm_stream', {}), ('current_stream', dict(use_comm_stream=False))):
+        for i, (name, kw) in enumerate((('comm_stream', {}), ('current_stream', dict(use_comm_stream=False)))):
             torch.cuda.synchronize()
             dist.barrier()                                 # both ranks start together
-            res[name] = _timed_barrier(buf, cycles if rank == 0 else 0, **kw)
+            res[name] = _timed_barrier(buf, clock, rank == 0, 3 * i, **kw)
+        res['stamps'] = clock.seconds()
         # the windows still serve a combine after the barriers (epochs agree on every rank)
         out, _, _ = buf.combine(ex_x, handle)
         ref, _, _ = buf.combine(ex_x, handle)
@@ -156,10 +194,20 @@ def test_xgmi_barrier_holds_the_stream_not_the_host():
             if p.is_alive():
                 p.kill()
     assert all(isinstance(v, dict) for v in results.values()) and len(results) == world, results
-    for name in ('comm_stream', 'current_stream'):
+    s0, s1 = results[0]['stamps'], results[1]['stamps']
+    for i, name in enumerate(('comm_stream', 'current_stream')):
+        spin_end0, after0 = s0[3 * i], s0[3 * i + 1]
+        before1, after1 = s1[3 * i], s1[3 * i + 1]
+        # device order (one clock for both processes): rank 1's stream passed the barrier only after rank 0's
+        # pre-barrier spin had ended, although rank 1 reached the barrier while rank 0 was still spinning
+        assert after1 >= spin_end0, (name, s0, s1)
+        assert after0 >= spin_end0, (name, s0, s1)
+        assert before1 < spin_end0, (name, s0, s1)
+        assert after1 - before1 > 0.5 * SPIN_S, (name, s0, s1)
+        if name == 'comm_stream':
+            assert s1[3 * i + 2] >= spin_end0, (name, s0, s1)          # rank 1's comm stream too
         c0, d0 = results[0][name]
-        c1, d1 = results[1][name]
-        assert d0 > MIN_S, (name, results)                                     # rank 0's stream slept
-        assert c0 < 0.5 * d0 and c1 < 0.5 * d0, (name, results)               # neither host waited
-        assert d1 > 0.5 * d0, (name, results)                                  # rank 1's stream waited for rank 0
+        c1, _ = results[1][name]
+        assert d0 > 0.9 * SPIN_S, (name, results)
+        assert c0 < 0.5 * SPIN_S and c1 < 0.5 * SPIN_S, (name, results)   # neither host waited
     assert all(results[r]['combine_after'] for r in range(world)), results

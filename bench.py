@@ -38,23 +38,31 @@ def _fail(msg: str, code: int = 3):
     sys.exit(code)
 
 
+# Ports above the ranks' MASTER_PORT P: the xGMI preflight children's gloo world, the RCCL preflight
+# children's world, and the store on which the ranks agree on the preflights' verdicts.
+PORT_XGMI_PREFLIGHT, PORT_RCCL_PREFLIGHT, PORT_AGREE = 1, 2, 3
+
+
 def _free_port_pair() -> int:
-    """A port P with P and P + 1 free on 127.0.0.1 (P: the ranks' rendezvous, P + 1: the xGMI preflight
-    children's own gloo world)."""
+    """A port P with P .. P + 3 free on 127.0.0.1 (P: the ranks' rendezvous; P + 1 / + 2 / + 3: see
+    PORT_XGMI_PREFLIGHT, PORT_RCCL_PREFLIGHT, PORT_AGREE)."""
+    import contextlib
     import socket
     for _ in range(64):
         with socket.socket() as a:
             a.bind(('127.0.0.1', 0))
             port = a.getsockname()[1]
-            if port >= 65535:
+            if port + PORT_AGREE > 65535:
                 continue
             try:
-                with socket.socket() as b:
-                    b.bind(('127.0.0.1', port + 1))
+                with contextlib.ExitStack() as stack:
+                    for off in range(1, PORT_AGREE + 1):
+                        b = stack.enter_context(socket.socket())
+                        b.bind(('127.0.0.1', port + off))
             except OSError:
                 continue
             return port
-    raise RuntimeError('no free port pair on 127.0.0.1')
+    raise RuntimeError('no free port range on 127.0.0.1')
 
 
 def _launch_ranks(n: int) -> int:
@@ -120,10 +128,11 @@ def _launch_ranks(n: int) -> int:
     return 0
 
 
-def _init_dist(n_gpus: int, use_gpu: bool = True):
+def _init_dist(n_gpus: int, use_gpu: bool = True, backend: str = None):
     """Join the ranks' process group and check it: the world must have exactly --gpus ranks, and over
-    RCCL every rank needs its own GPU.  A mismatch exits non-zero (never a silent one-rank line)."""
-    backend = os.environ.get('DEEPEP_BENCH_BACKEND', 'nccl')
+    RCCL every rank needs its own GPU.  A mismatch exits non-zero (never a silent one-rank line).
+    `backend` (default DEEPEP_BENCH_BACKEND, else nccl): gloo after a failed RCCL preflight."""
+    backend = backend or os.environ.get('DEEPEP_BENCH_BACKEND', 'nccl')
     if 'RANK' in os.environ and int(os.environ.get('WORLD_SIZE', '1')) > 1:
         local_rank = int(os.environ.get('LOCAL_RANK', 0))
         world_env = int(os.environ['WORLD_SIZE'])
@@ -172,36 +181,44 @@ def _launch_check(args) -> None:
 
 
 _XGMI = {'enabled': os.environ.get('DEEPEP_BENCH_XGMI', '1') != '0', 'preflight': None}
+_RCCL = {'preflight': None}
+PREFLIGHT_LIMIT_S = 150.0
 
 
-def _xgmi_preflight() -> dict:
-    """Start xgmi_preflight.py as a child (before this process touches the GPU): a small xGMI
-    dispatch + combine checked bit for bit against the default transport, in a gloo world of the
-    children on MASTER_PORT + 1.  A GPU fault there ends the child, not the bench."""
+def _start_child(script: str, port_offset: int):
+    """Start a preflight script as a child (before this process touches the GPU) on MASTER_PORT +
+    port_offset, its output in temporary files."""
     import subprocess
     import tempfile
     # the children's own store: torchrun's agent store (TORCHELASTIC_USE_AGENT_STORE) serves the parents
     env = {k: v for k, v in os.environ.items() if not k.startswith('TORCHELASTIC_')}
-    env['MASTER_PORT'] = str(int(os.environ.get('MASTER_PORT', '29500')) + 1)
+    env['MASTER_PORT'] = str(int(os.environ.get('MASTER_PORT', '29500')) + port_offset)
     env['MASTER_ADDR'] = os.environ.get('MASTER_ADDR', '127.0.0.1')
-    limit = 150.0
-    t0 = time.perf_counter()
-    with tempfile.TemporaryFile('w+') as out, tempfile.TemporaryFile('w+') as err:
-        p = subprocess.Popen([sys.executable, os.path.join(ROOT, 'xgmi_preflight.py')], env=env, cwd=ROOT,
-                             stdout=out, stderr=err, text=True)
-        rc = None
-        while rc is None and time.perf_counter() - t0 < limit:
-            try:
-                rc = p.wait(timeout=30)
-            except subprocess.TimeoutExpired:
-                print(f'[bench] xgmi preflight running ({time.perf_counter() - t0:.0f} s)', file=sys.stderr, flush=True)
-        if rc is None:
-            p.kill()
-            p.wait()
-            return dict(ok=False, error=f'preflight timed out ({limit:.0f} s)', seconds=round(time.perf_counter() - t0, 1))
-        out.seek(0)
-        err.seek(0)
-        stdout, stderr = out.read(), err.read()
+    out, err = tempfile.TemporaryFile('w+'), tempfile.TemporaryFile('w+')
+    p = subprocess.Popen([sys.executable, os.path.join(ROOT, script)], env=env, cwd=ROOT, stdout=out, stderr=err,
+                         text=True)
+    return dict(script=script, proc=p, out=out, err=err, t0=time.perf_counter())
+
+
+def _finish_child(c, limit: float = PREFLIGHT_LIMIT_S) -> dict:
+    """Wait for a preflight child (killed at `limit` s after its start) and read its JSON verdict; a child
+    that fails, hangs or prints nothing is ok=False with an error, never an exception."""
+    import subprocess
+    p, rc = c['proc'], None
+    while rc is None and time.perf_counter() - c['t0'] < limit:
+        try:
+            rc = p.wait(timeout=max(0.1, min(30.0, limit - (time.perf_counter() - c['t0']))))
+        except subprocess.TimeoutExpired:
+            print(f'[bench] {c["script"]} running ({time.perf_counter() - c["t0"]:.0f} s)', file=sys.stderr, flush=True)
+    if rc is None:
+        p.kill()
+        p.wait()
+        c['out'].close(), c['err'].close()
+        return dict(ok=False, error=f'preflight timed out ({limit:.0f} s)', seconds=round(time.perf_counter() - c['t0'], 1))
+    c['out'].seek(0)
+    c['err'].seek(0)
+    stdout, stderr = c['out'].read(), c['err'].read()
+    c['out'].close(), c['err'].close()
     lines = [ln for ln in stdout.splitlines() if ln.startswith('{')]
     try:
         res = json.loads(lines[-1]) if lines else {}
@@ -212,6 +229,66 @@ def _xgmi_preflight() -> dict:
     if not res['ok'] and not res.get('error'):
         res['error'] = (stderr.strip().splitlines() or ['no output'])[-1][:300]
     return res
+
+
+def _xgmi_preflight() -> dict:
+    """xgmi_preflight.py as a child: a small xGMI dispatch + combine checked bit for bit against the
+    default transport, in a gloo world of the children on MASTER_PORT + 1.  A GPU fault there ends the
+    child, not the bench."""
+    return _finish_child(_start_child('xgmi_preflight.py', PORT_XGMI_PREFLIGHT))
+
+
+def _rccl_preflight() -> dict:
+    """rccl_preflight.py as a child: a small RCCL dispatch + combine (pipelined all-to-alls) checked bit for
+    bit against the same calls over gloo, in an RCCL world of the children on MASTER_PORT + 2."""
+    return _finish_child(_start_child('rccl_preflight.py', PORT_RCCL_PREFLIGHT))
+
+
+def _run_preflights(rccl: bool, xgmi: bool):
+    """Both preflights at once (each child on its own port), before this process touches the GPU."""
+    kids = {}
+    if rccl:
+        kids['rccl'] = _start_child('rccl_preflight.py', PORT_RCCL_PREFLIGHT)
+    if xgmi:
+        kids['xgmi'] = _start_child('xgmi_preflight.py', PORT_XGMI_PREFLIGHT)
+    return {k: _finish_child(c) for k, c in kids.items()}
+
+
+def _agree(flags: dict, rank: int, world: int, timeout_s: float = 120.0) -> dict:
+    """Every rank's preflight verdicts, ANDed over the ranks through a TCP store on MASTER_PORT + 3 (no
+    process group exists yet: which backend the ranks' group uses depends on the result)."""
+    from datetime import timedelta
+    store = dist.TCPStore(os.environ.get('MASTER_ADDR', '127.0.0.1'),
+                          int(os.environ.get('MASTER_PORT', '29500')) + PORT_AGREE, world, rank == 0,
+                          timeout=timedelta(seconds=timeout_s))
+    store.set(f'preflight/{rank}', json.dumps(flags))
+    keys = [f'preflight/{r}' for r in range(world)]
+    store.wait(keys)
+    every = [json.loads(store.get(k)) for k in keys]
+    out = {name: all(bool(f.get(name)) for f in every) for name in flags}
+    # rank 0 hosts the store: it leaves only after every rank has read the verdicts
+    store.set(f'preflight_read/{rank}', '1')
+    if rank == 0:
+        store.wait([f'preflight_read/{r}' for r in range(world)])
+    return out
+
+
+def _choose_headline(backend_env: str, rccl_ok, xgmi_ok: bool) -> dict:
+    """The N > 1 headline's transport from the agreed preflight verdicts:
+      RCCL ok                 -> nccl group, RCCL all-to-all (the north star's transport)
+      RCCL failed, xGMI ok    -> gloo group (control only), xGMI window stores
+      both failed             -> gloo group, the all-to-all through host memory (marked)
+    DEEPEP_BENCH_BACKEND=gloo (rehearsal on shared GPUs) keeps the gloo exchange and runs no RCCL preflight."""
+    if backend_env == 'gloo':
+        return dict(backend='gloo', transport='rccl', label='gloo-host-exchange',
+                    reason='DEEPEP_BENCH_BACKEND=gloo rehearsal: the all-to-all goes through host memory')
+    if rccl_ok:
+        return dict(backend='nccl', transport='rccl', label='rccl', reason='rccl_preflight passed on every rank')
+    if xgmi_ok:
+        return dict(backend='gloo', transport='xgmi', label='xgmi',
+                    reason='rccl_preflight failed on at least one rank; xgmi_preflight passed on every rank')
+    return dict(backend='gloo', transport='rccl', label='gloo-host-exchange',
+                reason='rccl_preflight and xgmi_preflight failed: the all-to-all goes through host memory over gloo')
 
 
 def _xgmi_enabled() -> bool:
@@ -590,7 +667,10 @@ def _bench_single(y, handle, ex_w, weighted, total_bytes, steps, warmup, dev, re
         return float(t.item())
 
     res, outs = {}, {}
-    transports = ['rccl'] + (['xgmi'] if _xgmi_enabled() else [])
+    # over a gloo group (a failed RCCL preflight) the 'rccl' recipe would move its rows through host memory:
+    # then only the xGMI recipe runs, when it can
+    rccl_ok = dist.get_backend() == 'nccl' or not _xgmi_enabled()
+    transports = (['rccl'] if rccl_ok else []) + (['xgmi'] if _xgmi_enabled() else [])
     for transport in transports:
         sb, err = None, None
         try:
@@ -648,8 +728,8 @@ def _bench_single(y, handle, ex_w, weighted, total_bytes, steps, warmup, dev, re
         sb.destroy()
     if 'rccl' in outs and 'xgmi' in outs and 'value' in res.get('xgmi', {}):
         res['xgmi']['bitwise_equal_to_rccl'] = agree(bool(torch.equal(outs['rccl'], outs['xgmi'])))
-    if 'rccl' in outs:
-        d = vmax(_calc_diff(outs['rccl'], ref_multi))
+    if outs:
+        d = vmax(_calc_diff(outs.get('rccl', outs.get('xgmi')), ref_multi))
         res['calc_diff_vs_multi_reduction'] = d
     res['note'] = ('allow_multiple_reduction=False, same batch and bytes: rows unreduced to the source rank '
                    '(weighted: legacy low-latency fma chain), one reduce there; reduce_only = algorithmic bytes '
@@ -707,6 +787,9 @@ def main():
                     help='skip the token-major layout reference (keeps a rocprof kernel average to the product input)')
     ap.add_argument('--launch-check', action='store_true',
                     help='form and verify the N-rank world, print its launch fields, measure nothing')
+    ap.add_argument('--preflight-check', action='store_true',
+                    help='N > 1: run the RCCL / xGMI preflights, agree on them, print the chosen headline '
+                         'transport and the preflight fields, measure nothing')
     args = ap.parse_args()
     if args.gpus < 1:
         _fail('--gpus must be >= 1')
@@ -717,15 +800,37 @@ def main():
         return
 
     multi = 'RANK' in os.environ and int(os.environ.get('WORLD_SIZE', '1')) > 1
-    if multi and _XGMI['enabled']:
-        _XGMI['preflight'] = _xgmi_preflight()
-    rank, world = _init_dist(args.gpus)
-    if _XGMI['preflight'] is not None:
-        # the xGMI legs run only when every rank's preflight passed
-        ok = torch.tensor([1 if _XGMI['preflight']['ok'] else 0], dtype=torch.int32,
-                          device=torch.device('cuda', torch.cuda.current_device()))
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        _XGMI['enabled'] = bool(ok.item())
+    backend_env = os.environ.get('DEEPEP_BENCH_BACKEND', 'nccl')
+    headline = dict(backend=None, transport='rccl', label='local', reason='one rank')
+    if multi:
+        # Before this process touches the GPU: the RCCL and xGMI preflights as children (a fault or hang
+        # there ends a child, not the bench), their verdicts agreed over a store, and the headline's
+        # transport chosen from them -- so an RCCL failure on a new node never costs the line.
+        if args.gpus != int(os.environ['WORLD_SIZE']):
+            _fail(f'--gpus {args.gpus} but the launcher started {os.environ["WORLD_SIZE"]} ranks')
+        pf = _run_preflights(rccl=backend_env == 'nccl', xgmi=_XGMI['enabled'])
+        _RCCL['preflight'] = pf.get('rccl') or dict(ok=False, skipped=f'DEEPEP_BENCH_BACKEND={backend_env}')
+        _XGMI['preflight'] = pf.get('xgmi')
+        agreed = _agree({'rccl': bool(_RCCL['preflight'].get('ok')),
+                         'xgmi': bool(_XGMI['preflight'] and _XGMI['preflight'].get('ok'))},
+                        int(os.environ['RANK']), int(os.environ['WORLD_SIZE']))
+        _RCCL['preflight']['all_ranks_ok'] = agreed['rccl']
+        if _XGMI['preflight'] is not None:
+            _XGMI['preflight']['all_ranks_ok'] = agreed['xgmi']
+        _XGMI['enabled'] = _XGMI['enabled'] and agreed['xgmi']    # the xGMI legs run only when every rank passed
+        headline = _choose_headline(backend_env, agreed['rccl'], agreed['xgmi'])
+    if args.preflight_check:
+        if not multi:
+            _fail('--preflight-check needs N > 1 ranks')
+        rank, world = _init_dist(args.gpus, use_gpu=headline['backend'] == 'nccl', backend=headline['backend'])
+        if rank == 0:
+            print(json.dumps({'preflight_check': True, 'n_gpus': world, 'headline_transport': headline,
+                              'config': {'transport': headline['label']}, 'rccl_preflight': _RCCL['preflight'],
+                              'xgmi_preflight': _XGMI['preflight']}), flush=True)
+        dist.barrier()
+        dist.destroy_process_group()
+        return
+    rank, world = _init_dist(args.gpus, backend=headline['backend'])
     from deepep_amd import ElasticBuffer
     from deepep_amd.kernels import MODE_EPILOGUE, MODE_FUSED
     T, H, K, E = args.tokens, args.hidden, args.topk, args.experts
@@ -741,6 +846,8 @@ def main():
     topk_idx = topk_idx.to(torch.int64)
     x = torch.randn((T, H), device=dev).to(torch.bfloat16)
     buf = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=T, hidden=H, num_topk=K)
+    if world > 1:
+        buf.transport = headline['transport']
     if args.fp8_dispatch:
         from workloads import per_token_cast_to_fp8
         x = per_token_cast_to_fp8(x)
@@ -799,8 +906,9 @@ def main():
                                    f'{"FP8 dispatch, " if args.fp8_dispatch else ""}expanded layout, '
                                    f'{"gating-weighted" if weighted else "plain (reference semantics)"}',
                        'tokens_per_rank': T, 'hidden': H, 'topk': K, 'experts': E, 'accumulate': 'fp32',
-                       'parallelism': f'ep{world}', 'transport': buf.transport if world > 1 else None},
-            **res, 'xgmi_preflight': _XGMI['preflight'],
+                       'parallelism': f'ep{world}', 'transport': headline['label'] if world > 1 else None},
+            **res, 'headline_transport': headline if world > 1 else None,
+            'rccl_preflight': _RCCL['preflight'], 'xgmi_preflight': _XGMI['preflight'],
             'launch': {'world_size_seen': world, 'launcher': os.environ.get('DEEPEP_BENCH_LAUNCHER', 'external')
                        if world > 1 else 'single process', 'backend': dist.get_backend(),
                        'devices_visible': torch.cuda.device_count(), 'soft_budget_s': SOFT_BUDGET_S,
@@ -1063,14 +1171,23 @@ def main():
         rccl_budget = dict(phase_a_cus=128, value=round(total_bytes * args.steps / el_b / 1e9, 2),
                            ms_per_step=round(el_b * 1e3 / args.steps, 4), bitwise_equal=bool(same.item()))
         buf.phase_a_cus = 0
-    if world > 1:
+    if world > 1 and headline['label'] == 'rccl':
         res['rccl'] = dict(value=round(value, 2), ms_per_step=round(ms_per_step, 4), phase_a_budget=rccl_budget)
+        publish()
+    elif world > 1:
+        res['rccl'] = dict(skipped=headline['reason'], headline=dict(transport=headline['label'], value=round(value, 2),
+                                                                   ms_per_step=round(ms_per_step, 4),
+                                                                   phase_a_budget=rccl_budget))
         publish()
 
     xgmi = None
     if world > 1 and not _xgmi_enabled() and _XGMI['preflight'] is not None:
         xgmi = dict(skipped='xgmi_preflight failed on at least one rank (see xgmi_preflight)')
-    if world > 1 and _xgmi_enabled() and leg('xgmi'):
+    if world > 1 and headline['transport'] == 'xgmi':
+        xgmi = dict(skipped='the xGMI transport is the headline (`value`); xgmi_preflight checked it bit for bit '
+                            'against the gloo exchange')
+        res['xgmi'] = xgmi
+    elif world > 1 and _xgmi_enabled() and leg('xgmi'):
         xgmi = _bench_xgmi(buf, y, handle, ex_w, weighted, total_bytes, args.steps, args.warmup, dev)
         res['xgmi'] = xgmi
         publish()
@@ -1120,10 +1237,11 @@ def main():
                              'dispatch(handle=...) (no sync); bytes = x read once + expanded rows written')
         res['dispatch'] = dispatch
         publish()
-        if world > 1 and _xgmi_enabled() and leg('dispatch_xgmi'):
+        if world > 1 and _xgmi_enabled() and headline['transport'] != 'xgmi' and leg('dispatch_xgmi'):
             dispatch['xgmi'] = _bench_xgmi_dispatch(buf, x_disp, topk_idx, topk_w, E, disp_bytes, time_dispatch, dev)
             publish()
-        if world > 1 and os.environ.get('DEEPEP_BENCH_SYNC_FREE', '1') != '0' and leg('dispatch_sync_free'):
+        if world > 1 and os.environ.get('DEEPEP_BENCH_SYNC_FREE', '1') != '0' and headline['transport'] == 'rccl' \
+                and leg('dispatch_sync_free'):
             dispatch['sync_free'] = _bench_sync_free(buf, x_disp, topk_idx, topk_w, E, weighted, dev)
             publish()
     del x_disp
@@ -1169,10 +1287,11 @@ def main():
     # output matched the default bit for bit (information, never the headline).
     line.leg = 'summary'
     if world > 1:
-        legs = [('rccl', value)]
+        legs = [(headline['label'], value)]
         if rccl_budget is not None and rccl_budget['bitwise_equal']:
             legs.append((f'rccl, DEEPEP_PHASE_A_CUS={rccl_budget["phase_a_cus"]}', rccl_budget['value']))
-        if xgmi is not None and 'value' in xgmi and xgmi['bitwise_equal_to_rccl'] and not xgmi['barrier_timeout']:
+        if xgmi is not None and 'value' in xgmi and xgmi['bitwise_equal_to_rccl'] and not xgmi['barrier_timeout'] \
+                and headline['label'] == 'rccl':
             legs.append(('xgmi', xgmi['value']))
             xb_ = xgmi.get('phase_a_budget')
             if xb_ and xb_['bitwise_equal_to_rccl'] and not xb_['barrier_timeout']:

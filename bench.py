@@ -766,6 +766,22 @@ def _pmc_traffic(workload: str, build_id: str):
                                                              'MI355X_MICROARCH.md gfx950 corrections, same build')
 
 
+def _hbm_bytes_per_rank(world: int, T: int, H: int, K: int, build_id: str) -> dict:
+    """The whole EP = N step's HBM bytes per rank by transport (rccl / xgmi / algorithmic) from the same-build
+    PMC passes (tools/pmc_ep.py -> summarize_prof.py stepfold -> profiles/pmc_traffic.json); another build's
+    counters are not reported."""
+    e = _pmc_entry(f'step_ep{world}_t{T}_h{H}_k{K}')
+    if not e:
+        return dict(rccl=None, xgmi=None, algorithmic=None, note=f'no step PMC pass for EP = {world}')
+    if e.get('build_id') != build_id:
+        return dict(rccl=None, xgmi=None, algorithmic=None,
+                    note=f'step PMC pass of build {e.get("build_id")}, this is {build_id}: stale, not reported')
+    return dict(e['hbm_bytes_per_rank'], build_id=build_id, source=e.get('source'),
+                note='HBM bytes of one whole combine step per rank (2 x FETCH_SIZE + WRITE_SIZE): rccl = phase A + '
+                     'the exchange\'s copies + phase B; xgmi = phase A + phase B of the same passes (phase A stores '
+                     'into the owners\' windows, no exchange pass); algorithmic = `value`\'s bytes per rank')
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -1136,7 +1152,7 @@ def main():
                       reduce_only_gbps=round(total_bytes / (float(vals[0]) * 1e-3) / 1e9, 1),
                       exchange_gbps_per_rank=round(float(xb.item()) / world / (float(vals[1]) * 1e-3) / 1e9, 1),
                       pipeline_chunks=buf._num_chunks(handle), transport=buf.transport,
-                      local_bypass=buf.local_bypass,
+                      local_bypass=buf.local_bypass, hbm_bytes_per_rank=_hbm_bytes_per_rank(world, T, H, K, build_id),
                       note='phase_*_ms / exchange_ms: the step unpipelined (1 chunk); pipelined_phase_*_ms: the sum of the '
                            'per-chunk launches inside the pipelined step (`value`); max over ranks; reduce_only = algorithmic bytes of all ranks / (phase A + phase B); '
                            'exchange = off-rank partial rows + weights / exchange time, per rank (local_bypass: the '

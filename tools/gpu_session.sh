@@ -61,6 +61,7 @@ for step in "$@"; do
                         $(find $OUT/pmcep${n}_FETCH_SIZE $OUT/pmcep${n}_WRITE_SIZE -name '*counter_collection.csv')
                     run pmcstepfold$n 120 python tools/summarize_prof.py step $OUT/pmc_step_ep${n}.json $OUT/pmc_ep${n}_meta.json \
                         $(find $OUT/pmcep${n}_FETCH_SIZE $OUT/pmcep${n}_WRITE_SIZE -name '*counter_collection.csv')
+                    run pmcstepfold2$n 60 python tools/summarize_prof.py stepfold profiles/pmc_traffic.json $OUT/pmc_step_ep${n}.json
                 done
                 cp profiles/pmc_traffic.json $OUT/pmc_traffic.json ;;
         pmcstep) # the whole EP = N step with the diagonal travelling (DEEPEP_LOCAL_BYPASS=0), beside `pmcep`'s

@@ -212,9 +212,45 @@ def step(out, meta_json, *paths):
     print(json.dumps(summary, indent=1))
 
 
+def step_fold(out, step_json):
+    """Fold a `step` summary into `out` (profiles/pmc_traffic.json) as step_ep{N}_t{T}_h{H}_k{K}: the HBM bytes
+    per rank of one whole EP = N combine step by transport, with the build id -- what bench.py's N > 1 line
+    reports as phases.hbm_bytes_per_rank (its own build only).
+      rccl         every kernel of the step: phase A + the exchange's copies (on a real node RCCL's own read of
+                   the send rows and write of the received rows) + phase B
+      xgmi         phase A + phase B of the same passes: over the windows phase A stores each partial straight
+                   into its owner's window row and phase B reads it there, so the exchange adds no HBM pass
+                   (derived from the same counters, not a separate run)
+      algorithmic  the combine's algorithmic bytes per rank (bench.py's `value` numerator)"""
+    st = json.load(open(step_json))
+    m = st['meta']
+    n = m['world']
+    k = st['kernels']
+
+    def both(name):
+        e = k.get(name, {})
+        return e.get('read_bytes_per_step', 0.0) + e.get('write_bytes_per_step', 0.0)
+    key = f"step_ep{n}_t{m['tokens']}_h{m['hidden']}_k{m['topk']}"
+    entry = dict(build_id=st['build_id'], local_bypass=m['local_bypass'],
+                 source='tools/pmc_ep.py + summarize_prof.py step (ranks simulated on one GPU, one chunk per rank)',
+                 hbm_bytes_per_rank=dict(rccl=st['step_bytes'] / n, xgmi=(both('phase_a') + both('phase_b')) / n,
+                                         algorithmic=sum(m['b_bytes']) / n),
+                 kernels_bytes_per_step_all_ranks={name: both(name) for name in k})
+    entry['hbm_bytes_per_rank']['rccl_over_xgmi'] = entry['hbm_bytes_per_rank']['rccl'] / entry['hbm_bytes_per_rank']['xgmi']
+    try:
+        data = json.load(open(out))
+    except (OSError, ValueError):
+        data = {}
+    data[key] = entry
+    json.dump(data, open(out, 'w'), indent=1, sort_keys=True)
+    print(json.dumps({key: entry}, indent=1))
+
+
 if __name__ == '__main__':
     if sys.argv[1] == 'step':
         step(sys.argv[2], sys.argv[3], *sys.argv[4:])
+    elif sys.argv[1] == 'stepfold':
+        step_fold(sys.argv[2], sys.argv[3])
     elif sys.argv[1] == 'ep':
         pmc_ep(sys.argv[2], sys.argv[3], *sys.argv[4:])
     elif sys.argv[1] == 'phases':

@@ -189,14 +189,9 @@ __device__ __forceinline__ void store_weight(const Params& p, int64_t u, uint16_
 // source row of u.  The unit's slot table row (and its gating weights) arrive in my_slot / my_w, one
 // entry per lane; the valid slots are then visited in ascending order through the ballot mask,
 // which is exactly the compacted order of compute_topk_slots (combine_utils.cuh:41-53).
-// Load paths of the source rows.  kLoadVgpr: global_load_dwordx4 nt into registers (the product).
-// kLoadLdsNT / kLoadLds: LDS-DMA (global_load_lds_dwordx4, nt or default policy) into the wave's own LDS
-// slice, then ds_read_b128 -- the round-6 experiment; same arithmetic and order.
-constexpr int kLoadVgpr = 0, kLoadLdsNT = 1, kLoadLds = 2;
-
-template <int kMode, bool kWeighted, int kVPT, bool kFull, int kStoreAux, int kGroup, int kLoad = kLoadVgpr>
+template <int kMode, bool kWeighted, int kVPT, bool kFull, int kStoreAux, int kGroup>
 __device__ __forceinline__ void combine_item(const Params& p, int64_t it, int nchunks, int nvec, int lane,
-                                             int32_t my_slot, float my_w, u32x4* lds_rows = nullptr) {
+                                             int32_t my_slot, float my_w) {
     constexpr int kChunkVecs = 64 * kVPT;
     const int64_t u = it / nchunks;
     const int c = static_cast<int>(it - u * nchunks);
@@ -267,43 +262,14 @@ __device__ __forceinline__ void combine_item(const Params& p, int64_t it, int nc
             rem &= rem - 1ull;                              // (no-op once empty)
         }
         u32x4 vals[kGroup][kVPT];
-        if constexpr (kLoad == kLoadVgpr) {
 #pragma unroll
-            for (int j = 0; j < kGroup; ++j) {
-                if (lane_of[j] >= 0) {
-                    const int32_t sj = __builtin_amdgcn_readlane(my_slot, lane_of[j]);
-                    const u32x4* row = reinterpret_cast<const u32x4*>(p.src + static_cast<int64_t>(sj) * p.src_stride);
+        for (int j = 0; j < kGroup; ++j) {
+            if (lane_of[j] >= 0) {
+                const int32_t sj = __builtin_amdgcn_readlane(my_slot, lane_of[j]);
+                const u32x4* row = reinterpret_cast<const u32x4*>(p.src + static_cast<int64_t>(sj) * p.src_stride);
 #pragma unroll
-                    for (int v = 0; v < kVPT; ++v)
-                        vals[j][v] = vok[v] ? load16<true>(row + vidx[v]) : (u32x4){0u, 0u, 0u, 0u};
-                }
-            }
-        } else {
-            // One 1 KiB LDS-DMA per (row, vector): lane l's 16 bytes land at slice + 16 l (wave-uniform
-            // base + lane x size), then this wave's own vmcnt orders its ds_reads behind them.  The slice
-            // is re-filled only after every ds_read of the previous group was consumed (program order).
-#pragma unroll
-            for (int j = 0; j < kGroup; ++j) {
-                if (lane_of[j] >= 0) {
-                    const int32_t sj = __builtin_amdgcn_readlane(my_slot, lane_of[j]);
-                    const u32x4* row = reinterpret_cast<const u32x4*>(p.src + static_cast<int64_t>(sj) * p.src_stride);
-#pragma unroll
-                    for (int v = 0; v < kVPT; ++v)
-                        if (vok[v])
-                            __builtin_amdgcn_global_load_lds(
-                                (const __attribute__((address_space(1))) void*)(row + vidx[v]),
-                                (__attribute__((address_space(3))) void*)(lds_rows + (j * kVPT + v) * 64),
-                                16, 0, kLoad == kLoadLdsNT ? 2 : 0);
-                }
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-            for (int j = 0; j < kGroup; ++j) {
-                if (lane_of[j] >= 0) {
-#pragma unroll
-                    for (int v = 0; v < kVPT; ++v)
-                        vals[j][v] = vok[v] ? lds_rows[(j * kVPT + v) * 64 + lane] : (u32x4){0u, 0u, 0u, 0u};
-                }
+                for (int v = 0; v < kVPT; ++v)
+                    vals[j][v] = vok[v] ? load16<true>(row + vidx[v]) : (u32x4){0u, 0u, 0u, 0u};
             }
         }
         if (copy_row) {
@@ -361,13 +327,12 @@ __device__ __forceinline__ void combine_item(const Params& p, int64_t it, int nc
 // A workgroup of kWaves waves takes kWaves consecutive items; the slot-table rows of the units those
 // items belong to (and their gating weights) are staged once per workgroup in LDS, one entry per lane.
 // One workgroup per kWaves items: 28,672 workgroups at config 2, no tail imbalance.
-template <int kMode, bool kWeighted, int kVPT, bool kFull, int kStoreAux, int kWaves, int kGroup, int kLoad = kLoadVgpr>
+template <int kMode, bool kWeighted, int kVPT, bool kFull, int kStoreAux, int kWaves, int kGroup>
 __global__ void __launch_bounds__(64 * kWaves)
 combine_rows_kernel(const Params p) {
     constexpr int kChunkVecs = 64 * kVPT;
     __shared__ int32_t s_slot[kWaves][kMaxWidth];
     __shared__ float s_w[kWaves][kMaxWidth];
-    __shared__ u32x4 s_rows[kLoad == kLoadVgpr ? 1 : kWaves * kGroup * kVPT * 64];
     const int tid = static_cast<int>(threadIdx.x), lane = tid & 63, wave = tid >> 6;
     const int nvec = p.hidden >> 3;                          // 16-byte vectors per row
     const int nchunks = (nvec + kChunkVecs - 1) / kChunkVecs;
@@ -397,8 +362,7 @@ combine_rows_kernel(const Params p) {
         my_slot = s_slot[ul][lane];
         if constexpr (kWeighted) my_w = s_w[ul][lane];
     }
-    combine_item<kMode, kWeighted, kVPT, kFull, kStoreAux, kGroup, kLoad>(p, it, nchunks, nvec, lane, my_slot, my_w,
-                                                                       s_rows + wave * (kGroup * kVPT * 64));
+    combine_item<kMode, kWeighted, kVPT, kFull, kStoreAux, kGroup>(p, it, nchunks, nvec, lane, my_slot, my_w);
 }
 
 // CU-budget streams created by deepep_stream_create_cu_budget (symmetric.hip) and their CU counts: a
@@ -424,29 +388,11 @@ struct Shape {
     int vpt, waves, group;
 };
 
-// Round-6 experiment (deepep_amd_exp_load_path, not part of the C-ABI): 0 = registers (product), 1 = LDS-DMA
-// nt, 2 = LDS-DMA default policy; honoured by the fused reduce over whole 64 x vpt chunks only.
-std::atomic<int> g_load_path{0};
-
 template <int kMode, bool kWeighted, int kVPT, bool kFull, int kAux, int kWaves>
 void launch_group(const Params& p, int group, hipStream_t stream) {
     const int nvec = p.hidden / 8;
     const int64_t items = static_cast<int64_t>(p.num_units) * ((nvec + 64 * kVPT - 1) / (64 * kVPT));
     const dim3 grid(static_cast<unsigned>((items + kWaves - 1) / kWaves)), block(64 * kWaves);
-    if constexpr (kMode == DEEPEP_MODE_FUSED && kFull) {
-        const int path = g_load_path.load(std::memory_order_relaxed);
-#define DEEPEP_LDS(L)                                                                                                          \
-    do {                                                                                                                       \
-        if (group <= 4)                                                                                                        \
-            hipLaunchKernelGGL((combine_rows_kernel<kMode, kWeighted, kVPT, kFull, kAux, kWaves, 4, L>), grid, block, 0, stream, p); \
-        else                                                                                                                   \
-            hipLaunchKernelGGL((combine_rows_kernel<kMode, kWeighted, kVPT, kFull, kAux, kWaves, 8, L>), grid, block, 0, stream, p); \
-        return;                                                                                                                \
-    } while (0)
-        if (path == kLoadLdsNT) DEEPEP_LDS(kLoadLdsNT);
-        if (path == kLoadLds) DEEPEP_LDS(kLoadLds);
-#undef DEEPEP_LDS
-    }
     if (group == 2)
         hipLaunchKernelGGL((combine_rows_kernel<kMode, kWeighted, kVPT, kFull, kAux, kWaves, 2>), grid, block, 0, stream, p);
     else if (group == 4)
@@ -750,13 +696,6 @@ int deepep_build_local_plan(const int32_t* src_metadata, int num_recv_tokens, in
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess)
         return set_error(DEEPEP_ERR_HIP, "plan launch failed: %s", hipGetErrorString(err));
-    return DEEPEP_OK;
-}
-
-// Round-6 experiment only (see g_load_path); not declared in include/deepep_amd.h.
-int deepep_amd_exp_load_path(int path) {
-    if (path < kLoadVgpr || path > kLoadLds) return set_error(DEEPEP_ERR_INVALID_ARG, "load path 0-2");
-    g_load_path.store(path, std::memory_order_relaxed);
     return DEEPEP_OK;
 }
 

@@ -141,23 +141,6 @@ def test_kernel_launch_configs_identical(kern, cfg, upb):
         kern.lib.deepep_set_launch_config(0, 0)
 
 
-@pytest.mark.parametrize('path', [1, 2])
-@pytest.mark.parametrize('cfg', [(1, 4), (1, 8), (2, 4)])
-def test_kernel_lds_dma_load_path_identical(kern, path, cfg):
-    """The round-6 LDS-DMA load path of the fused reduce (nt / default policy) gives the oracle's bits:
-    plain and weighted, bias 0-2, -0 / inf / denormal rows, > 8 valid rows (several groups)."""
-    assert kern.lib.deepep_amd_exp_load_path(path) == 0
-    assert kern.lib.deepep_set_launch_config(*cfg) == 0
-    try:
-        for nb in (0, 1, 2):
-            _run(kern, MODE_FUSED, False, 31, 8, 7168, nb, seed=40 + nb, special=True, upb=4)
-            _run(kern, MODE_FUSED, True, 31, 8, 7168, nb, seed=50 + nb, upb=8)
-            _run(kern, MODE_FUSED, True, 23, 17, 1024, nb, seed=60 + nb, upb=4)
-    finally:
-        kern.lib.deepep_amd_exp_load_path(0)
-        kern.lib.deepep_set_launch_config(0, 0)
-
-
 @pytest.mark.parametrize('weighted,hidden', [(False, 7168), (True, 520), (False, 64)])
 def test_kernel_reduce_scatter_rows(kern, weighted, hidden):
     """deepep_combine_reduce_scatter (phase A of the xGMI transport) = the LOCAL reduce with each

@@ -75,10 +75,6 @@ for step in "$@"; do
                     run pmcnbfold$n 120 python tools/summarize_prof.py step $OUT/pmc_step_ep${n}_nobypass.json $OUT/pmc_ep${n}_nobypass_meta.json \
                         $(find $OUT/pmcnb${n}_FETCH_SIZE $OUT/pmcnb${n}_WRITE_SIZE -name '*counter_collection.csv')
                 done ;;
-        ldsdma) # round-6 item 1: LDS-DMA load path vs registers, both layouts, one process; bitwise first
-                run ldsdma_test 300 python -u -m pytest tests/test_combine_gpu.py -k lds_dma -x -q --timeout 120 --timeout-method thread
-                run ldsdma 600 python -u tools/kldsdma.py
-                grep '^{' $OUT/ldsdma.log > $OUT/ldsdma.jsonl || true ;;
         cumask) run cumask 120 python tools/probe_cumask.py ;;
         kdisp)  run kdisp 300 python tools/kdispatch.py ;;
         khost)  run khost 300 python tools/khost.py ;;

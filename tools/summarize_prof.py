@@ -212,6 +212,30 @@ def step(out, meta_json, *paths):
     print(json.dumps(summary, indent=1))
 
 
+def bykernel(out, *paths):
+    """HBM bytes per launch of every combine_rows_kernel instantiation in PMC passes (2 x FETCH_SIZE +
+    WRITE_SIZE, KiB), keyed by the kernel's template arguments: variants of one run told apart."""
+    per = defaultdict(lambda: defaultdict(list))
+    for p in paths:
+        for r in csv.DictReader(open(p)):
+            name = r.get('Kernel_Name', '').replace('(anonymous namespace)::', '')
+            if 'combine_rows_kernel<' not in name:
+                continue
+            key = name[name.index('combine_rows_kernel<'):].split('(')[0]
+            per[key][r['Counter_Name']].append(float(r['Counter_Value']))
+    res = {}
+    for k, cs in per.items():
+        avg = {c: sum(v) / len(v) for c, v in cs.items()}
+        e = {'counters_avg_per_launch': avg, 'launches': {c: len(v) for c, v in cs.items()}}
+        if 'FETCH_SIZE' in avg:
+            e['hbm_read_bytes_per_launch'] = 2 * avg['FETCH_SIZE'] * 1024
+        if 'WRITE_SIZE' in avg:
+            e['hbm_write_bytes_per_launch'] = avg['WRITE_SIZE'] * 1024
+        res[k] = e
+    json.dump(dict(kernels=res, build_id=_build_id()), open(out, 'w'), indent=1, sort_keys=True)
+    print(json.dumps(res, indent=1))
+
+
 def step_fold(out, step_json):
     """Fold a `step` summary into `out` (profiles/pmc_traffic.json) as step_ep{N}_t{T}_h{H}_k{K}: the HBM bytes
     per rank of one whole EP = N combine step by transport, with the build id -- what bench.py's N > 1 line
@@ -249,6 +273,8 @@ def step_fold(out, step_json):
 if __name__ == '__main__':
     if sys.argv[1] == 'step':
         step(sys.argv[2], sys.argv[3], *sys.argv[4:])
+    elif sys.argv[1] == 'bykernel':
+        bykernel(sys.argv[2], *sys.argv[3:])
     elif sys.argv[1] == 'stepfold':
         step_fold(sys.argv[2], sys.argv[3])
     elif sys.argv[1] == 'ep':

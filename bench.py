@@ -1141,7 +1141,7 @@ def main():
         su_line = dict(gbps_per_rank=round(float(su[0]), 1), gbps_per_rank_phase_a_exchange=round(float(su[1]), 1),
                        bytes_rank0=su_bytes,
                        note='reference definition: received tokens x (2H + 4K) / t; gbps_per_rank uses the whole '
-                            'pipelined combine step (RCCL transport, the main loop), gbps_per_rank_phase_a_exchange '
+                            'pipelined combine step (the headline transport, the main loop), gbps_per_rank_phase_a_exchange '
                             'the unpipelined phase A + exchange (the analogue of combine_impl, which the reference '
                             'times); min over ranks')
         pipe = torch.tensor([t_a_pipe, t_b_pipe], dtype=torch.float64, device=dev)

@@ -255,22 +255,38 @@ def _run_preflights(rccl: bool, xgmi: bool):
 
 
 def _agree(flags: dict, rank: int, world: int, timeout_s: float = 120.0) -> dict:
-    """Every rank's preflight verdicts, ANDed over the ranks through a TCP store on MASTER_PORT + 3 (no
-    process group exists yet: which backend the ranks' group uses depends on the result)."""
+    """Every rank's preflight verdicts, ANDed over the ranks through a TCP store (no process group exists
+    yet: which backend the ranks' group uses depends on the result).  Under torchrun the launcher's agent
+    store on MASTER_PORT serves it (keys under a prefix, as the env:// rendezvous uses it); when bench.py
+    starts its own ranks, rank 0 hosts a store on MASTER_PORT + 3 (checked free at launch)."""
     from datetime import timedelta
-    store = dist.TCPStore(os.environ.get('MASTER_ADDR', '127.0.0.1'),
-                          int(os.environ.get('MASTER_PORT', '29500')) + PORT_AGREE, world, rank == 0,
-                          timeout=timedelta(seconds=timeout_s))
+    host, port = os.environ.get('MASTER_ADDR', '127.0.0.1'), int(os.environ.get('MASTER_PORT', '29500'))
+    agent = os.environ.get('TORCHELASTIC_USE_AGENT_STORE', '').lower() == 'true'
+    base = dist.TCPStore(host, port if agent else port + PORT_AGREE, world, rank == 0 and not agent,
+                         timeout=timedelta(seconds=timeout_s))
+    store = dist.PrefixStore(f'deepep_bench_preflight_{os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")}/', base)
     store.set(f'preflight/{rank}', json.dumps(flags))
     keys = [f'preflight/{r}' for r in range(world)]
     store.wait(keys)
     every = [json.loads(store.get(k)) for k in keys]
     out = {name: all(bool(f.get(name)) for f in every) for name in flags}
-    # rank 0 hosts the store: it leaves only after every rank has read the verdicts
+    # rank 0 may host the store: it leaves only after every rank has read the verdicts
     store.set(f'preflight_read/{rank}', '1')
     if rank == 0:
         store.wait([f'preflight_read/{r}' for r in range(world)])
     return out
+
+
+def _agree_or_default(flags: dict, rank: int, world: int) -> dict:
+    """_agree, or -- when the store itself fails, on every rank alike (rank 0 could not host it, or the
+    others timed out reaching it) -- the pre-preflight default (RCCL headline, no xGMI legs), named in
+    the line."""
+    try:
+        return dict(_agree(flags, rank, world), agreement='store')
+    except Exception as e:          # noqa: BLE001 -- reported in the line
+        print(f'[bench] rank {rank}: preflight agreement failed ({type(e).__name__}: {e}); default transport',
+              file=sys.stderr, flush=True)
+        return dict(rccl=True, xgmi=False, agreement=f'failed ({type(e).__name__}: {str(e)[:200]}): default')
 
 
 def _choose_headline(backend_env: str, rccl_ok, xgmi_ok: bool) -> dict:
@@ -827,10 +843,11 @@ def main():
         pf = _run_preflights(rccl=backend_env == 'nccl', xgmi=_XGMI['enabled'])
         _RCCL['preflight'] = pf.get('rccl') or dict(ok=False, skipped=f'DEEPEP_BENCH_BACKEND={backend_env}')
         _XGMI['preflight'] = pf.get('xgmi')
-        agreed = _agree({'rccl': bool(_RCCL['preflight'].get('ok')),
-                         'xgmi': bool(_XGMI['preflight'] and _XGMI['preflight'].get('ok'))},
-                        int(os.environ['RANK']), int(os.environ['WORLD_SIZE']))
+        agreed = _agree_or_default({'rccl': bool(_RCCL['preflight'].get('ok')),
+                                    'xgmi': bool(_XGMI['preflight'] and _XGMI['preflight'].get('ok'))},
+                                   int(os.environ['RANK']), int(os.environ['WORLD_SIZE']))
         _RCCL['preflight']['all_ranks_ok'] = agreed['rccl']
+        _RCCL['preflight']['agreement'] = agreed['agreement']
         if _XGMI['preflight'] is not None:
             _XGMI['preflight']['all_ranks_ok'] = agreed['xgmi']
         _XGMI['enabled'] = _XGMI['enabled'] and agreed['xgmi']    # the xGMI legs run only when every rank passed
@@ -847,6 +864,17 @@ def main():
         dist.destroy_process_group()
         return
     rank, world = _init_dist(args.gpus, backend=headline['backend'])
+    line = _Line(rank)
+    if world > 1:
+        # N > 1: the watchdog runs from here, so even a headline that hangs on a node leaves a line (value
+        # null, `incomplete` naming the leg) with the preflight fields that explain it
+        line.fields = {'metric': 'combine GB/s (device-resident BF16 top-k weighted reduce) at 1/2/4/8 MI355X',
+                       'value': None, 'unit': 'GB/s', 'n_gpus': world, 'higher_is_better': True,
+                       'config': {'parallelism': f'ep{world}', 'transport': headline['label']},
+                       'headline_transport': headline, 'rccl_preflight': _RCCL['preflight'],
+                       'xgmi_preflight': _XGMI['preflight']}
+        _LINE[0] = line
+        line.start_watchdog()
     from deepep_amd import ElasticBuffer
     from deepep_amd.kernels import MODE_EPILOGUE, MODE_FUSED
     T, H, K, E = args.tokens, args.hidden, args.topk, args.experts
@@ -877,6 +905,7 @@ def main():
     def step():
         return buf.combine(y, handle, topk_weights=ex_w, apply_topk_weights=weighted)
 
+    line.leg = 'headline'
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -906,7 +935,6 @@ def main():
     value = total_bytes * args.steps / elapsed / 1e9
     ms_per_step = elapsed * 1e3 / args.steps
 
-    line = _Line(rank)
     _LINE[0] = line
     res = dict(roofline=None, cpu_baseline=None, cpu_torch=None, loopback=None, phases=None, su_bandwidth=None,
                rccl=None, xgmi=None, single_reduction=None, fastest_leg=None, dispatch=None)
@@ -931,8 +959,6 @@ def main():
                        'hard_deadline_s': HARD_DEADLINE_S},
         }
     publish()
-    if world > 1:
-        line.start_watchdog()
 
     def leg(name: str, secondary: bool = True) -> bool:
         """Enter leg `name`; a secondary leg runs only inside the soft budget (every rank agrees)."""

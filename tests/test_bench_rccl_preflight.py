@@ -68,8 +68,32 @@ def test_injected_rccl_failure_is_named():
 
 def test_gloo_rehearsal_runs_no_rccl_preflight():
     d = _check(2, DEEPEP_BENCH_BACKEND='gloo', DEEPEP_BENCH_XGMI='0')
-    assert d['rccl_preflight'] == {'ok': False, 'skipped': 'DEEPEP_BENCH_BACKEND=gloo', 'all_ranks_ok': False}
+    assert d['rccl_preflight'] == {'ok': False, 'skipped': 'DEEPEP_BENCH_BACKEND=gloo', 'all_ranks_ok': False,
+                                   'agreement': 'store'}
     assert d['config']['transport'] == 'gloo-host-exchange'
+
+
+def test_torchrun_agreement_uses_the_agent_store():
+    """Under torchrun (the driver's N > 1 form) the ranks agree through the launcher's own store."""
+    r = subprocess.run([sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
+                        '--master-addr', '127.0.0.1', '--master-port', '29741', BENCH, '--gpus', '2',
+                        '--preflight-check'], env=_env(DEEPEP_BENCH_BACKEND='nccl', DEEPEP_BENCH_XGMI='0',
+                                                       DEEPEP_BENCH_FAIL_RCCL_PREFLIGHT='1'),
+                       cwd='/tmp', capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith('{')][-1])
+    assert d['rccl_preflight']['agreement'] == 'store' and d['rccl_preflight']['all_ranks_ok'] is False
+    assert d['config']['transport'] == 'gloo-host-exchange'
+
+
+def test_failed_agreement_falls_back_to_the_default(monkeypatch):
+    import bench
+
+    def broken(*a, **k):
+        raise RuntimeError('store unreachable')
+    monkeypatch.setattr(bench, '_agree', broken)
+    got = bench._agree_or_default({'rccl': False, 'xgmi': True}, 0, 2)
+    assert got['rccl'] is True and got['xgmi'] is False and 'store unreachable' in got['agreement']
 
 
 _AGREE = r'''
@@ -93,3 +117,18 @@ def test_agreement_is_the_and_over_ranks():
     assert all(p.returncode == 0 for p in procs), outs
     for o in outs:
         assert json.loads(o.strip().splitlines()[-1]) == {'rccl': False, 'xgmi': True}
+
+
+def test_headline_hang_still_leaves_a_line():
+    """N > 1: the watchdog starts before the headline; a line built from the preflights alone has value null."""
+    import bench
+    line = bench._Line(0)
+    line.fields = {'metric': 'm', 'value': None, 'launch': {}}
+    line.leg = 'headline'
+    import io
+    import contextlib
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        line.emit(incomplete='hard deadline hit during leg "headline"')
+    d = json.loads(buf.getvalue())
+    assert d['value'] is None and 'headline' in d['incomplete']

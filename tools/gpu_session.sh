@@ -16,15 +16,16 @@ run() {   # run <name> <timeout> <cmd...>
     if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after rc=$rc"; exit $rc; fi
     return 0
 }
-# Round-5 steps, each mapped to the verdict item it serves (VERDICT.md "Next round: do this"):
-#   tests / smoke            items 1, 3, 4: the GPU suite (weighted EP > 1 tolerance, masked full-size C3,
-#                            local bypass, the cut library) and the driver's smoke
-#   bench8gloo               item 2: the driver's N = 8 command, self-launched, 8 gloo ranks on one GPU
-#   bench2gloo / bench4gloo  item 3: phases.exchange_ms with the local bypass in a rehearsal line
-#   pmcstep                  item 3: PMC of the whole EP = 8 step (phase A + exchange + phase B) with and
-#                            without the local bypass (tools/pmc_ep.py, summarize_prof.py step)
-#   pmc / pmcfold / pmcep    item 6: same-build traffic for the final bench lines (N = 1 and N > 1)
-#   benchjson / profdefault  item 6: one bench line of the final build and the driver's command under rocprofv3
+# Round-6 steps, each mapped to the verdict item it serves (VERDICT.md "Next round: do this"):
+#   ldsdma / ldsdmaprof      item 1: the LDS-DMA load-path experiment (timing, rocprof, PMC, both layouts); removed
+#                            with the variant after the negative (results: profiles/r06a_ldsdma*, CHANGELOG round 6)
+#   bench2def / bench8def    item 2: the driver's default N > 1 command on this one GPU: the RCCL preflight fails
+#                            (duplicate GPU), the ranks agree, the headline falls back to xGMI, the line is complete
+#   barrier                  item 3: the barrier tests' device-clock ordering evidence
+#   pmcep (+ stepfold)       item 5: same-build step PMC per transport -> phases.hbm_bytes_per_rank
+#   bench8gloo               item 5: the N = 8 gloo rehearsal line carrying phases.hbm_bytes_per_rank
+#   tests / smoke / pmc / pmcfold / benchjson / profdefault
+#                            item 6: the final build's suite, smoke, bench line, same-build PMC and rocprof
 for step in "$@"; do
     case $step in
         tests)  run pytest_gpu 1100 python -u -m pytest tests -m gpu -x -q --timeout 170 --timeout-method thread ;;
@@ -75,6 +76,11 @@ for step in "$@"; do
                     run pmcnbfold$n 120 python tools/summarize_prof.py step $OUT/pmc_step_ep${n}_nobypass.json $OUT/pmc_ep${n}_nobypass_meta.json \
                         $(find $OUT/pmcnb${n}_FETCH_SIZE $OUT/pmcnb${n}_WRITE_SIZE -name '*counter_collection.csv')
                 done ;;
+        barrier) run barrier 300 python -u -m pytest tests/test_barrier_gpu.py -x -v --timeout 150 --timeout-method thread ;;
+        bench2def) run bench2def 420 python3 bench.py --gpus 2 --steps 10 --warmup 3
+                grep '^{' $OUT/bench2def.log | tail -1 > $OUT/bench2def.json || true ;;
+        bench8def) run bench8def 700 python3 bench.py --gpus 8 --steps 20 --warmup 5
+                grep '^{' $OUT/bench8def.log | tail -1 > $OUT/bench8def.json || true ;;
         cumask) run cumask 120 python tools/probe_cumask.py ;;
         kdisp)  run kdisp 300 python tools/kdispatch.py ;;
         khost)  run khost 300 python tools/khost.py ;;

@@ -1332,8 +1332,7 @@ def main():
         legs = [(headline['label'], value)]
         if rccl_budget is not None and rccl_budget['bitwise_equal']:
             legs.append((f'rccl, DEEPEP_PHASE_A_CUS={rccl_budget["phase_a_cus"]}', rccl_budget['value']))
-        if xgmi is not None and 'value' in xgmi and xgmi['bitwise_equal_to_rccl'] and not xgmi['barrier_timeout'] \
-                and headline['label'] == 'rccl':
+        if xgmi is not None and 'value' in xgmi and xgmi['bitwise_equal_to_rccl'] and not xgmi['barrier_timeout']:
             legs.append(('xgmi', xgmi['value']))
             xb_ = xgmi.get('phase_a_budget')
             if xb_ and xb_['bitwise_equal_to_rccl'] and not xb_['barrier_timeout']:

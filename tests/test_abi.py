@@ -154,3 +154,17 @@ def test_reference_version_and_alias():
     assert deep_ep.ElasticBuffer is deepep_amd.ElasticBuffer
     assert deep_ep.EPHandle is deepep_amd.EPHandle
     assert deepep_amd.__build_version__ != deep_ep.__version__
+
+
+def test_reference_submodule_import_paths():
+    """The reference's own import paths for the combine path's Python surface resolve to this build's
+    objects (deep_ep/buffers/elastic.py, deep_ep/utils/event.py, deep_ep/utils/envs.py)."""
+    import deepep_amd
+    from deep_ep.buffers.elastic import ElasticBuffer, EPHandle
+    from deep_ep.utils.envs import check_torch_deterministic, get_logical_domain_size, get_physical_domain_size
+    from deep_ep.utils.event import EventHandle, EventOverlap
+    assert ElasticBuffer is deepep_amd.ElasticBuffer and EPHandle is deepep_amd.EPHandle
+    assert EventOverlap is deepep_amd.EventOverlap and EventHandle is deepep_amd.EventHandle
+    assert get_physical_domain_size is deepep_amd.get_physical_domain_size
+    assert get_logical_domain_size is deepep_amd.get_logical_domain_size
+    assert callable(check_torch_deterministic)

@@ -132,3 +132,25 @@ def test_headline_hang_still_leaves_a_line():
         line.emit(incomplete='hard deadline hit during leg "headline"')
     d = json.loads(buf.getvalue())
     assert d['value'] is None and 'headline' in d['incomplete']
+
+
+def test_a_hanging_preflight_child_is_killed_and_reported(tmp_path, monkeypatch):
+    """A preflight child that never finishes (a hung collective) is killed at the limit: ok=False with
+    the reason, no exception, and the bench goes on."""
+    import bench
+    script = tmp_path / 'hang.py'
+    script.write_text('import time\ntime.sleep(600)\n')
+    monkeypatch.setattr(bench, 'ROOT', str(tmp_path))
+    c = bench._start_child('hang.py', 1)
+    res = bench._finish_child(c, limit=2.0)
+    assert res['ok'] is False and 'timed out' in res['error']
+    assert c['proc'].poll() is not None                   # the child is gone
+
+
+def test_a_crashing_preflight_child_reports_its_last_stderr_line(tmp_path, monkeypatch):
+    import bench
+    script = tmp_path / 'crash.py'
+    script.write_text('import sys\nprint("diagnostic", file=sys.stderr)\nraise SystemExit(7)\n')
+    monkeypatch.setattr(bench, 'ROOT', str(tmp_path))
+    res = bench._finish_child(bench._start_child('crash.py', 2), limit=60.0)
+    assert res == {'exit_status': 7, 'ok': False, 'error': 'diagnostic'}

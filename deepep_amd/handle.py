@@ -277,8 +277,11 @@ class EPHandle:
         self._bypass = False                                  # rows laid out for the dispatch's local bypass
         self._combine_plans = {}
 
-    def deterministic_sort(self, *args, **kwargs) -> None:
-        """The dispatch of this build is deterministic by construction (received tokens sorted by
-        source global index, expanded rows by (expert, source index)), which is the order the
-        reference's deterministic_sort produces (elastic.py:100-192); nothing to do."""
+    def deterministic_sort(self, do_cpu_sync: bool, is_cached_dispatch: bool, recv_x: torch.Tensor,
+                           recv_sf: Optional[torch.Tensor], recv_topk_idx: torch.Tensor,
+                           recv_topk_weights: torch.Tensor, channel_linked_list: Optional[torch.Tensor]) -> None:
+        """The reference's signature (elastic.py:100-107).  The dispatch of this build is deterministic by
+        construction (received tokens sorted by source global index, expanded rows by (expert, source index)),
+        which is the order the reference's in-place permutation produces (elastic.py:108-192): the permutation
+        is the identity, so nothing moves."""
         return None

@@ -213,12 +213,14 @@ def _finish_child(c, limit: float = PREFLIGHT_LIMIT_S) -> dict:
     if rc is None:
         p.kill()
         p.wait()
-        c['out'].close(), c['err'].close()
+        c['out'].close()
+        c['err'].close()
         return dict(ok=False, error=f'preflight timed out ({limit:.0f} s)', seconds=round(time.perf_counter() - c['t0'], 1))
     c['out'].seek(0)
     c['err'].seek(0)
     stdout, stderr = c['out'].read(), c['err'].read()
-    c['out'].close(), c['err'].close()
+    c['out'].close()
+    c['err'].close()
     lines = [ln for ln in stdout.splitlines() if ln.startswith('{')]
     try:
         res = json.loads(lines[-1]) if lines else {}

@@ -14,7 +14,8 @@ T, H, K, E = 16, 64, 4, 8
 @pytest.fixture(scope='module')
 def setup():
     os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
-    if not dist.is_initialized():
+    created = not dist.is_initialized()
+    if created:
         import socket
         with socket.socket() as s:
             s.bind(('127.0.0.1', 0))
@@ -32,6 +33,8 @@ def setup():
     rx, _, rw, h, _ = buf.dispatch(x, topk_idx=idx, topk_weights=w, num_experts=E)
     yield dict(buf=buf, ex_x=ex_x, ex_w=ex_w, ex_h=ex_h, rx=rx, rw=rw, h=h)
     buf.destroy()
+    if created:
+        dist.destroy_process_group()
 
 
 def _raises(fn, text):

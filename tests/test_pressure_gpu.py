@@ -83,3 +83,79 @@ def test_pressure_one_buffer(group):
         bad += _one_seed(buf, seed)
     buf.destroy()
     assert not bad, bad
+
+
+def _xgmi_pressure_worker(rank, world, port, queue):
+    import sys
+    import traceback
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    try:
+        os.environ['MASTER_ADDR'] = '127.0.0.1'
+        os.environ['MASTER_PORT'] = str(port)
+        import torch.distributed as dist
+        torch.cuda.set_device(0)
+        dist.init_process_group('gloo', rank=rank, world_size=world)
+        from deepep_amd import ElasticBuffer
+        Tx, Hx, Kx, Ex = 256, 1024, 4, 8 * world
+        ref = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=Tx, hidden=Hx, num_topk=Kx, explicitly_destroy=True)
+        ref.transport = 'rccl'                          # the exchange through gloo: the reference result
+        bad, base = [], None
+        for it in range(6):
+            g = torch.Generator(device='cuda').manual_seed(100 * it + rank)
+            idx = torch.topk(torch.rand((Tx, Ex), device='cuda', generator=g), Kx, dim=-1, sorted=False)[1]
+            w = torch.rand((Tx, Kx), device='cuda', generator=g)
+            x = torch.randn((Tx, Hx), device='cuda', generator=g).to(torch.bfloat16)
+            buf = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=Tx, hidden=Hx, num_topk=Kx,
+                                explicitly_destroy=True, num_gpu_timeout_secs=20)
+            buf.transport = 'xgmi'                      # a new window every iteration (IPC export / import)
+            outs = []
+            for b in (buf, ref):
+                _, _, ex_w, h, _ = b.dispatch(x, topk_idx=idx, topk_weights=w, num_experts=Ex, do_expand=True)
+                y = torch.randn((h.num_expanded_tokens, Hx), device='cuda',
+                                generator=torch.Generator(device='cuda').manual_seed(7 + it + rank)).to(torch.bfloat16)
+                outs.append(b.combine(y, h, topk_weights=ex_w, apply_topk_weights=True)[:2])
+            torch.cuda.synchronize()
+            if not (torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])):
+                bad.append(f'iteration {it}: xgmi != gloo exchange')
+            buf._sym.check()
+            buf.destroy()
+            del buf, outs, h, y, ex_w
+            gc.collect()
+            torch.cuda.synchronize()
+            if base is None:
+                base = torch.cuda.memory_allocated()
+            elif torch.cuda.memory_allocated() != base:
+                bad.append(f'iteration {it}: {torch.cuda.memory_allocated() - base} bytes more allocated')
+        ref.destroy()
+        queue.put((rank, bad))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:
+        queue.put((rank, [traceback.format_exc()]))
+
+
+def test_pressure_xgmi_windows_recreated():
+    """Six iterations, 2 processes sharing the GPU: each creates an xGMI buffer (a new HIP-IPC window, exported
+    and imported), dispatches and combines bitwise equal to the same calls through gloo, destroys it; the
+    allocated bytes come back every time (windows and imports released)."""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context('spawn')
+    queue = ctx.Queue()
+    procs = [ctx.Process(target=_xgmi_pressure_worker, args=(r, 2, port, queue)) for r in range(2)]
+    for p in procs:
+        p.start()
+    results = {}
+    try:
+        for _ in range(2):
+            rank, bad = queue.get(timeout=140)
+            results[rank] = bad
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    assert len(results) == 2 and not any(results.values()), results

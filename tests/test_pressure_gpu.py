@@ -118,14 +118,24 @@ def _xgmi_pressure_worker(rank, world, port, queue):
             if not (torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])):
                 bad.append(f'iteration {it}: xgmi != gloo exchange')
             buf._sym.check()
+            window_bytes = buf._sym.data_bytes
             buf.destroy()
             del buf, outs, h, y, ex_w
             gc.collect()
             torch.cuda.synchronize()
+            dist.barrier()                              # both processes quiescent: device free memory is stable
+            free = torch.cuda.mem_get_info()[0]
+            dist.barrier()
             if base is None:
-                base = torch.cuda.memory_allocated()
-            elif torch.cuda.memory_allocated() != base:
-                bad.append(f'iteration {it}: {torch.cuda.memory_allocated() - base} bytes more allocated')
+                base = (torch.cuda.memory_allocated(), free)
+            else:
+                if torch.cuda.memory_allocated() != base[0]:
+                    bad.append(f'iteration {it}: {torch.cuda.memory_allocated() - base[0]} bytes more allocated')
+                # the windows live outside torch's allocator: a window (or an import of the peer's) kept per
+                # iteration would take the device's free memory down by a window each time
+                if base[1] - free > window_bytes // 2:
+                    bad.append(f'iteration {it}: device free memory down {base[1] - free} bytes '
+                               f'(window {window_bytes} bytes)')
         ref.destroy()
         queue.put((rank, bad))
         dist.barrier()
@@ -136,8 +146,8 @@ def _xgmi_pressure_worker(rank, world, port, queue):
 
 def test_pressure_xgmi_windows_recreated():
     """Six iterations, 2 processes sharing the GPU: each creates an xGMI buffer (a new HIP-IPC window, exported
-    and imported), dispatches and combines bitwise equal to the same calls through gloo, destroys it; the
-    allocated bytes come back every time (windows and imports released)."""
+    and imported), dispatches and combines bitwise equal to the same calls through gloo, destroys it; torch's
+    allocated bytes and the device's free memory come back every time (windows and imports released)."""
     import socket
     import torch.multiprocessing as mp
     with socket.socket() as s:

@@ -5,6 +5,9 @@ own C-ABI (deepep_sym_alloc / _export / _import / _close / _free), per iteration
   python tools/probe_ipc_leak.py alloc      alloc + free
   python tools/probe_ipc_leak.py export     alloc + hipIpcGetMemHandle + free
   python tools/probe_ipc_leak.py reexport   one allocation, exported again every iteration
+  python tools/probe_ipc_leak.py streams    a new torch.cuda.Stream() per iteration, used once (torch's stream pool
+                                            creates its HIP streams lazily: each new one takes runtime resources)
+  python tools/probe_ipc_leak.py buffers    a new ElasticBuffer per iteration (one rank), combine, destroy
   python tools/probe_ipc_leak.py pair       2 processes (gloo): alloc, export, exchange, import the peer's,
                                             close, free
   python tools/probe_ipc_leak.py pairpool   the same with ONE allocation per process kept across iterations
@@ -36,7 +39,32 @@ def single(mode):
     keep = ctypes.c_void_p()
     if mode == 'reexport':
         assert lib.deepep_sym_alloc(BYTES, ctypes.byref(keep)) == 0
-    for _ in range(N_ITER):
+    streams = []
+    for i in range(N_ITER):
+        if mode == 'streams':
+            st = torch.cuda.Stream()
+            with torch.cuda.stream(st):
+                torch.zeros(1, device='cuda').add_(1)
+            streams.append(st)
+            frees.append(_free())
+            continue
+        if mode == 'buffers':
+            import torch.distributed as dist
+            if not dist.is_initialized():
+                os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+                os.environ.setdefault('MASTER_PORT', '29571')
+                dist.init_process_group('gloo', rank=0, world_size=1)
+            from deepep_amd import ElasticBuffer
+            b = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=64, hidden=256, num_topk=2,
+                              explicitly_destroy=True)
+            idx = torch.topk(torch.rand((64, 8), device='cuda'), 2, dim=-1)[1]
+            ex, _, _, h, _ = b.dispatch(torch.randn((64, 256), device='cuda').to(torch.bfloat16), topk_idx=idx,
+                                        num_experts=8, do_expand=True)
+            b.combine(ex, h)
+            b.destroy()
+            del b, ex, h
+            frees.append(_free() + torch.cuda.memory_reserved())
+            continue
         if mode == 'reexport':
             h = ctypes.create_string_buffer(64)
             assert lib.deepep_sym_export(keep, h) == 0

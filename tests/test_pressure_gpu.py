@@ -96,6 +96,14 @@ def _xgmi_pressure_worker(rank, world, port, queue):
         torch.cuda.set_device(0)
         dist.init_process_group('gloo', rank=rank, world_size=world)
         from deepep_amd import ElasticBuffer
+        # torch hands out its pooled streams round robin and the HIP runtime sets each one up on first use
+        # (about 2-4 MiB of device memory per stream, tools/probe_ipc_leak.py `streams`); every buffer takes
+        # two of them, so the pool is used once up front and later iterations measure only what they keep
+        for _ in range(64):
+            st = torch.cuda.Stream()
+            with torch.cuda.stream(st):
+                torch.zeros(1, device='cuda').add_(1)
+        torch.cuda.synchronize()
         Tx, Hx, Kx, Ex = 256, 1024, 4, 8 * world
         ref = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=Tx, hidden=Hx, num_topk=Kx, explicitly_destroy=True)
         ref.transport = 'rccl'                          # the exchange through gloo: the reference result

@@ -98,11 +98,13 @@ def _xgmi_pressure_worker(rank, world, port, queue):
         from deepep_amd import ElasticBuffer
         # torch hands out its pooled streams round robin and the HIP runtime sets each one up on first use
         # (about 2-4 MiB of device memory per stream, tools/probe_ipc_leak.py `streams`); every buffer takes
-        # two of them, so the pool is used once up front and later iterations measure only what they keep
-        for _ in range(64):
-            st = torch.cuda.Stream()
-            with torch.cuda.stream(st):
-                torch.zeros(1, device='cuda').add_(1)
+        # two of them and every gloo collective on device tensors one of the high-priority pool, so both pools
+        # are used once up front and later iterations measure only what they keep
+        for priority in (0, -1):
+            for _ in range(64):
+                st = torch.cuda.Stream(priority=priority)
+                with torch.cuda.stream(st):
+                    torch.zeros(1, device='cuda').add_(1)
         torch.cuda.synchronize()
         Tx, Hx, Kx, Ex = 256, 1024, 4, 8 * world
         ref = ElasticBuffer(dist.group.WORLD, num_max_tokens_per_rank=Tx, hidden=Hx, num_topk=Kx, explicitly_destroy=True)
